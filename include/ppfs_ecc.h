@@ -1,0 +1,138 @@
+/*
+ * ppfs_ecc.h -- C ABI of the MI355X (gfx950) per-block ECC engine.
+ *
+ * This is the drop-in boundary underneath PPFS's IBlockDevice layer
+ * (reference: lib/blockdevice/include/ppfs/blockdevice/iblock_device.hpp:34-97).
+ * Each entry point replaces the per-block arithmetic of one reference codec with a batch
+ * of blocks processed by hand-written HIP kernels:
+ *
+ *   ppfs_ecc_encode  <- ReedSolomonBlockDevice::_encodeBlock   rs_block_device.cpp:95-117
+ *                       CrcBlockDevice::_calculateAndWrite     crc_block_device.cpp:37-67
+ *                       HammingBlockDevice::_encodeData        hamming_block_device.cpp:76-109
+ *                       ParityBlockDevice::writeBlock (parity) parity_block_device.cpp:49-54
+ *   ppfs_ecc_decode  <- ReedSolomonBlockDevice::_fixBlockAndExtract  rs_block_device.cpp:119-183
+ *                       CrcBlockDevice::_readAndCheckRaw             crc_block_device.cpp:12-35
+ *                       HammingBlockDevice::_readAndFixBlock/_extractData hamming_block_device.cpp:21-74
+ *                       ParityBlockDevice::_checkParity              parity_block_device.cpp:90-97
+ *   ppfs_ecc_write   <- IBlockDevice::writeBlock of a full payload at offset 0
+ *                       (read-modify-write: check/fix the old block, then encode)
+ *   ppfs_ecc_create  <- PpFS::_createAppropriateBlockDevice   lib/filesystem/src/ppfs.cpp:35-70
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; no exceptions cross the ABI.  Return 0 on success or a
+ *     negative errno-style code.
+ *   - Blocks are packed: raw block i at raw + i*raw_block_size, payload i at
+ *     data + i*data_size (the on-disk image layout: IDisk address = index * rawBlockSize()).
+ *   - *_device functions take device pointers and a hipStream_t passed as void* (NULL =
+ *     the null stream); they enqueue work and return without synchronising.
+ *   - *_host functions take host pointers, stage through pinned buffers with overlapped
+ *     H2D / kernel / D2H, and return after the results are in host memory.
+ *   - Per-block status bytes use FsError values (lib/common/include/ppfs/common/types.hpp):
+ *       PPFS_ECC_OK (0), PPFS_ECC_CORRECTED (1: the reference writes the block back and logs
+ *       an ErrorCorrectionEvent), PPFS_ECC_CORRECTION_ERROR (5 = BlockDevice_CorrectionError).
+ *   - One context per (host thread, GPU); a context is not internally locked.
+ */
+#ifndef PPFS_ECC_H
+#define PPFS_ECC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ECCType (lib/blockdevice/include/ppfs/blockdevice/ecc_type.hpp:8-14) */
+enum ppfs_ecc_type {
+    PPFS_ECC_NONE = 0,
+    PPFS_ECC_CRC = 1,
+    PPFS_ECC_HAMMING = 2,
+    PPFS_ECC_PARITY = 3,
+    PPFS_ECC_REED_SOLOMON = 4
+};
+
+enum ppfs_ecc_status {
+    PPFS_ECC_OK = 0,
+    PPFS_ECC_CORRECTED = 1,
+    PPFS_ECC_CORRECTION_ERROR = 5
+};
+
+/* Error codes returned by the entry points. */
+#define PPFS_ECC_EINVAL (-22)
+#define PPFS_ECC_ENOMEM (-12)
+#define PPFS_ECC_EHIP (-5)
+#define PPFS_ECC_ENOTSUP (-95)
+
+/* Parameters persisted in the SuperBlock (super_block.hpp:20-23) / FsConfig (types.hpp:47-70). */
+typedef struct ppfs_ecc_params {
+    uint32_t ecc_type;             /* enum ppfs_ecc_type */
+    uint32_t block_size;           /* FS block size in bytes (<= 4096, MAX_BLOCK_SIZE) */
+    uint32_t rs_correctable_bytes; /* Reed-Solomon t (clamped to min(block,255)/2 like the reference) */
+    uint32_t reserved;
+    uint64_t crc_polynomial;       /* CRC polynomial in EXPLICIT form (CrcPolynomial::MsgExplicit) */
+} ppfs_ecc_params;
+
+typedef struct ppfs_ecc_ctx ppfs_ecc_ctx;
+
+/* Convert a config-file ("implicit +1") CRC polynomial to the explicit form:
+ * CrcPolynomial::MsgImplicit, crc_polynomial.cpp:41-54.  */
+uint64_t ppfs_ecc_crc_implicit_to_explicit(uint64_t implicit_poly);
+
+/* Create a codec context on HIP device `device`.  Validates params with the reference's
+ * clamping rules; builds and uploads the codec tables.  */
+int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_ecc_ctx** out);
+void ppfs_ecc_destroy(ppfs_ecc_ctx* ctx);
+
+/* IBlockDevice::rawBlockSize() / dataSize() of the equivalent reference device. */
+size_t ppfs_ecc_raw_block_size(const ppfs_ecc_ctx* ctx);
+size_t ppfs_ecc_data_size(const ppfs_ecc_ctx* ctx);
+
+/* Short human-readable name of the kernel path the context dispatches to (for logs/tests). */
+const char* ppfs_ecc_kernel_name(const ppfs_ecc_ctx* ctx);
+
+/*
+ * Encode nblocks full payloads.  raw is read-modify-write: bits the codec does not define
+ * (CRC unused tail bits when degree % 8 != 0, Hamming bits after the last data bit) keep
+ * raw's previous contents exactly as the reference's writeBlock keeps the old block's.
+ */
+int ppfs_ecc_encode_device(ppfs_ecc_ctx* ctx, const uint8_t* d_data, uint8_t* d_raw, size_t nblocks,
+    void* stream);
+
+/*
+ * Decode / check nblocks raw blocks.
+ *   d_data    (may be NULL) receives the payloads (undefined for blocks with status 5).
+ *   d_status  (may be NULL) receives one status byte per block.
+ *   write_back != 0 applies the reference's write-back to d_raw in place (RS: the corrected
+ *             bytes of the codeword; Hamming: the one flipped byte).
+ *   d_spill   (RS only, may be NULL; meaningful only when rawBlockSize() < 255): per block
+ *             (256 - rawBlockSize()) bytes: [0] = bytes the reference's write-back writes
+ *             past the end of the block, [1..] = those bytes.  Blocks are decoded
+ *             independently; a spill is reported, never applied to the neighbouring block.
+ */
+int ppfs_ecc_decode_device(ppfs_ecc_ctx* ctx, uint8_t* d_raw, uint8_t* d_data, uint8_t* d_status,
+    size_t nblocks, int write_back, uint8_t* d_spill, void* stream);
+
+/*
+ * writeBlock(full payload, {i, 0}) for nblocks blocks: check/fix the old block held in
+ * d_raw, then encode d_data into it.  d_status (may be NULL): 0, 1 (old block corrected and
+ * logged), 5 (old block failed its check: the reference returns CorrectionError and leaves
+ * the block untouched -- CRC, parity, uncorrectable Hamming).
+ */
+int ppfs_ecc_write_device(ppfs_ecc_ctx* ctx, const uint8_t* d_data, uint8_t* d_raw, uint8_t* d_status,
+    size_t nblocks, void* stream);
+
+/* Host-memory variants (pinned staging, chunked, H2D/kernel/D2H overlapped). */
+int ppfs_ecc_encode_host(ppfs_ecc_ctx* ctx, const uint8_t* data, uint8_t* raw, size_t nblocks);
+int ppfs_ecc_decode_host(ppfs_ecc_ctx* ctx, uint8_t* raw, uint8_t* data, uint8_t* status, size_t nblocks,
+    int write_back, uint8_t* spill);
+int ppfs_ecc_write_host(ppfs_ecc_ctx* ctx, const uint8_t* data, uint8_t* raw, uint8_t* status,
+    size_t nblocks);
+
+/* Last HIP error string recorded by this thread (diagnostics). */
+const char* ppfs_ecc_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PPFS_ECC_H */

@@ -1,0 +1,1099 @@
+/*
+ * ppfs_oracle.c -- TEST INFRASTRUCTURE ONLY (the checker, never the product).
+ *
+ * A plain-C restatement of the ParityPartyFS (PPFS) per-block ECC maths and of the
+ * IBlockDevice read/write/format semantics that sit on top of it.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library.
+ * The product path (paritypartyfs_amd/csrc) never links or calls it.
+ *
+ * Every function cites the reference file:line it restates (paths relative to the
+ * reference repository root, lib/...).  The reference itself cannot be compiled in this
+ * image (it needs C++23 <expected>, absent from libstdc++ 11 and there are no libc++
+ * headers), so this restatement is pinned by:
+ *   - the reference's own known-answer tests (unit_tests/test_crc_block_device.cpp:39-71,
+ *     unit_tests/test_bits.cpp:5-34) and round-trip tests (test_rs/crc/hamming/parity),
+ *   - known-answer vectors recorded from a reference build in SURVEY.md section 8(a)
+ *     (tests/golden/reference_kats.json).
+ *
+ * Semantics that matter for bit-exactness and are reproduced on purpose:
+ *   - GF(2^8) over 0x11D, alpha = 2, a/0 = 0, inv(0) = 0           (gf256.cpp:6-81)
+ *   - RS codeword byte i = coefficient of x^i, parity in [0,2t)    (rs_block_device.cpp:95-117)
+ *   - RS decode never fails; roots are searched over all 255 field values and every
+ *     root is applied, even when #roots != deg(sigma)               (rs_block_device.cpp:119-183,271-280)
+ *   - RS write-back writes code_word.size() bytes (may exceed n for shortened codes)
+ *   - CRC division stops one step early                             (crc_polynomial.cpp:63)
+ *   - Hamming MSB-first bit numbering, unused tail bits untouched   (hamming_block_device.cpp:76-109)
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define EXPORT __attribute__((visibility("default")))
+
+/* FsError values (lib/common/include/ppfs/common/types.hpp:11-80). */
+enum {
+    FS_OK = 0,
+    FS_CORRECTED = 1, /* oracle-internal: decode succeeded after a write-back */
+    FS_BLOCKDEVICE_CORRECTION_ERROR = 5,
+    FS_DISK_OUT_OF_BOUNDS = 9,
+    FS_DISK_INVALID_REQUEST = 10,
+    FS_UNDEFINED = 255 /* the reference's behaviour is undefined for this input */
+};
+
+/* ------------------------------------------------------------------------------------ */
+/* GF(2^8)  -- lib/ecc_helpers/src/gf256.cpp:6-83                                        */
+/* ------------------------------------------------------------------------------------ */
+static uint8_t EXP[256], LOG[256];
+static int gf_ready;
+
+static void gf_init(void)
+{
+    if (gf_ready)
+        return;
+    unsigned x = 1;
+    for (int i = 0; i < 255; ++i) { /* gf256.cpp:9-15 */
+        EXP[i] = (uint8_t)x;
+        x <<= 1;
+        if (x & 0x100)
+            x ^= 0x11D;
+    }
+    EXP[255] = EXP[0]; /* gf256.cpp:16 */
+    memset(LOG, 0, sizeof LOG);
+    for (int i = 0; i < 255; ++i) /* gf256.cpp:20-26, LOG[0] stays 0 */
+        LOG[EXP[i]] = (uint8_t)i;
+    gf_ready = 1;
+}
+
+static inline uint8_t gf_mul(uint8_t a, uint8_t b) /* gf256.cpp:46-54 */
+{
+    if (!a || !b)
+        return 0;
+    unsigned s = (unsigned)LOG[a] + LOG[b];
+    if (s >= 255)
+        s -= 255;
+    return EXP[s];
+}
+
+static inline uint8_t gf_div(uint8_t a, uint8_t b) /* gf256.cpp:56-64: a/0 == 0 */
+{
+    if (!a || !b)
+        return 0;
+    int d = (int)LOG[a] - (int)LOG[b];
+    if (d < 0)
+        d += 255;
+    return EXP[d];
+}
+
+static inline uint8_t gf_inv(uint8_t a) /* gf256.cpp:76-81 */
+{
+    if (!a)
+        return 0;
+    return EXP[255 - LOG[a]];
+}
+
+EXPORT void oracle_gf_tables(uint8_t* exp_out, uint8_t* log_out)
+{
+    gf_init();
+    memcpy(exp_out, EXP, 256);
+    memcpy(log_out, LOG, 256);
+}
+
+EXPORT uint8_t oracle_gf_mul(uint8_t a, uint8_t b) { gf_init(); return gf_mul(a, b); }
+EXPORT uint8_t oracle_gf_div(uint8_t a, uint8_t b) { gf_init(); return gf_div(a, b); }
+EXPORT uint8_t oracle_gf_inv(uint8_t a) { gf_init(); return gf_inv(a); }
+
+/* ------------------------------------------------------------------------------------ */
+/* PolynomialGF256 -- lib/ecc_helpers/src/polynomial_gf256.cpp                           */
+/* Fixed 256-entry coefficient array, low degree first, size trimmed of high zeros.      */
+/* Operations that the reference would run past its 256-entry buffer set poly_ub.        */
+/* ------------------------------------------------------------------------------------ */
+#define PMAX 256
+typedef struct {
+    uint8_t c[PMAX];
+    int size;
+} poly;
+
+static int poly_ub; /* set when the reference would overflow its fixed buffers (UB) */
+
+static void poly_trim(poly* p) /* polynomial_gf256.cpp:18-22 */
+{
+    while (p->size > 0 && p->c[p->size - 1] == 0)
+        p->size--;
+}
+
+static void poly_from(poly* p, const uint8_t* v, int n) /* :4-9 (static_vector clamps size) */
+{
+    if (n > PMAX) {
+        poly_ub = 1;
+        n = PMAX;
+    }
+    memcpy(p->c, v, (size_t)n);
+    p->size = n;
+    poly_trim(p);
+}
+
+static void poly_add(poly* r, const poly* a, const poly* b) /* :24-38 */
+{
+    int n = a->size > b->size ? a->size : b->size;
+    poly t;
+    for (int i = 0; i < n; ++i)
+        t.c[i] = (uint8_t)((i < a->size ? a->c[i] : 0) ^ (i < b->size ? b->c[i] : 0));
+    t.size = n;
+    poly_trim(&t);
+    *r = t;
+}
+
+static void poly_mul(poly* r, const poly* a, const poly* b) /* :46-65 */
+{
+    if (a->size == 0 || b->size == 0) {
+        r->size = 0;
+        return;
+    }
+    int rs = a->size + b->size - 1;
+    if (rs > PMAX) {
+        poly_ub = 1; /* reference writes past its 256-entry result buffer */
+        rs = PMAX;
+    }
+    poly t;
+    memset(t.c, 0, (size_t)rs);
+    for (int i = 0; i < a->size; ++i)
+        for (int j = 0; j < b->size; ++j)
+            if (i + j < rs)
+                t.c[i + j] ^= gf_mul(a->c[i], b->c[j]);
+    t.size = rs;
+    poly_trim(&t);
+    *r = t;
+}
+
+static void poly_xk(poly* r, const poly* p, int k) /* multiply_by_xk :90-99 */
+{
+    int rs = k + p->size;
+    if (rs > PMAX) {
+        poly_ub = 1;
+        rs = PMAX;
+    }
+    poly t;
+    memset(t.c, 0, (size_t)rs);
+    for (int i = 0; i < p->size && k + i < rs; ++i)
+        t.c[k + i] = p->c[i];
+    t.size = rs;
+    poly_trim(&t);
+    *r = t;
+}
+
+static void poly_mod(poly* r, const poly* p, const poly* d) /* :101-127 schoolbook */
+{
+    if (d->size == 0) {
+        *r = *p;
+        return;
+    }
+    poly rem = *p;
+    uint8_t lead = d->c[d->size - 1];
+    while (rem.size >= d->size) {
+        int shift = rem.size - d->size;
+        uint8_t factor = gf_div(rem.c[rem.size - 1], lead);
+        for (int i = 0; i < d->size; ++i)
+            rem.c[shift + i] ^= gf_mul(d->c[i], factor);
+        poly_trim(&rem);
+    }
+    *r = rem;
+}
+
+static uint8_t poly_eval(const poly* p, uint8_t x) /* evaluate :129-138 (power-sum Horner) */
+{
+    uint8_t result = 0, power = 1;
+    for (int i = 0; i < p->size; ++i) {
+        result = (uint8_t)(gf_mul(p->c[i], power) ^ result);
+        power = gf_mul(x, power);
+    }
+    return result;
+}
+
+static void poly_deriv(poly* r, const poly* p) /* derivative :189-200 */
+{
+    int ds = p->size > 0 ? p->size - 1 : 0;
+    poly t;
+    for (int i = 1; i < p->size; ++i)
+        t.c[i - 1] = (i % 2) ? p->c[i] : 0;
+    t.size = ds;
+    poly_trim(&t);
+    *r = t;
+}
+
+static uint8_t* poly_at(poly* p, int i) /* non-const operator[] :80-88 zero-extends */
+{
+    if (i >= PMAX) {
+        poly_ub = 1;
+        i = PMAX - 1;
+    }
+    if (i >= p->size) {
+        for (int j = p->size; j <= i; ++j)
+            p->c[j] = 0;
+        p->size = i + 1;
+    }
+    return &p->c[i];
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Reed-Solomon -- lib/blockdevice/src/rs_block_device.cpp                               */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+    int n; /* raw block size = min(block_size, 255)            rs_block_device.cpp:57 */
+    int t; /* correctable bytes = min(t, n/2)                   rs_block_device.cpp:58 */
+    poly gen;
+} rs_code;
+
+static void rs_setup(rs_code* rs, int block_size, int t)
+{
+    gf_init();
+    rs->n = block_size < 255 ? block_size : 255;
+    rs->t = t < rs->n / 2 ? t : rs->n / 2;
+    /* _calculateGenerator :195-208  g = prod_{i=1..2t} (x + alpha^i) */
+    poly g = { { 1 }, 1 };
+    uint8_t power = 2;
+    for (int i = 0; i < 2 * rs->t; ++i) {
+        poly term = { { 0 }, 2 };
+        term.c[0] = power;
+        term.c[1] = 1;
+        poly_mul(&g, &g, &term);
+        power = gf_mul(power, 2);
+    }
+    rs->gen = g;
+}
+
+EXPORT int oracle_rs_sizes(int block_size, int t, int* n_out, int* k_out)
+{
+    rs_code rs;
+    rs_setup(&rs, block_size, t);
+    *n_out = rs.n;
+    *k_out = rs.n - 2 * rs.t;
+    return rs.t;
+}
+
+EXPORT int oracle_rs_generator(int block_size, int t, uint8_t* out)
+{
+    rs_code rs;
+    rs_setup(&rs, block_size, t);
+    memcpy(out, rs.gen.c, (size_t)rs.gen.size);
+    return rs.gen.size;
+}
+
+/* _encodeBlock :95-117: c(x) = m(x) x^2t + (m(x) x^2t mod g), sliced to n bytes. */
+static void rs_encode_one(const rs_code* rs, const uint8_t* data, uint8_t* out)
+{
+    int k = rs->n - 2 * rs->t;
+    poly m, sh, rem, enc;
+    poly_from(&m, data, k);
+    poly_xk(&sh, &m, 2 * rs->t);
+    poly_mod(&rem, &sh, &rs->gen);
+    poly_add(&enc, &sh, &rem);
+    for (int i = 0; i < rs->n; ++i) /* slice(0, n) zero-pads past size */
+        out[i] = i < enc.size ? enc.c[i] : 0;
+}
+
+EXPORT int oracle_rs_encode(int block_size, int t, const uint8_t* data, uint8_t* raw, size_t nblocks)
+{
+    rs_code rs;
+    rs_setup(&rs, block_size, t);
+    int k = rs.n - 2 * rs.t;
+    poly_ub = 0;
+    for (size_t b = 0; b < nblocks; ++b)
+        rs_encode_one(&rs, data + b * (size_t)k, raw + b * (size_t)rs.n);
+    return poly_ub ? -1 : 0;
+}
+
+/* _berlekampMassey :234-269, restated with the same sizes and update order. */
+static void rs_bm(const uint8_t* S, int nsyn, poly* sigma_out)
+{
+    poly sigma = { { 1 }, 1 }, B = { { 1 }, 1 };
+    uint8_t b = 1;
+    int L = 0, m = 1;
+    for (int n = 0; n < nsyn; ++n) {
+        uint8_t d = S[n];
+        for (int i = 1; i <= L; ++i)
+            d ^= gf_mul(*poly_at(&sigma, i), S[n - i]);
+        if (d != 0) {
+            poly T = sigma, diff, scale = { { 0 }, 1 };
+            scale.c[0] = gf_div(d, b);
+            poly_trim(&scale);
+            poly_mul(&diff, &B, &scale);
+            poly_xk(&diff, &diff, m);
+            poly_add(&sigma, &sigma, &diff);
+            if (2 * L <= n) {
+                L = n + 1 - L;
+                B = T;
+                b = d;
+                m = 1;
+            } else {
+                m++;
+            }
+        } else {
+            m++;
+        }
+    }
+    *sigma_out = sigma;
+}
+
+/*
+ * _fixBlockAndExtract :119-183.  Returns FS_OK (clean) or FS_CORRECTED (write-back),
+ * or FS_UNDEFINED when the reference would overflow its fixed buffers.
+ * data_out gets k bytes; fixed_out (>= 256 bytes) gets the written-back bytes and
+ * *wb_len their count (code_word.size() after corrections; 0 when clean).
+ */
+static int rs_decode_one(const rs_code* rs, const uint8_t* raw, uint8_t* data_out, uint8_t* fixed_out,
+    int* wb_len, int* nroots_out)
+{
+    int n = rs->n, t2 = 2 * rs->t, k = n - t2;
+    poly cw;
+    poly_from(&cw, raw, n);
+    uint8_t S[256];
+    int clean = 1;
+    uint8_t power = 2;
+    for (int i = 0; i < t2; ++i) { /* :131-141 */
+        S[i] = poly_eval(&cw, power);
+        if (S[i])
+            clean = 0;
+        power = gf_mul(power, 2);
+    }
+    *wb_len = 0;
+    if (nroots_out)
+        *nroots_out = 0;
+    if (!clean) {
+        poly sigma;
+        rs_bm(S, t2, &sigma);
+        /* _errorLocations :271-280 : every v in 1..255 with sigma(v)==0 */
+        uint8_t X[255];
+        int nr = 0;
+        for (int v = 1; v <= 255; ++v)
+            if (poly_eval(&sigma, (uint8_t)v) == 0)
+                X[nr++] = gf_inv((uint8_t)v);
+        /* _calculateOmega :224-232 */
+        poly Sp, prod, omega;
+        poly_from(&Sp, S, t2);
+        poly_mul(&prod, &Sp, &sigma);
+        uint8_t om[256];
+        for (int i = 0; i < t2; ++i)
+            om[i] = i < prod.size ? prod.c[i] : 0;
+        poly_from(&omega, om, t2);
+        /* _forney :210-222 then correction :165-168 */
+        poly dsig;
+        poly_deriv(&dsig, &sigma);
+        for (int i = 0; i < nr; ++i) {
+            uint8_t xinv = gf_inv(X[i]);
+            uint8_t e = gf_div(poly_eval(&omega, xinv), poly_eval(&dsig, xinv));
+            int pos = LOG[X[i]];
+            uint8_t* c = poly_at(&cw, pos);
+            *c ^= e;
+        }
+        if (nroots_out)
+            *nroots_out = nr;
+        /* write back code_word.slice(0) :175-180 -> size() bytes */
+        *wb_len = cw.size;
+        for (int i = 0; i < cw.size; ++i)
+            fixed_out[i] = cw.c[i];
+    }
+    /* _extractMessage :185-193 : slice(2t, n) zero padded */
+    for (int i = 0; i < k; ++i)
+        data_out[i] = (t2 + i) < cw.size ? cw.c[t2 + i] : 0;
+    return clean ? FS_OK : FS_CORRECTED;
+}
+
+/*
+ * Batch decode.  status[b] = 0 clean / 1 corrected; raw_fixed (may be NULL) receives the
+ * n-byte block as the disk holds it after the write-back (the input when clean);
+ * wb_len (may be NULL) receives the reference's write-back length per block (0 if clean).
+ * Returns -1 if any block hit reference-undefined behaviour.
+ */
+EXPORT int oracle_rs_decode(int block_size, int t, const uint8_t* raw, uint8_t* data, uint8_t* status,
+    uint8_t* raw_fixed, int32_t* wb_len, size_t nblocks)
+{
+    rs_code rs;
+    rs_setup(&rs, block_size, t);
+    int n = rs.n, k = n - 2 * rs.t;
+    poly_ub = 0;
+    uint8_t fixed[PMAX];
+    for (size_t b = 0; b < nblocks; ++b) {
+        int wl = 0;
+        const uint8_t* in = raw + b * (size_t)n;
+        int st = rs_decode_one(&rs, in, data + b * (size_t)k, fixed, &wl, NULL);
+        if (status)
+            status[b] = (uint8_t)st;
+        if (wb_len)
+            wb_len[b] = wl;
+        if (raw_fixed) {
+            uint8_t* o = raw_fixed + b * (size_t)n;
+            memcpy(o, in, (size_t)n);
+            for (int i = 0; i < wl && i < n; ++i)
+                o[i] = fixed[i];
+        }
+    }
+    return poly_ub ? -1 : 0;
+}
+
+/* Full corrected polynomial of one block (for spill checks on shortened codes). */
+EXPORT int oracle_rs_decode_one_full(int block_size, int t, const uint8_t* raw, uint8_t* data, uint8_t* fixed256,
+    int32_t* wb_len, int32_t* nroots)
+{
+    rs_code rs;
+    rs_setup(&rs, block_size, t);
+    poly_ub = 0;
+    int wl = 0, nr = 0;
+    memset(fixed256, 0, 256);
+    int st = rs_decode_one(&rs, raw, data, fixed256, &wl, &nr);
+    *wb_len = wl;
+    *nroots = nr;
+    return poly_ub ? FS_UNDEFINED : st;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* CRC -- lib/ecc_helpers/src/crc_polynomial.cpp, lib/blockdevice/src/crc_block_device.cpp */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+    int n;           /* degree                              crc_polynomial.cpp:7-17 */
+    uint8_t co[65];  /* coefficients MSB first incl. x^n and +1 */
+    uint64_t explicit_poly;
+} crc_poly;
+
+static int bitlen64(uint64_t v)
+{
+    int c = 0;
+    while (v) {
+        v >>= 1;
+        c++;
+    }
+    return c;
+}
+
+static void crc_from_explicit(crc_poly* p, uint64_t P) /* MsgExplicit :27-39 */
+{
+    p->n = bitlen64(P) - 1;
+    p->explicit_poly = P;
+    memset(p->co, 0, sizeof p->co);
+    for (int j = 0; j <= p->n; ++j)
+        p->co[j] = (uint8_t)((P >> (p->n - j)) & 1);
+}
+
+EXPORT uint64_t oracle_crc_implicit_to_explicit(uint64_t p) /* MsgImplicit :41-54 */
+{
+    return (p << 1) + 1;
+}
+
+EXPORT int oracle_crc_degree(uint64_t explicit_poly) { return bitlen64(explicit_poly) - 1; }
+
+/* divide :56-76 -- note the loop bound skips the last reduction step. */
+static void crc_divide(const crc_poly* p, const uint8_t* bits, size_t L, uint8_t* rem)
+{
+    uint8_t* r = (uint8_t*)malloc(L ? L : 1);
+    memcpy(r, bits, L);
+    size_t lim = L - (size_t)(p->n + 1); /* size_t arithmetic exactly as the reference */
+    for (size_t i = 0; i < lim; ++i) {
+        if (!r[i])
+            continue;
+        for (int j = 0; j < p->n + 1; ++j)
+            r[i + j] ^= p->co[j];
+    }
+    for (int i = 0; i < p->n; ++i)
+        rem[i] = r[L - (size_t)p->n + i];
+    free(r);
+}
+
+/* Known-answer hook for CrcPolynomial.division tests: bits MSB first. */
+EXPORT void oracle_crc_divide_bits(uint64_t explicit_poly, const uint8_t* bits, size_t L, uint8_t* rem)
+{
+    crc_poly p;
+    crc_from_explicit(&p, explicit_poly);
+    crc_divide(&p, bits, L, rem);
+}
+
+static inline int get_bit(const uint8_t* d, size_t i) /* bit_helpers.hpp:8-24 MSB first */
+{
+    return (d[i / 8] >> (7 - (i % 8))) & 1;
+}
+
+static inline void set_bit(uint8_t* d, size_t i, int v) /* bit_helpers.hpp:26-52 */
+{
+    if (v)
+        d[i / 8] |= (uint8_t)(1u << (7 - (i % 8)));
+    else
+        d[i / 8] &= (uint8_t)~(1u << (7 - (i % 8)));
+}
+
+EXPORT int oracle_crc_data_size(int block_size, uint64_t explicit_poly) /* crc_block_device.cpp:117-120 */
+{
+    int n = bitlen64(explicit_poly) - 1;
+    return block_size - (n + 7) / 8;
+}
+
+/* _calculateAndWrite :37-67, reference-faithful bit arrays.  block is bs bytes in/out. */
+static void crc_encode_faithful(const crc_poly* p, int bs, uint8_t* block)
+{
+    int ds = bs - (p->n + 7) / 8;
+    size_t L = (size_t)ds * 8 + (size_t)p->n;
+    uint8_t* bits = (uint8_t*)calloc(L, 1);
+    for (size_t i = 0; i < (size_t)ds * 8; ++i)
+        bits[i] = (uint8_t)get_bit(block, i);
+    uint8_t rem[64];
+    crc_divide(p, bits, L, rem);
+    for (int i = 0; i < p->n; ++i)
+        set_bit(block, (size_t)ds * 8 + (size_t)i, rem[i]);
+    free(bits);
+}
+
+/* _readAndCheckRaw :12-35 -> 0 ok / 5 CorrectionError. */
+static int crc_check_faithful(const crc_poly* p, int bs, const uint8_t* block)
+{
+    int ds = bs - (p->n + 7) / 8;
+    size_t L = (size_t)ds * 8 + (size_t)p->n; /* bs*8 - unused bits */
+    uint8_t* bits = (uint8_t*)malloc(L);
+    for (size_t i = 0; i < L; ++i)
+        bits[i] = (uint8_t)get_bit(block, i);
+    uint8_t rem[64];
+    crc_divide(p, bits, L, rem);
+    free(bits);
+    for (int i = 0; i < p->n; ++i)
+        if (rem[i])
+            return FS_BLOCKDEVICE_CORRECTION_ERROR;
+    return FS_OK;
+}
+
+/*
+ * Closed form of the early-stopping division (derived in DESIGN.md, checked against the
+ * faithful bit-array version in tests):  V = D(x) * x^(n-1) mod P,  stored = (V << 1) & mask.
+ * Computed here bit-serially, MSB first, for any degree 1..63.
+ */
+static uint64_t crc_stored_value(const crc_poly* p, const uint8_t* data, int ds)
+{
+    int n = p->n;
+    uint64_t mask = (n == 64) ? ~0ull : ((1ull << n) - 1);
+    uint64_t Plow = p->explicit_poly & mask;
+    uint64_t top = 1ull << (n - 1);
+    /* standard MSB-first CRC c = D * x^n mod P */
+    uint64_t c = 0;
+    for (int i = 0; i < ds; ++i) {
+        uint8_t byte = data[i];
+        for (int b = 7; b >= 0; --b) {
+            int in = (byte >> b) & 1;
+            int fb = ((c & top) ? 1 : 0) ^ in;
+            c = (c << 1) & mask;
+            if (fb)
+                c ^= Plow;
+        }
+    }
+    /* V = c * x^-1 mod P */
+    uint64_t V = (c & 1) ? ((c ^ Plow) >> 1) | top : (c >> 1);
+    return (V << 1) & mask;
+}
+
+static void crc_encode_fast(const crc_poly* p, int bs, uint8_t* block)
+{
+    int ds = bs - (p->n + 7) / 8;
+    uint64_t st = crc_stored_value(p, block, ds);
+    for (int i = 0; i < p->n; ++i)
+        set_bit(block, (size_t)ds * 8 + (size_t)i, (int)((st >> (p->n - 1 - i)) & 1));
+}
+
+static int crc_check_fast(const crc_poly* p, int bs, const uint8_t* block)
+{
+    int ds = bs - (p->n + 7) / 8;
+    uint64_t st = crc_stored_value(p, block, ds);
+    for (int i = 0; i < p->n; ++i)
+        if (get_bit(block, (size_t)ds * 8 + (size_t)i) != (int)((st >> (p->n - 1 - i)) & 1))
+            return FS_BLOCKDEVICE_CORRECTION_ERROR;
+    return FS_OK;
+}
+
+/*
+ * Batch CRC encode of full data payloads: raw is in/out (bs bytes per block); the data
+ * bytes [0,ds) are taken from data, the n CRC bits written MSB-first after them, the
+ * ceil(n/8)*8-n unused tail bits keep raw's old contents.  faithful selects the
+ * bit-array division (slow) or the closed form.
+ */
+EXPORT int oracle_crc_encode(int bs, uint64_t explicit_poly, const uint8_t* data, uint8_t* raw, size_t nblocks,
+    int faithful)
+{
+    crc_poly p;
+    crc_from_explicit(&p, explicit_poly);
+    if (p.n < 1 || p.n > 63)
+        return -1;
+    int ds = bs - (p.n + 7) / 8;
+    for (size_t b = 0; b < nblocks; ++b) {
+        uint8_t* blk = raw + b * (size_t)bs;
+        memcpy(blk, data + b * (size_t)ds, (size_t)ds);
+        if (faithful)
+            crc_encode_faithful(&p, bs, blk);
+        else
+            crc_encode_fast(&p, bs, blk);
+    }
+    return 0;
+}
+
+EXPORT int oracle_crc_check(int bs, uint64_t explicit_poly, const uint8_t* raw, uint8_t* data, uint8_t* status,
+    size_t nblocks, int faithful)
+{
+    crc_poly p;
+    crc_from_explicit(&p, explicit_poly);
+    if (p.n < 1 || p.n > 63)
+        return -1;
+    int ds = bs - (p.n + 7) / 8;
+    for (size_t b = 0; b < nblocks; ++b) {
+        const uint8_t* blk = raw + b * (size_t)bs;
+        status[b] = (uint8_t)(faithful ? crc_check_faithful(&p, bs, blk) : crc_check_fast(&p, bs, blk));
+        if (data)
+            memcpy(data + b * (size_t)ds, blk, (size_t)ds);
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Hamming (extended SECDED) -- lib/blockdevice/src/hamming_block_device.cpp             */
+/* ------------------------------------------------------------------------------------ */
+static int ham_data_size(int bs_pow) /* :11-19 */
+{
+    int bs = 1 << bs_pow;
+    int parity_bytes = (bs_pow * 3 + 1 + 7) / 8; /* ceil((3p+1)/8) */
+    return bs - parity_bytes;
+}
+
+EXPORT int oracle_hamming_data_size(int block_size)
+{
+    int p = 0;
+    while ((1 << (p + 1)) <= block_size) /* binLog, math_helpers.hpp:12-19 */
+        p++;
+    return ham_data_size(p);
+}
+
+/* HammingDataBitsIterator :180-198 */
+typedef struct {
+    unsigned cur;
+    long returned, limit;
+} ham_data_it;
+
+static long ham_data_next(ham_data_it* it)
+{
+    if (it->returned >= it->limit)
+        return -1;
+    while ((it->cur & (it->cur - 1)) == 0)
+        it->cur++;
+    it->returned++;
+    return (long)it->cur++;
+}
+
+/* HammingUsedBitsIterator :200-230 */
+typedef struct {
+    unsigned cur, next_parity;
+    long returned, limit, bits;
+} ham_used_it;
+
+static long ham_used_next(ham_used_it* it)
+{
+    if (it->returned >= it->limit && it->next_parity >= it->bits)
+        return -1;
+    if (it->returned >= it->limit) {
+        it->cur = it->next_parity;
+        it->next_parity <<= 1;
+        return (long)it->cur;
+    }
+    if (it->cur && (it->cur & (it->cur - 1)) == 0)
+        it->next_parity = it->cur << 1;
+    if (it->cur && (it->cur & (it->cur - 1)) != 0)
+        it->returned++;
+    return (long)it->cur++;
+}
+
+/* _encodeData :76-109 : enc is bs bytes in/out (unused tail bits keep their contents). */
+static void ham_encode_one(int bs_pow, const uint8_t* data, uint8_t* enc)
+{
+    int bs = 1 << bs_pow, ds = ham_data_size(bs_pow);
+    int parity = 1;
+    unsigned pxor = 0;
+    ham_data_it it = { 0, 0, (long)ds * 8 };
+    for (long i = 0; i < (long)ds * 8; ++i) {
+        int v = get_bit(data, (size_t)i);
+        long ri = ham_data_next(&it);
+        if (v) {
+            parity = !parity;
+            pxor ^= (unsigned)ri;
+        }
+        set_bit(enc, (size_t)ri, v);
+    }
+    for (unsigned pi = 1; pi < (unsigned)bs * 8; pi <<= 1) {
+        int pv = 0;
+        if (pxor & pi) {
+            parity = !parity;
+            pv = 1;
+        }
+        set_bit(enc, pi, pv);
+    }
+    set_bit(enc, 0, !parity);
+}
+
+/* _readAndFixBlock :21-65 : returns 0 ok / 1 corrected (*fix_byte set) / 5 error. */
+static int ham_fix_one(int bs_pow, uint8_t* blk, int* fix_byte)
+{
+    int bs = 1 << bs_pow, ds = ham_data_size(bs_pow);
+    unsigned epos = 0;
+    int parity = 1;
+    ham_used_it it = { 0, 1, 0, (long)ds * 8, (long)bs * 8 };
+    long idx;
+    while ((idx = ham_used_next(&it)) >= 0) {
+        if (get_bit(blk, (size_t)idx)) {
+            epos ^= (unsigned)idx;
+            parity = !parity;
+        }
+    }
+    *fix_byte = -1;
+    if (!parity) {
+        set_bit(blk, epos, !get_bit(blk, epos));
+        *fix_byte = (int)(epos / 8);
+        return FS_CORRECTED;
+    }
+    if (epos != 0)
+        return FS_BLOCKDEVICE_CORRECTION_ERROR;
+    return FS_OK;
+}
+
+static void ham_extract_one(int bs_pow, const uint8_t* enc, uint8_t* data) /* _extractData :67-74 */
+{
+    int ds = ham_data_size(bs_pow);
+    ham_data_it it = { 0, 0, (long)ds * 8 };
+    for (long i = 0; i < (long)ds * 8; ++i)
+        set_bit(data, (size_t)i, get_bit(enc, (size_t)ham_data_next(&it)));
+}
+
+static int ham_pow(int block_size)
+{
+    int p = 0;
+    while ((1 << (p + 1)) <= block_size)
+        p++;
+    return p;
+}
+
+/* Batch encode of full payloads; raw in/out (tail bits preserved). */
+EXPORT int oracle_hamming_encode(int block_size, const uint8_t* data, uint8_t* raw, size_t nblocks)
+{
+    int p = ham_pow(block_size), bs = 1 << p, ds = ham_data_size(p);
+    for (size_t b = 0; b < nblocks; ++b)
+        ham_encode_one(p, data + b * (size_t)ds, raw + b * (size_t)bs);
+    return 0;
+}
+
+/*
+ * Batch decode: raw_fixed (bs bytes per block, may be NULL) receives the block after the
+ * one-byte write-back; status 0/1/5; data gets the extracted payload when status != 5
+ * (unchanged/undefined otherwise -- the reference returns an error and no data).
+ */
+EXPORT int oracle_hamming_decode(int block_size, const uint8_t* raw, uint8_t* data, uint8_t* status,
+    uint8_t* raw_fixed, int32_t* fix_byte, size_t nblocks)
+{
+    int p = ham_pow(block_size), bs = 1 << p, ds = ham_data_size(p);
+    uint8_t* tmp = (uint8_t*)malloc((size_t)bs);
+    for (size_t b = 0; b < nblocks; ++b) {
+        memcpy(tmp, raw + b * (size_t)bs, (size_t)bs);
+        int fb = -1;
+        int st = ham_fix_one(p, tmp, &fb);
+        status[b] = (uint8_t)st;
+        if (fix_byte)
+            fix_byte[b] = fb;
+        if (raw_fixed)
+            memcpy(raw_fixed + b * (size_t)bs, tmp, (size_t)bs);
+        if (st != FS_BLOCKDEVICE_CORRECTION_ERROR && data)
+            ham_extract_one(p, tmp, data + b * (size_t)ds);
+    }
+    free(tmp);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Parity -- lib/blockdevice/src/parity_block_device.cpp                                 */
+/* ------------------------------------------------------------------------------------ */
+static int parity_ok(const uint8_t* blk, int bs) /* _checkParity :90-97 */
+{
+    unsigned ones = 0;
+    for (int i = 0; i < bs; ++i)
+        ones += (unsigned)__builtin_popcount(blk[i]);
+    return !(ones & 1);
+}
+
+/* Full-payload encode (writeBlock :31-61 with offset 0, size bs-1): raw in/out. */
+EXPORT int oracle_parity_encode(int bs, const uint8_t* data, uint8_t* raw, size_t nblocks)
+{
+    for (size_t b = 0; b < nblocks; ++b) {
+        uint8_t* blk = raw + b * (size_t)bs;
+        memcpy(blk, data + b * (size_t)(bs - 1), (size_t)(bs - 1));
+        if (!parity_ok(blk, bs))
+            blk[bs - 1] ^= 1;
+    }
+    return 0;
+}
+
+EXPORT int oracle_parity_check(int bs, const uint8_t* raw, uint8_t* data, uint8_t* status, size_t nblocks)
+{
+    for (size_t b = 0; b < nblocks; ++b) {
+        const uint8_t* blk = raw + b * (size_t)bs;
+        status[b] = parity_ok(blk, bs) ? FS_OK : FS_BLOCKDEVICE_CORRECTION_ERROR;
+        if (data)
+            memcpy(data + b * (size_t)(bs - 1), blk, (size_t)(bs - 1));
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* IBlockDevice semantics over an in-memory disk (StackDisk/HeapDisk behaviour:         */
+/* lib/disk/include/ppfs/disk/stack_disk.hpp:19-44 -- out-of-range accesses fail whole).  */
+/* The device state is (type, params); the disk is a caller-owned byte array.            */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+    int type; /* ECCType: 0 None, 1 Crc, 2 Hamming, 3 Parity, 4 ReedSolomon (ecc_type.hpp:8-14) */
+    int block_size;
+    int t;
+    uint64_t poly;
+    uint8_t* disk;
+    size_t disk_size;
+    /* correction log: ErrorCorrectionEvent block indices (rs:171-173, hamming:53-57) */
+    int32_t* log;
+    size_t log_cap, log_len;
+} odev;
+
+static int disk_read(odev* d, size_t addr, size_t size, uint8_t* out)
+{
+    if (addr + size > d->disk_size)
+        return FS_DISK_OUT_OF_BOUNDS;
+    memcpy(out, d->disk + addr, size);
+    return 0;
+}
+
+static int disk_write(odev* d, size_t addr, const uint8_t* in, size_t size)
+{
+    if (addr + size > d->disk_size)
+        return FS_DISK_OUT_OF_BOUNDS;
+    memcpy(d->disk + addr, in, size);
+    return 0;
+}
+
+static void log_correction(odev* d, int block)
+{
+    if (d->log && d->log_len < d->log_cap)
+        d->log[d->log_len] = block;
+    d->log_len++;
+}
+
+EXPORT void* oracle_dev_create(int type, int block_size, int t, uint64_t explicit_poly, uint8_t* disk,
+    size_t disk_size, int32_t* log, size_t log_cap)
+{
+    gf_init();
+    odev* d = (odev*)calloc(1, sizeof(odev));
+    d->type = type;
+    d->block_size = block_size;
+    d->t = t;
+    d->poly = explicit_poly;
+    d->disk = disk;
+    d->disk_size = disk_size;
+    d->log = log;
+    d->log_cap = log_cap;
+    return d;
+}
+
+EXPORT void oracle_dev_destroy(void* h) { free(h); }
+
+EXPORT size_t oracle_dev_log_len(void* h) { return ((odev*)h)->log_len; }
+
+static size_t dev_raw_size(odev* d)
+{
+    switch (d->type) {
+    case 4: {
+        rs_code rs;
+        rs_setup(&rs, d->block_size, d->t);
+        return (size_t)rs.n;
+    }
+    case 2:
+        return (size_t)1 << ham_pow(d->block_size);
+    default:
+        return (size_t)d->block_size;
+    }
+}
+
+static size_t dev_data_size(odev* d)
+{
+    switch (d->type) {
+    case 0:
+        return (size_t)d->block_size;
+    case 1:
+        return (size_t)oracle_crc_data_size(d->block_size, d->poly);
+    case 2:
+        return (size_t)ham_data_size(ham_pow(d->block_size));
+    case 3:
+        return (size_t)d->block_size - 1;
+    default: {
+        rs_code rs;
+        rs_setup(&rs, d->block_size, d->t);
+        return (size_t)(rs.n - 2 * rs.t);
+    }
+    }
+}
+
+EXPORT size_t oracle_dev_raw_block_size(void* h) { return dev_raw_size((odev*)h); }
+EXPORT size_t oracle_dev_data_size(void* h) { return dev_data_size((odev*)h); }
+
+EXPORT int oracle_dev_format(void* h, unsigned block) /* formatBlock for each codec */
+{
+    odev* d = (odev*)h;
+    size_t raw = dev_raw_size(d);
+    uint8_t buf[4096];
+    memset(buf, 0, sizeof buf);
+    switch (d->type) {
+    case 0:
+        return 0; /* raw_block_device.cpp:39 no-op */
+    case 1: {      /* crc_block_device.cpp:124-134 : zero data + computed CRC, whole block */
+        crc_poly p;
+        crc_from_explicit(&p, d->poly);
+        crc_encode_fast(&p, (int)raw, buf);
+        return disk_write(d, (size_t)block * raw, buf, raw);
+    }
+    default: /* rs:15-23 hamming:164-172 parity:22-29 all-zero raw block */
+        return disk_write(d, (size_t)block * raw, buf, raw);
+    }
+}
+
+/* RS _fixBlockAndExtract with its disk write-back (rs_block_device.cpp:119-183). */
+static void rs_dev_fix(odev* d, const rs_code* rs, int block, const uint8_t* rawblk, uint8_t* data)
+{
+    uint8_t fixed[PMAX];
+    int wl = 0;
+    int st = rs_decode_one(rs, rawblk, data, fixed, &wl, NULL);
+    if (st == FS_CORRECTED) {
+        log_correction(d, block);
+        (void)disk_write(d, (size_t)block * (size_t)rs->n, fixed, (size_t)wl); /* result ignored (:180) */
+    }
+}
+
+/* readBlock for each codec: returns FsError (0 ok). out gets *out_len bytes. */
+EXPORT int oracle_dev_read(void* h, int block, size_t offset, size_t nbytes, size_t out_capacity, uint8_t* out,
+    size_t* out_len)
+{
+    odev* d = (odev*)h;
+    size_t raw = dev_raw_size(d), ds = dev_data_size(d);
+    uint8_t blk[4096], dec[4096];
+    *out_len = 0;
+    if (d->type == 0) { /* raw_block_device.cpp:30-37 -> StackDisk::read checks bounds, then capacity */
+        size_t to_read = nbytes < raw - offset ? nbytes : raw - offset;
+        if ((size_t)block * raw + offset + to_read > d->disk_size)
+            return FS_DISK_OUT_OF_BOUNDS;
+        if (out_capacity < to_read)
+            return FS_DISK_INVALID_REQUEST;
+        int r = disk_read(d, (size_t)block * raw + offset, to_read, out);
+        if (!r)
+            *out_len = to_read;
+        return r;
+    }
+    if (out_capacity < nbytes)
+        return FS_DISK_INVALID_REQUEST;
+    size_t to_read = nbytes < ds - offset ? nbytes : ds - offset;
+    int r = disk_read(d, (size_t)block * raw, raw, blk);
+    if (r)
+        return r;
+    switch (d->type) {
+    case 4: {
+        rs_code rs;
+        rs_setup(&rs, d->block_size, d->t);
+        rs_dev_fix(d, &rs, block, blk, dec);
+        break;
+    }
+    case 1: {
+        crc_poly p;
+        crc_from_explicit(&p, d->poly);
+        if (crc_check_fast(&p, (int)raw, blk))
+            return FS_BLOCKDEVICE_CORRECTION_ERROR;
+        memcpy(dec, blk, ds);
+        break;
+    }
+    case 2: {
+        int fb;
+        int st = ham_fix_one(ham_pow(d->block_size), blk, &fb);
+        if (st == FS_CORRECTED) {
+            int wr = disk_write(d, (size_t)block * raw + (size_t)fb, blk + fb, 1);
+            if (wr)
+                return wr;
+            log_correction(d, block);
+        } else if (st != FS_OK) {
+            return st;
+        }
+        ham_extract_one(ham_pow(d->block_size), blk, dec);
+        break;
+    }
+    case 3:
+        if (!parity_ok(blk, (int)raw))
+            return FS_BLOCKDEVICE_CORRECTION_ERROR;
+        memcpy(dec, blk, ds);
+        break;
+    }
+    memcpy(out, dec + offset, to_read);
+    *out_len = to_read;
+    return 0;
+}
+
+/* writeBlock for each codec; *written gets the returned byte count. */
+EXPORT int oracle_dev_write(void* h, int block, size_t offset, const uint8_t* data, size_t len, size_t* written)
+{
+    odev* d = (odev*)h;
+    size_t raw = dev_raw_size(d), ds = dev_data_size(d);
+    uint8_t blk[4096], dec[4096];
+    *written = 0;
+    if (d->type == 0) { /* raw_block_device.cpp:16-28 */
+        size_t to_write = len < raw - offset ? len : raw - offset;
+        int r = disk_write(d, (size_t)block * raw + offset, data, to_write);
+        if (!r)
+            *written = to_write;
+        return r;
+    }
+    size_t to_write = len < ds - offset ? len : ds - offset;
+    int r = disk_read(d, (size_t)block * raw, raw, blk);
+    if (r)
+        return r;
+    switch (d->type) {
+    case 4: { /* rs_block_device.cpp:61-93 */
+        rs_code rs;
+        rs_setup(&rs, d->block_size, d->t);
+        rs_dev_fix(d, &rs, block, blk, dec);
+        memcpy(dec + offset, data, to_write);
+        rs_encode_one(&rs, dec, blk);
+        break;
+    }
+    case 1: { /* crc_block_device.cpp:78-94 */
+        crc_poly p;
+        crc_from_explicit(&p, d->poly);
+        if (crc_check_fast(&p, (int)raw, blk))
+            return FS_BLOCKDEVICE_CORRECTION_ERROR;
+        memcpy(blk + offset, data, to_write);
+        crc_encode_fast(&p, (int)raw, blk);
+        break;
+    }
+    case 2: { /* hamming_block_device.cpp:111-137 */
+        int fb, pw = ham_pow(d->block_size);
+        int st = ham_fix_one(pw, blk, &fb);
+        if (st == FS_CORRECTED) {
+            int wr = disk_write(d, (size_t)block * raw + (size_t)fb, blk + fb, 1);
+            if (wr)
+                return wr;
+            log_correction(d, block);
+        } else if (st != FS_OK) {
+            return st;
+        }
+        ham_extract_one(pw, blk, dec);
+        memcpy(dec + offset, data, to_write);
+        ham_encode_one(pw, dec, blk);
+        break;
+    }
+    case 3: /* parity_block_device.cpp:31-61 */
+        if (!parity_ok(blk, (int)raw))
+            return FS_BLOCKDEVICE_CORRECTION_ERROR;
+        memcpy(blk + offset, data, to_write);
+        if (!parity_ok(blk, (int)raw))
+            blk[raw - 1] ^= 1;
+        break;
+    }
+    r = disk_write(d, (size_t)block * raw, blk, raw);
+    if (r)
+        return r;
+    *written = to_write;
+    return 0;
+}

@@ -1,0 +1,106 @@
+"""ctypes binding of the C ABI in include/ppfs_ecc.h (libppfs_ecc.so, built in-tree).
+
+The library is the product path: it holds the HIP kernels for gfx950.  Loading fails loudly
+when it is missing -- there is no CPU fallback anywhere in this package.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_int, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libppfs_ecc.so")
+
+# ECCType (lib/blockdevice/include/ppfs/blockdevice/ecc_type.hpp:8-14)
+ECC_NONE, ECC_CRC, ECC_HAMMING, ECC_PARITY, ECC_REED_SOLOMON = 0, 1, 2, 3, 4
+
+STATUS_OK, STATUS_CORRECTED, STATUS_CORRECTION_ERROR = 0, 1, 5
+
+# every symbol include/ppfs_ecc.h declares
+EXPORTED_SYMBOLS = (
+    "ppfs_ecc_crc_implicit_to_explicit",
+    "ppfs_ecc_create",
+    "ppfs_ecc_destroy",
+    "ppfs_ecc_raw_block_size",
+    "ppfs_ecc_data_size",
+    "ppfs_ecc_kernel_name",
+    "ppfs_ecc_encode_device",
+    "ppfs_ecc_decode_device",
+    "ppfs_ecc_write_device",
+    "ppfs_ecc_encode_host",
+    "ppfs_ecc_decode_host",
+    "ppfs_ecc_write_host",
+    "ppfs_ecc_last_error",
+)
+
+
+class EccParams(ctypes.Structure):
+    _fields_ = [
+        ("ecc_type", c_uint32),
+        ("block_size", c_uint32),
+        ("rs_correctable_bytes", c_uint32),
+        ("reserved", c_uint32),
+        ("crc_polynomial", c_uint64),
+    ]
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libppfs_ecc.so (raises NativeLibraryMissing if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryMissing(
+            f"{LIB_PATH} not found: build it with `make -C paritypartyfs_amd/csrc` "
+            "(or __graft_entry__.build()); the HIP engine has no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    u8p = POINTER(c_uint8)
+    L.ppfs_ecc_crc_implicit_to_explicit.restype = c_uint64
+    L.ppfs_ecc_crc_implicit_to_explicit.argtypes = [c_uint64]
+    L.ppfs_ecc_create.restype = c_int
+    L.ppfs_ecc_create.argtypes = [POINTER(EccParams), c_int, POINTER(c_void_p)]
+    L.ppfs_ecc_destroy.restype = None
+    L.ppfs_ecc_destroy.argtypes = [c_void_p]
+    L.ppfs_ecc_raw_block_size.restype = c_size_t
+    L.ppfs_ecc_raw_block_size.argtypes = [c_void_p]
+    L.ppfs_ecc_data_size.restype = c_size_t
+    L.ppfs_ecc_data_size.argtypes = [c_void_p]
+    L.ppfs_ecc_kernel_name.restype = c_char_p
+    L.ppfs_ecc_kernel_name.argtypes = [c_void_p]
+    L.ppfs_ecc_encode_device.restype = c_int
+    L.ppfs_ecc_encode_device.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
+    L.ppfs_ecc_decode_device.restype = c_int
+    L.ppfs_ecc_decode_device.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_void_p,
+                                         c_void_p]
+    L.ppfs_ecc_write_device.restype = c_int
+    L.ppfs_ecc_write_device.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
+    L.ppfs_ecc_encode_host.restype = c_int
+    L.ppfs_ecc_encode_host.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t]
+    L.ppfs_ecc_decode_host.restype = c_int
+    L.ppfs_ecc_decode_host.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_void_p]
+    L.ppfs_ecc_write_host.restype = c_int
+    L.ppfs_ecc_write_host.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]
+    L.ppfs_ecc_last_error.restype = c_char_p
+    L.ppfs_ecc_last_error.argtypes = []
+    _ = u8p
+    _lib = L
+    return L
+
+
+class EccError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        super().__init__(f"ppfs_ecc error {code}: {what}")
+        self.code = code
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise EccError(rc, lib().ppfs_ecc_last_error().decode(errors="replace"))

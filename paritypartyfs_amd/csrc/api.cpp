@@ -1,0 +1,733 @@
+// api.cpp -- host implementation of the ppfs_ecc C ABI (include/ppfs_ecc.h).
+//
+// Builds the per-context codec tables (GF(2^8) log/antilog, RS slicing tables, CRC shift
+// tables), uploads them once, and dispatches batches to the HIP kernels in rs_kernels.hip and
+// bit_kernels.hip.  Parameter handling mirrors the reference constructors:
+//   ReedSolomonBlockDevice  rs_block_device.cpp:52-60  (n = min(bs,255), t = min(t, n/2))
+//   CrcBlockDevice          crc_block_device.cpp:71-76, dataSize :117-120
+//   HammingBlockDevice      hamming_block_device.cpp:11-19 (bs = 2^binLog(block_size))
+//   ParityBlockDevice       parity_block_device.cpp:9-15
+//   RawBlockDevice          raw_block_device.cpp:5-9
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/ppfs_ecc.h"
+
+// kernels (rs_kernels.hip / bit_kernels.hip)
+extern "C" {
+int ppfs_rs_fast_supported(int n, int t2);
+int ppfs_rs_fast_tables_bytes(int t2);
+hipError_t ppfs_rs_fast_encode(int t2, const uint8_t* d, uint8_t* r, uint64_t nb, const uint8_t* tab, hipStream_t s);
+hipError_t ppfs_rs_fast_decode(int t2, uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, const uint8_t* tab, int wb,
+    hipStream_t s);
+hipError_t ppfs_rs_generic_encode(const uint8_t* d, uint8_t* r, uint64_t nb, int n, int t2, const uint8_t* tab,
+    hipStream_t s);
+hipError_t ppfs_rs_generic_decode(uint8_t* r, uint8_t* d, uint8_t* st, uint8_t* spill, uint64_t nb, int n, int t2,
+    int wb, const uint8_t* tab, hipStream_t s);
+int ppfs_crc_tables_bytes(void);
+hipError_t ppfs_crc_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs, uint32_t ds,
+    uint32_t n, uint64_t mask, const uint8_t* tab, hipStream_t s);
+hipError_t ppfs_crc_check(const uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, uint32_t bs, uint32_t ds, uint32_t n,
+    uint64_t mask, const uint8_t* tab, hipStream_t s);
+hipError_t ppfs_ham_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs, uint32_t ds,
+    uint32_t L, hipStream_t s);
+hipError_t ppfs_ham_decode(uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, int wb, uint32_t bs, uint32_t ds,
+    uint32_t L, hipStream_t s);
+hipError_t ppfs_parity_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs,
+    hipStream_t s);
+hipError_t ppfs_parity_check(const uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, uint32_t bs, hipStream_t s);
+}
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* what, hipError_t e = hipSuccess)
+{
+    g_last_error = what;
+    if (e != hipSuccess) {
+        g_last_error += ": ";
+        g_last_error += hipGetErrorString(e);
+    }
+    return code;
+}
+
+#define HIP_TRY(expr, what)                                                                                            \
+    do {                                                                                                               \
+        hipError_t _e = (expr);                                                                                        \
+        if (_e != hipSuccess)                                                                                          \
+            return fail(PPFS_ECC_EHIP, what, _e);                                                                      \
+    } while (0)
+
+// ---------------------------------------------------------------------------------------
+// GF(2^8) host tables (gf256.cpp:6-29)
+// ---------------------------------------------------------------------------------------
+struct GfHost {
+    uint8_t exp[256], log[256];
+    GfHost()
+    {
+        unsigned x = 1;
+        for (int i = 0; i < 255; ++i) {
+            exp[i] = (uint8_t)x;
+            x <<= 1;
+            if (x & 0x100)
+                x ^= 0x11D;
+        }
+        exp[255] = exp[0];
+        std::memset(log, 0, sizeof log);
+        for (int i = 0; i < 255; ++i)
+            log[exp[i]] = (uint8_t)i;
+    }
+    uint8_t mul(uint8_t a, uint8_t b) const
+    {
+        if (!a || !b)
+            return 0;
+        return exp[(log[a] + log[b]) % 255];
+    }
+};
+const GfHost& gf()
+{
+    static GfHost g;
+    return g;
+}
+
+// 1 KiB block: EXP2[512] | LOG[256] | QS[256]
+void build_gf_block(uint8_t* out)
+{
+    const GfHost& g = gf();
+    for (int i = 0; i < 512; ++i)
+        out[i] = g.exp[i % 255];
+    std::memcpy(out + 512, g.log, 256);
+    uint8_t* qs = out + 768;
+    std::memset(qs, 0, 256);
+    for (int y = 2; y < 256; ++y) {
+        const uint8_t c = (uint8_t)(g.mul((uint8_t)y, (uint8_t)y) ^ y);
+        if (!qs[c])
+            qs[c] = (uint8_t)y;
+    }
+}
+
+// generator g(x) = prod_{i=1..2t}(x + alpha^i), low -> high (rs_block_device.cpp:195-208)
+std::vector<uint8_t> rs_generator(int t2)
+{
+    const GfHost& G = gf();
+    std::vector<uint8_t> g(1, 1);
+    uint8_t power = 2;
+    for (int i = 0; i < t2; ++i) {
+        std::vector<uint8_t> ng(g.size() + 1, 0);
+        for (size_t k = 0; k < g.size(); ++k) {
+            ng[k] ^= G.mul(g[k], power);
+            ng[k + 1] ^= g[k];
+        }
+        g.swap(ng);
+        power = G.mul(power, 2);
+    }
+    return g;
+}
+
+// x^e mod g (monic, degree t2): returns t2 coefficients
+std::vector<uint8_t> rs_xpow_mod(int e, const std::vector<uint8_t>& g, int t2)
+{
+    const GfHost& G = gf();
+    std::vector<uint8_t> r(t2, 0);
+    r[0] = 1;
+    if (t2 == 0)
+        return r;
+    for (int k = 0; k < e; ++k) {
+        const uint8_t top = r[t2 - 1];
+        for (int q = t2 - 1; q >= 1; --q)
+            r[q] = (uint8_t)(r[q - 1] ^ G.mul(top, g[q]));
+        r[0] = G.mul(top, g[0]);
+    }
+    return r;
+}
+
+// slicing tables for the fast path (see rs_kernels.hip: slice8)
+std::vector<uint8_t> build_rs_slice_tables(int t2)
+{
+    const GfHost& G = gf();
+    const int W = t2 <= 8 ? 2 : (t2 <= 16 ? 4 : 8);
+    const int bytes = ppfs_rs_fast_tables_bytes(t2);
+    std::vector<uint8_t> out((size_t)bytes, 0);
+    const std::vector<uint8_t> g = rs_generator(t2);
+    for (int i = 0; i < 8; ++i) {
+        const std::vector<uint8_t> xi = rs_xpow_mod(t2 + i, g, t2);
+        for (int h = 0; h < 2; ++h) {
+            for (int v = 0; v < 16; ++v) {
+                const uint8_t val = (uint8_t)(v << (4 * h));
+                uint8_t entry[32] = { 0 };
+                for (int q = 0; q < t2; ++q)
+                    entry[4 * W - t2 + q] = G.mul(val, xi[q]);
+                const size_t slot = (size_t)((2 * i + h) * 16 + v) * 16;
+                if (W <= 4) {
+                    std::memcpy(&out[slot], entry, (size_t)(4 * W));
+                } else {
+                    std::memcpy(&out[slot], entry, 16);
+                    std::memcpy(&out[4096 + slot], entry + 16, 16);
+                }
+            }
+        }
+    }
+    return out;
+}
+
+// ---------------------------------------------------------------------------------------
+// CRC host maths over GF(2)[x] / P  (P explicit, degree n <= 63)
+// ---------------------------------------------------------------------------------------
+struct CrcHost {
+    uint64_t P;
+    int n;
+    uint64_t mask;
+    uint64_t mod(uint64_t a) const // reduce a polynomial of degree <= 63
+    {
+        for (int k = 63; k >= n; --k)
+            if ((a >> k) & 1u)
+                a ^= P << (k - n);
+        return a;
+    }
+    uint64_t mulx(uint64_t a) const
+    {
+        const bool top = (a >> (n - 1)) & 1u;
+        a = (a << 1) & mask;
+        return top ? a ^ (P & mask) : a;
+    }
+    uint64_t mul(uint64_t a, uint64_t b) const // a*b mod P (a, b reduced)
+    {
+        uint64_t r = 0;
+        for (int k = n - 1; k >= 0; --k) {
+            r = mulx(r);
+            if ((b >> k) & 1u)
+                r ^= a;
+        }
+        return r;
+    }
+    uint64_t xpow(long e) const // x^e mod P, e may be negative (x is invertible: P(0) = 1)
+    {
+        uint64_t base = e >= 0 ? mod(2u) : (P >> 1); // x or x^-1 = (P - 1)/x
+        if (e < 0)
+            e = -e;
+        uint64_t r = mod(1u);
+        while (e) {
+            if (e & 1)
+                r = mul(r, base);
+            base = mul(base, base);
+            e >>= 1;
+        }
+        return r;
+    }
+};
+
+std::vector<uint8_t> build_crc_tables(uint64_t P, int n, uint32_t ds)
+{
+    CrcHost c { P, n, n == 64 ? ~0ull : ((1ull << n) - 1) };
+    const uint32_t G = (ds + 63) / 64;
+    const long z = 64L * G - ds;
+    std::vector<uint8_t> out((size_t)ppfs_crc_tables_bytes(), 0);
+    uint64_t* pt = (uint64_t*)out.data();
+    for (int pos = 0; pos < 64; ++pos) {
+        const uint64_t f = c.xpow(8L * (63 - pos) + n - 8 * z - 1);
+        for (int h = 0; h < 2; ++h)
+            for (int v = 0; v < 16; ++v)
+                pt[(pos * 2 + h) * 16 + v] = c.mul(c.mod((uint64_t)v << (4 * h)), f);
+    }
+    uint64_t* lv = (uint64_t*)(out.data() + 64 * 2 * 16 * 8);
+    for (int j = 0; j < 6; ++j) {
+        const uint64_t f = c.xpow(512L << j);
+        for (int k = 0; k < 16; ++k)
+            for (int v = 0; v < 16; ++v)
+                lv[(j * 16 + k) * 16 + v] = (4 * k < 64) ? c.mul(c.mod((uint64_t)v << (4 * k)), f) : 0;
+    }
+    return out;
+}
+
+int bitlen64(uint64_t v)
+{
+    int c = 0;
+    while (v) {
+        v >>= 1;
+        c++;
+    }
+    return c;
+}
+
+} // namespace
+
+// ---------------------------------------------------------------------------------------
+// Context
+// ---------------------------------------------------------------------------------------
+struct ppfs_ecc_ctx {
+    ppfs_ecc_params p {};
+    int device = 0;
+    // derived
+    uint32_t raw = 0, data = 0;
+    int rs_n = 0, rs_t2 = 0;
+    bool rs_fast = false;
+    int crc_n = 0;
+    uint64_t crc_mask = 0;
+    uint32_t ham_L = 0;
+    const char* kname = "";
+    // device tables
+    uint8_t* d_tables = nullptr;
+    // scratch for write_device status when the caller passes none
+    uint8_t* d_scratch = nullptr;
+    size_t scratch_bytes = 0;
+    // host staging
+    hipStream_t hs[2] = { nullptr, nullptr };
+    uint8_t* h_pin[2] = { nullptr, nullptr };
+    uint8_t* d_stage[2] = { nullptr, nullptr };
+    size_t stage_bytes = 0;
+};
+
+extern "C" uint64_t ppfs_ecc_crc_implicit_to_explicit(uint64_t implicit_poly) { return (implicit_poly << 1) + 1; }
+
+extern "C" const char* ppfs_ecc_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_ecc_ctx** out)
+{
+    if (!params || !out)
+        return fail(PPFS_ECC_EINVAL, "null argument");
+    *out = nullptr;
+    const ppfs_ecc_params p = *params;
+    if (p.block_size == 0 || p.block_size > 4096)
+        return fail(PPFS_ECC_EINVAL, "block_size must be in [1, 4096] (MAX_BLOCK_SIZE)");
+    ppfs_ecc_ctx* c = new (std::nothrow) ppfs_ecc_ctx();
+    if (!c)
+        return fail(PPFS_ECC_ENOMEM, "ctx alloc");
+    c->p = p;
+    c->device = device;
+    std::vector<uint8_t> tables;
+    switch (p.ecc_type) {
+    case PPFS_ECC_NONE:
+        c->raw = c->data = p.block_size;
+        c->kname = "raw-copy";
+        break;
+    case PPFS_ECC_REED_SOLOMON: {
+        c->rs_n = (int)std::min<uint32_t>(p.block_size, 255);
+        const int t = (int)std::min<uint32_t>(p.rs_correctable_bytes, (uint32_t)c->rs_n / 2);
+        c->rs_t2 = 2 * t;
+        c->raw = (uint32_t)c->rs_n;
+        c->data = (uint32_t)(c->rs_n - c->rs_t2);
+        c->rs_fast = ppfs_rs_fast_supported(c->rs_n, c->rs_t2) != 0;
+        tables.resize(4096 + 8192 + 1024, 0);
+        if (c->rs_fast) {
+            std::vector<uint8_t> s = build_rs_slice_tables(c->rs_t2);
+            tables.assign(s.begin(), s.end());
+            tables.resize(s.size() + 1024);
+            build_gf_block(tables.data() + s.size());
+            c->kname = "rs255-slice8-lds";
+        } else {
+            tables.assign(1024 + 256, 0);
+            build_gf_block(tables.data());
+            std::vector<uint8_t> g = rs_generator(c->rs_t2);
+            std::memcpy(tables.data() + 1024, g.data(), g.size());
+            c->kname = "rs-generic-lfsr";
+        }
+        break;
+    }
+    case PPFS_ECC_CRC: {
+        const int n = bitlen64(p.crc_polynomial) - 1;
+        if (n < 1 || n > 63) {
+            delete c;
+            return fail(PPFS_ECC_EINVAL, "CRC polynomial degree must be in [1, 63]");
+        }
+        const uint32_t nbc = (uint32_t)((n + 7) / 8);
+        if (p.block_size <= nbc) {
+            delete c;
+            return fail(PPFS_ECC_EINVAL, "block too small for the CRC");
+        }
+        c->crc_n = n;
+        c->crc_mask = (1ull << n) - 1;
+        c->raw = p.block_size;
+        c->data = p.block_size - nbc;
+        tables = build_crc_tables(p.crc_polynomial, n, c->data);
+        c->kname = "crc-nibble-shift";
+        break;
+    }
+    case PPFS_ECC_HAMMING: {
+        int pw = 0;
+        while ((1u << (pw + 1)) <= p.block_size)
+            pw++;
+        if (pw < 3) {
+            delete c;
+            return fail(PPFS_ECC_EINVAL, "Hamming block must be >= 8 bytes");
+        }
+        c->raw = 1u << pw;
+        c->data = c->raw - (uint32_t)((3 * pw + 1 + 7) / 8);
+        // raw index of the last payload bit (HammingDataBitsIterator, hamming_block_device.cpp:180-198)
+        uint32_t idx = 0;
+        for (uint32_t i = 0; i < 8 * c->data; ++i) {
+            while ((idx & (idx - 1)) == 0)
+                idx++;
+            c->ham_L = idx++;
+        }
+        c->kname = "hamming-funnel";
+        break;
+    }
+    case PPFS_ECC_PARITY:
+        if (p.block_size < 2) {
+            delete c;
+            return fail(PPFS_ECC_EINVAL, "parity block must be >= 2 bytes");
+        }
+        c->raw = p.block_size;
+        c->data = p.block_size - 1;
+        c->kname = "parity-popcount";
+        break;
+    default:
+        delete c;
+        return fail(PPFS_ECC_EINVAL, "unknown ecc_type");
+    }
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) {
+        delete c;
+        return fail(PPFS_ECC_EHIP, "hipSetDevice", e);
+    }
+    if (!tables.empty()) {
+        e = hipMalloc(&c->d_tables, tables.size());
+        if (e == hipSuccess)
+            e = hipMemcpy(c->d_tables, tables.data(), tables.size(), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            ppfs_ecc_destroy(c);
+            return fail(PPFS_ECC_EHIP, "table upload", e);
+        }
+    }
+    *out = c;
+    return 0;
+}
+
+extern "C" void ppfs_ecc_destroy(ppfs_ecc_ctx* c)
+{
+    if (!c)
+        return;
+    (void)hipSetDevice(c->device);
+    for (int i = 0; i < 2; ++i) {
+        if (c->hs[i])
+            (void)hipStreamDestroy(c->hs[i]);
+        if (c->h_pin[i])
+            (void)hipHostFree(c->h_pin[i]);
+        if (c->d_stage[i])
+            (void)hipFree(c->d_stage[i]);
+    }
+    if (c->d_tables)
+        (void)hipFree(c->d_tables);
+    if (c->d_scratch)
+        (void)hipFree(c->d_scratch);
+    delete c;
+}
+
+extern "C" size_t ppfs_ecc_raw_block_size(const ppfs_ecc_ctx* c) { return c ? c->raw : 0; }
+extern "C" size_t ppfs_ecc_data_size(const ppfs_ecc_ctx* c) { return c ? c->data : 0; }
+extern "C" const char* ppfs_ecc_kernel_name(const ppfs_ecc_ctx* c) { return c ? c->kname : ""; }
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+static int check_hip(hipError_t e, const char* what)
+{
+    if (e != hipSuccess)
+        return fail(PPFS_ECC_EHIP, what, e);
+    return 0;
+}
+
+extern "C" int ppfs_ecc_encode_device(ppfs_ecc_ctx* c, const uint8_t* d_data, uint8_t* d_raw, size_t nblocks,
+    void* stream)
+{
+    if (!c || (nblocks && (!d_data || !d_raw)))
+        return fail(PPFS_ECC_EINVAL, "encode: null argument");
+    if (nblocks == 0)
+        return 0;
+    hipStream_t s = (hipStream_t)stream;
+    switch (c->p.ecc_type) {
+    case PPFS_ECC_NONE:
+        return check_hip(hipMemcpyAsync(d_raw, d_data, nblocks * c->raw, hipMemcpyDeviceToDevice, s), "copy");
+    case PPFS_ECC_REED_SOLOMON:
+        if (c->rs_fast && aligned16(d_data) && aligned16(d_raw))
+            return check_hip(ppfs_rs_fast_encode(c->rs_t2, d_data, d_raw, nblocks, c->d_tables, s), "rs encode");
+        if (c->rs_fast) {
+            // fast tables but unaligned pointers: the generic kernel needs gf block + generator
+            return fail(PPFS_ECC_EINVAL, "rs encode: device pointers must be 16-byte aligned");
+        }
+        return check_hip(ppfs_rs_generic_encode(d_data, d_raw, nblocks, c->rs_n, c->rs_t2, c->d_tables, s),
+            "rs generic encode");
+    case PPFS_ECC_CRC:
+        return check_hip(ppfs_crc_encode(d_data, d_raw, nullptr, nblocks, c->raw, c->data, (uint32_t)c->crc_n,
+                             c->crc_mask, c->d_tables, s),
+            "crc encode");
+    case PPFS_ECC_HAMMING:
+        if (!aligned16(d_raw))
+            return fail(PPFS_ECC_EINVAL, "hamming: raw pointer must be 16-byte aligned");
+        return check_hip(ppfs_ham_encode(d_data, d_raw, nullptr, nblocks, c->raw, c->data, c->ham_L, s),
+            "hamming encode");
+    case PPFS_ECC_PARITY:
+        return check_hip(ppfs_parity_encode(d_data, d_raw, nullptr, nblocks, c->raw, s), "parity encode");
+    }
+    return fail(PPFS_ECC_EINVAL, "bad ctx");
+}
+
+extern "C" int ppfs_ecc_decode_device(ppfs_ecc_ctx* c, uint8_t* d_raw, uint8_t* d_data, uint8_t* d_status,
+    size_t nblocks, int write_back, uint8_t* d_spill, void* stream)
+{
+    if (!c || (nblocks && !d_raw))
+        return fail(PPFS_ECC_EINVAL, "decode: null argument");
+    if (nblocks == 0)
+        return 0;
+    hipStream_t s = (hipStream_t)stream;
+    switch (c->p.ecc_type) {
+    case PPFS_ECC_NONE:
+        if (d_status) {
+            int r = check_hip(hipMemsetAsync(d_status, 0, nblocks, s), "status");
+            if (r)
+                return r;
+        }
+        if (d_data)
+            return check_hip(hipMemcpyAsync(d_data, d_raw, nblocks * c->raw, hipMemcpyDeviceToDevice, s), "copy");
+        return 0;
+    case PPFS_ECC_REED_SOLOMON:
+        if (c->rs_fast) {
+            if (!aligned16(d_raw) || (d_data && !aligned16(d_data)) || (d_status && !aligned16(d_status)))
+                return fail(PPFS_ECC_EINVAL, "rs decode: device pointers must be 16-byte aligned");
+            if (d_spill) {
+                int r = check_hip(hipMemsetAsync(d_spill, 0, nblocks * (256 - (size_t)c->rs_n), s), "spill");
+                if (r)
+                    return r;
+            }
+            return check_hip(
+                ppfs_rs_fast_decode(c->rs_t2, d_raw, d_data, d_status, nblocks, c->d_tables, write_back, s),
+                "rs decode");
+        }
+        return check_hip(ppfs_rs_generic_decode(d_raw, d_data, d_status, d_spill, nblocks, c->rs_n, c->rs_t2,
+                             write_back, c->d_tables, s),
+            "rs generic decode");
+    case PPFS_ECC_CRC:
+        return check_hip(ppfs_crc_check(d_raw, d_data, d_status, nblocks, c->raw, c->data, (uint32_t)c->crc_n,
+                             c->crc_mask, c->d_tables, s),
+            "crc check");
+    case PPFS_ECC_HAMMING:
+        if (!aligned16(d_raw))
+            return fail(PPFS_ECC_EINVAL, "hamming: raw pointer must be 16-byte aligned");
+        return check_hip(ppfs_ham_decode(d_raw, d_data, d_status, nblocks, write_back, c->raw, c->data, c->ham_L, s),
+            "hamming decode");
+    case PPFS_ECC_PARITY:
+        return check_hip(ppfs_parity_check(d_raw, d_data, d_status, nblocks, c->raw, s), "parity check");
+    }
+    return fail(PPFS_ECC_EINVAL, "bad ctx");
+}
+
+static int ensure_scratch(ppfs_ecc_ctx* c, size_t bytes)
+{
+    if (c->scratch_bytes >= bytes)
+        return 0;
+    if (c->d_scratch)
+        (void)hipFree(c->d_scratch);
+    c->d_scratch = nullptr;
+    c->scratch_bytes = 0;
+    HIP_TRY(hipMalloc(&c->d_scratch, bytes), "scratch alloc");
+    c->scratch_bytes = bytes;
+    return 0;
+}
+
+extern "C" int ppfs_ecc_write_device(ppfs_ecc_ctx* c, const uint8_t* d_data, uint8_t* d_raw, uint8_t* d_status,
+    size_t nblocks, void* stream)
+{
+    if (!c || (nblocks && (!d_data || !d_raw)))
+        return fail(PPFS_ECC_EINVAL, "write: null argument");
+    if (nblocks == 0)
+        return 0;
+    hipStream_t s = (hipStream_t)stream;
+    uint8_t* st = d_status;
+    if (!st) {
+        int r = ensure_scratch(c, (nblocks + 15) & ~(size_t)15);
+        if (r)
+            return r;
+        st = c->d_scratch;
+    }
+    int r = 0;
+    switch (c->p.ecc_type) {
+    case PPFS_ECC_NONE:
+        if (d_status && (r = check_hip(hipMemsetAsync(d_status, 0, nblocks, s), "status")))
+            return r;
+        return check_hip(hipMemcpyAsync(d_raw, d_data, nblocks * c->raw, hipMemcpyDeviceToDevice, s), "copy");
+    case PPFS_ECC_REED_SOLOMON:
+        // old block decoded for its status (correction event) only; the new codeword does
+        // not depend on it (rs_block_device.cpp:61-93)
+        if ((r = ppfs_ecc_decode_device(c, d_raw, nullptr, st, nblocks, 0, nullptr, stream)))
+            return r;
+        return ppfs_ecc_encode_device(c, d_data, d_raw, nblocks, stream);
+    case PPFS_ECC_CRC:
+        if ((r = check_hip(ppfs_crc_check(d_raw, nullptr, st, nblocks, c->raw, c->data, (uint32_t)c->crc_n,
+                               c->crc_mask, c->d_tables, s),
+                 "crc check")))
+            return r;
+        return check_hip(ppfs_crc_encode(d_data, d_raw, st, nblocks, c->raw, c->data, (uint32_t)c->crc_n,
+                             c->crc_mask, c->d_tables, s),
+            "crc encode");
+    case PPFS_ECC_HAMMING:
+        if ((r = ppfs_ecc_decode_device(c, d_raw, nullptr, st, nblocks, 1, nullptr, stream)))
+            return r;
+        return check_hip(ppfs_ham_encode(d_data, d_raw, st, nblocks, c->raw, c->data, c->ham_L, s), "hamming encode");
+    case PPFS_ECC_PARITY:
+        if ((r = check_hip(ppfs_parity_check(d_raw, nullptr, st, nblocks, c->raw, s), "parity check")))
+            return r;
+        return check_hip(ppfs_parity_encode(d_data, d_raw, st, nblocks, c->raw, s), "parity encode");
+    }
+    return fail(PPFS_ECC_EINVAL, "bad ctx");
+}
+
+// ---------------------------------------------------------------------------------------
+// Host-memory paths: chunked, double-buffered pinned staging, H2D / kernel / D2H overlapped.
+// ---------------------------------------------------------------------------------------
+static int ensure_staging(ppfs_ecc_ctx* c, size_t bytes)
+{
+    if (c->stage_bytes >= bytes)
+        return 0;
+    HIP_TRY(hipSetDevice(c->device), "set device");
+    for (int i = 0; i < 2; ++i) {
+        if (c->h_pin[i])
+            (void)hipHostFree(c->h_pin[i]);
+        if (c->d_stage[i])
+            (void)hipFree(c->d_stage[i]);
+        c->h_pin[i] = nullptr;
+        c->d_stage[i] = nullptr;
+        if (!c->hs[i])
+            HIP_TRY(hipStreamCreateWithFlags(&c->hs[i], hipStreamNonBlocking), "stream");
+        HIP_TRY(hipHostMalloc(&c->h_pin[i], bytes, hipHostMallocDefault), "pinned alloc");
+        HIP_TRY(hipMalloc(&c->d_stage[i], bytes), "stage alloc");
+    }
+    c->stage_bytes = bytes;
+    return 0;
+}
+
+namespace {
+constexpr size_t kChunkBlocks = 1u << 15; // 32 Ki blocks per chunk (~8 MiB of RS codewords)
+
+struct Layout { // offsets inside one staging buffer
+    size_t data, raw, status, spill, total;
+};
+
+Layout layout_for(const ppfs_ecc_ctx* c, size_t nb)
+{
+    Layout L {};
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    L.data = 0;
+    L.raw = al(L.data + nb * c->data);
+    L.status = al(L.raw + nb * c->raw);
+    L.spill = al(L.status + nb);
+    L.total = al(L.spill + nb * (256 - std::min<size_t>(c->raw, 255)));
+    return L;
+}
+} // namespace
+
+enum HostOp { OP_ENCODE, OP_DECODE, OP_WRITE };
+
+// Does encode read the old raw block?  (CRC tail bits, Hamming unused bits, parity fix byte)
+static bool raw_is_rmw(const ppfs_ecc_ctx* c)
+{
+    return c->p.ecc_type == PPFS_ECC_HAMMING || c->p.ecc_type == PPFS_ECC_PARITY
+        || (c->p.ecc_type == PPFS_ECC_CRC && (c->crc_n % 8) != 0);
+}
+
+static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t* data_out, uint8_t* raw,
+    uint8_t* status, uint8_t* spill, size_t nblocks, int write_back)
+{
+    if (!c)
+        return fail(PPFS_ECC_EINVAL, "null ctx");
+    if (nblocks == 0)
+        return 0;
+    const size_t chunk = std::min(nblocks, kChunkBlocks);
+    const Layout L = layout_for(c, chunk);
+    int r = ensure_staging(c, L.total);
+    if (r)
+        return r;
+    HIP_TRY(hipSetDevice(c->device), "set device");
+    const size_t spill_b = 256 - std::min<size_t>(c->raw, 255);
+    size_t pending_first[2] = { 0, 0 }, pending_n[2] = { 0, 0 };
+    bool busy[2] = { false, false };
+
+    auto drain = [&](int i) -> int {
+        if (!busy[i])
+            return 0;
+        HIP_TRY(hipStreamSynchronize(c->hs[i]), "sync");
+        const size_t b0 = pending_first[i], nb = pending_n[i];
+        uint8_t* h = c->h_pin[i];
+        if (op == OP_ENCODE || op == OP_WRITE || write_back)
+            std::memcpy(raw + b0 * c->raw, h + L.raw, nb * c->raw);
+        if (op == OP_DECODE && data_out)
+            std::memcpy(data_out + b0 * c->data, h + L.data, nb * c->data);
+        if (status)
+            std::memcpy(status + b0, h + L.status, nb);
+        if (spill)
+            std::memcpy(spill + b0 * spill_b, h + L.spill, nb * spill_b);
+        busy[i] = false;
+        return 0;
+    };
+
+    int slot = 0;
+    for (size_t b0 = 0; b0 < nblocks; b0 += chunk, slot ^= 1) {
+        const size_t nb = std::min(chunk, nblocks - b0);
+        if ((r = drain(slot)))
+            return r;
+        uint8_t* h = c->h_pin[slot];
+        uint8_t* d = c->d_stage[slot];
+        hipStream_t s = c->hs[slot];
+        // inputs host -> pinned -> device (data and raw regions are adjacent in the layout)
+        const bool need_data = op == OP_ENCODE || op == OP_WRITE;
+        const bool need_raw = op != OP_ENCODE || raw_is_rmw(c);
+        if (need_data)
+            std::memcpy(h + L.data, data_in + b0 * c->data, nb * c->data);
+        if (need_raw)
+            std::memcpy(h + L.raw, raw + b0 * c->raw, nb * c->raw);
+        const size_t in_lo = need_data ? L.data : L.raw;
+        const size_t in_hi = need_raw ? L.raw + nb * c->raw : L.data + nb * c->data;
+        HIP_TRY(hipMemcpyAsync(d + in_lo, h + in_lo, in_hi - in_lo, hipMemcpyHostToDevice, s), "H2D");
+        switch (op) {
+        case OP_ENCODE:
+            r = ppfs_ecc_encode_device(c, d + L.data, d + L.raw, nb, s);
+            break;
+        case OP_WRITE:
+            r = ppfs_ecc_write_device(c, d + L.data, d + L.raw, d + L.status, nb, s);
+            break;
+        case OP_DECODE:
+            r = ppfs_ecc_decode_device(c, d + L.raw, data_out ? d + L.data : nullptr, d + L.status, nb, write_back,
+                spill ? d + L.spill : nullptr, s);
+            break;
+        }
+        if (r)
+            return r;
+        // outputs device -> pinned
+        if (op == OP_ENCODE || op == OP_WRITE || write_back)
+            HIP_TRY(hipMemcpyAsync(h + L.raw, d + L.raw, nb * c->raw, hipMemcpyDeviceToHost, s), "D2H raw");
+        if (op == OP_DECODE && data_out)
+            HIP_TRY(hipMemcpyAsync(h + L.data, d + L.data, nb * c->data, hipMemcpyDeviceToHost, s), "D2H data");
+        if (status && (op != OP_ENCODE))
+            HIP_TRY(hipMemcpyAsync(h + L.status, d + L.status, nb, hipMemcpyDeviceToHost, s), "D2H status");
+        if (spill)
+            HIP_TRY(hipMemcpyAsync(h + L.spill, d + L.spill, nb * spill_b, hipMemcpyDeviceToHost, s), "D2H spill");
+        pending_first[slot] = b0;
+        pending_n[slot] = nb;
+        busy[slot] = true;
+    }
+    if ((r = drain(0)))
+        return r;
+    return drain(1);
+}
+
+extern "C" int ppfs_ecc_encode_host(ppfs_ecc_ctx* c, const uint8_t* data, uint8_t* raw, size_t nblocks)
+{
+    return host_run(c, OP_ENCODE, data, nullptr, raw, nullptr, nullptr, nblocks, 0);
+}
+
+extern "C" int ppfs_ecc_decode_host(ppfs_ecc_ctx* c, uint8_t* raw, uint8_t* data, uint8_t* status, size_t nblocks,
+    int write_back, uint8_t* spill)
+{
+    return host_run(c, OP_DECODE, nullptr, data, raw, status, spill, nblocks, write_back);
+}
+
+extern "C" int ppfs_ecc_write_host(ppfs_ecc_ctx* c, const uint8_t* data, uint8_t* raw, uint8_t* status, size_t nblocks)
+{
+    return host_run(c, OP_WRITE, data, nullptr, raw, status, nullptr, nblocks, 0);
+}

@@ -1,0 +1,110 @@
+"""EccEngine: one codec context on one GPU (wraps ppfs_ecc_ctx from include/ppfs_ecc.h).
+
+Device-resident calls take torch uint8 CUDA tensors (HBM buffers, packed blocks) and enqueue
+the HIP kernels on the current torch stream; host calls take numpy uint8 arrays and go through
+the library's pinned, double-buffered staging.  torch is used only as the HBM allocator and
+stream provider.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_void_p
+from typing import Optional
+
+import numpy as np
+
+from . import _native
+from ._native import EccParams, check, lib
+
+
+def _ptr(x) -> Optional[int]:
+    """Device/host address of a torch tensor or numpy array (None passes NULL)."""
+    if x is None:
+        return None
+    if isinstance(x, np.ndarray):
+        if not x.flags["C_CONTIGUOUS"] or x.dtype != np.uint8:
+            raise ValueError("numpy buffers must be C-contiguous uint8")
+        return x.ctypes.data
+    # torch tensor
+    if not x.is_contiguous() or x.element_size() != 1:
+        raise ValueError("tensors must be contiguous uint8")
+    return x.data_ptr()
+
+
+def _stream_handle(stream) -> Optional[int]:
+    if stream is not None:
+        return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+    import torch
+
+    return torch.cuda.current_stream().cuda_stream
+
+
+class EccEngine:
+    """Codec context: params follow PpFS::_createAppropriateBlockDevice (ppfs.cpp:35-70)."""
+
+    def __init__(self, ecc_type: int, block_size: int, rs_correctable_bytes: int = 3,
+                 crc_polynomial_explicit: int = 0, device: int = 0):
+        p = EccParams(int(ecc_type), int(block_size), int(rs_correctable_bytes), 0, int(crc_polynomial_explicit))
+        h = c_void_p()
+        check(lib().ppfs_ecc_create(byref(p), int(device), byref(h)))
+        self._h = h
+        self.ecc_type = int(ecc_type)
+        self.block_size = int(block_size)
+        self.device = int(device)
+        self.raw_block_size = int(lib().ppfs_ecc_raw_block_size(h))
+        self.data_size = int(lib().ppfs_ecc_data_size(h))
+        self.kernel_name = lib().ppfs_ecc_kernel_name(h).decode()
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().ppfs_ecc_destroy(self._h)
+            self._h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------- device-resident batches (torch CUDA uint8 tensors) ----------------
+    def encode(self, data, raw, nblocks: Optional[int] = None, stream=None) -> None:
+        n = nblocks if nblocks is not None else data.numel() // self.data_size
+        check(lib().ppfs_ecc_encode_device(self._h, _ptr(data), _ptr(raw), n, _stream_handle(stream)))
+
+    def decode(self, raw, data=None, status=None, write_back: bool = True, spill=None,
+               nblocks: Optional[int] = None, stream=None) -> None:
+        n = nblocks if nblocks is not None else raw.numel() // self.raw_block_size
+        check(lib().ppfs_ecc_decode_device(self._h, _ptr(raw), _ptr(data), _ptr(status), n, int(bool(write_back)),
+                                           _ptr(spill), _stream_handle(stream)))
+
+    def write(self, data, raw, status=None, nblocks: Optional[int] = None, stream=None) -> None:
+        n = nblocks if nblocks is not None else data.numel() // self.data_size
+        check(lib().ppfs_ecc_write_device(self._h, _ptr(data), _ptr(raw), _ptr(status), n,
+                                          _stream_handle(stream)))
+
+    # ---------------- host-memory batches (numpy uint8) ----------------
+    def encode_host(self, data: np.ndarray, raw: np.ndarray) -> None:
+        n = data.size // self.data_size
+        assert raw.size >= n * self.raw_block_size
+        check(lib().ppfs_ecc_encode_host(self._h, _ptr(data), _ptr(raw), n))
+
+    def decode_host(self, raw: np.ndarray, data: Optional[np.ndarray] = None, status: Optional[np.ndarray] = None,
+                    write_back: bool = True, spill: Optional[np.ndarray] = None) -> None:
+        n = raw.size // self.raw_block_size
+        check(lib().ppfs_ecc_decode_host(self._h, _ptr(raw), _ptr(data), _ptr(status), n, int(bool(write_back)),
+                                         _ptr(spill)))
+
+    def write_host(self, data: np.ndarray, raw: np.ndarray, status: Optional[np.ndarray] = None) -> None:
+        n = data.size // self.data_size
+        check(lib().ppfs_ecc_write_host(self._h, _ptr(data), _ptr(raw), _ptr(status), n))
+
+    def spill_bytes_per_block(self) -> int:
+        return 256 - min(self.raw_block_size, 255)
+
+
+def crc_implicit_to_explicit(p: int) -> int:
+    """CrcPolynomial::MsgImplicit (crc_polynomial.cpp:41-54) -> explicit form."""
+    return int(lib().ppfs_ecc_crc_implicit_to_explicit(ctypes.c_uint64(p)))
+
+
+__all__ = ["EccEngine", "crc_implicit_to_explicit", "_native"]

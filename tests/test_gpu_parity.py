@@ -1,0 +1,330 @@
+"""GPU parity tests: HIP kernels (through the C ABI) vs the CPU oracle, bit-exact.
+
+Every case compares the device results with oracle/ppfs_oracle.c on the same seeded inputs:
+codewords / raw blocks, payloads, per-block status, write-back bytes (and RS spill for
+shortened codes).  Edge cases follow the reference tests: 0..t+3 byte errors for RS
+(miscorrection included), 0..3 bit flips for Hamming (parity, data and unused tail bits),
+CRC flips including the undetected last payload bit, ragged batch sizes.
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+from tests.conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+if gpu_available():
+    import torch
+
+from paritypartyfs_amd import (ECC_CRC, ECC_HAMMING, ECC_NONE, ECC_PARITY, ECC_REED_SOLOMON, EccEngine)
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def rng_for(*k):
+    return np.random.default_rng(zlib.crc32(repr(k).encode()))
+
+
+# ------------------------------------------------------------------------------------
+# Reed-Solomon
+# ------------------------------------------------------------------------------------
+RS_CASES = [(512, 3), (255, 1), (255, 2), (256, 4), (1024, 5), (4096, 8), (4096, 16),  # fast path
+            (255, 6), (255, 7), (64, 3), (128, 10), (32, 1)]                           # generic path
+
+
+@pytest.mark.parametrize("bs,t", RS_CASES, ids=lambda x: str(x))
+@pytest.mark.parametrize("nblocks", [1, 300, 1024, 2333])
+def test_rs_encode_matches_oracle(oracle, bs, t, nblocks):
+    n, k, tt = oracle.rs_sizes(bs, t)
+    eng = EccEngine(ECC_REED_SOLOMON, bs, t)
+    assert (eng.raw_block_size, eng.data_size) == (n, k)
+    rng = rng_for("rse", bs, t, nblocks)
+    data = rng.integers(0, 256, nblocks * k, dtype=np.uint8)
+    if nblocks > 2:  # all-zero and all-0xFF payloads
+        data[:k] = 0
+        data[k:2 * k] = 0xFF
+    raw = torch.zeros(nblocks * n, dtype=torch.uint8, device="cuda")
+    eng.encode(dev(data), raw, nblocks=nblocks)
+    assert np.array_equal(host(raw), oracle.rs_encode(bs, t, data))
+
+
+def inject_rs(rng, cw, n, t, nblocks):
+    bad = cw.copy().reshape(nblocks, n)
+    for b in range(nblocks):
+        ne = b % (t + 4)  # 0..t+3 errors
+        pos = rng.choice(n, min(ne, n), replace=False)
+        bad[b, pos] ^= rng.integers(1, 256, pos.size, dtype=np.uint8)
+    return bad.reshape(-1)
+
+
+@pytest.mark.parametrize("bs,t", RS_CASES, ids=lambda x: str(x))
+@pytest.mark.parametrize("nblocks", [300, 1024])
+def test_rs_decode_matches_oracle(oracle, bs, t, nblocks):
+    n, k, _ = oracle.rs_sizes(bs, t)
+    eng = EccEngine(ECC_REED_SOLOMON, bs, t)
+    rng = rng_for("rsd", bs, t, nblocks)
+    data = rng.integers(0, 256, nblocks * k, dtype=np.uint8)
+    cw = oracle.rs_encode(bs, t, data)
+    bad = inject_rs(rng, cw, n, t, nblocks)
+    o_data, o_st, o_fixed, o_wbl, rc = oracle.rs_decode(bs, t, bad)
+    assert rc == 0
+    raw_d = dev(bad)
+    data_d = torch.zeros(nblocks * k, dtype=torch.uint8, device="cuda")
+    st_d = torch.full((nblocks,), 77, dtype=torch.uint8, device="cuda")
+    spill_d = torch.zeros(nblocks * eng.spill_bytes_per_block(), dtype=torch.uint8, device="cuda")
+    eng.decode(raw_d, data_d, st_d, write_back=True, spill=spill_d, nblocks=nblocks)
+    assert np.array_equal(host(st_d), o_st)
+    assert np.array_equal(host(data_d), o_data)
+    assert np.array_equal(host(raw_d), o_fixed)  # in-place write-back == reference's written bytes
+    sp = host(spill_d).reshape(nblocks, -1)
+    for b in range(nblocks):
+        extra = max(0, int(o_wbl[b]) - n)
+        assert sp[b, 0] == extra
+    # <= t errors are always corrected to the original payload
+    okb = np.array([b % (t + 4) <= t for b in range(nblocks)])
+    assert np.array_equal(host(data_d).reshape(nblocks, k)[okb], data.reshape(nblocks, k)[okb])
+
+
+def test_rs_decode_no_writeback_and_status_only(oracle):
+    bs, t, nb = 512, 3, 777
+    n, k, _ = oracle.rs_sizes(bs, t)
+    eng = EccEngine(ECC_REED_SOLOMON, bs, t)
+    rng = rng_for("rsnw")
+    cw = oracle.rs_encode(bs, t, rng.integers(0, 256, nb * k, dtype=np.uint8))
+    bad = inject_rs(rng, cw, n, t, nb)
+    o_data, o_st, _, _, _ = oracle.rs_decode(bs, t, bad)
+    raw_d = dev(bad)
+    st_d = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+    eng.decode(raw_d, None, st_d, write_back=False, nblocks=nb)
+    assert np.array_equal(host(st_d), o_st)
+    assert np.array_equal(host(raw_d), bad)
+
+
+def test_rs_generic_spill_matches_oracle(oracle):
+    """Shortened code (n = 64): miscorrections past the block are reported in the spill."""
+    bs, t, nb = 64, 3, 600
+    n, k, _ = oracle.rs_sizes(bs, t)
+    eng = EccEngine(ECC_REED_SOLOMON, bs, t)
+    rng = rng_for("spill")
+    cw = oracle.rs_encode(bs, t, rng.integers(0, 256, nb * k, dtype=np.uint8)).reshape(nb, n)
+    for b in range(nb):
+        pos = rng.choice(n, 5, replace=False)
+        cw[b, pos] ^= rng.integers(1, 256, 5, dtype=np.uint8)
+    bad = cw.reshape(-1)
+    spill_d = torch.zeros(nb * eng.spill_bytes_per_block(), dtype=torch.uint8, device="cuda")
+    eng.decode(dev(bad), None, None, write_back=False, spill=spill_d, nblocks=nb)
+    sp = host(spill_d).reshape(nb, -1)
+    nspill = 0
+    for b in range(nb):
+        st, _, fixed, wl, _ = oracle.rs_decode_one_full(bs, t, bad[b * n:(b + 1) * n])
+        extra = max(0, wl - n)
+        assert sp[b, 0] == extra
+        assert sp[b, 1:1 + extra].tobytes() == fixed[n:n + extra].tobytes()
+        nspill += extra > 0
+    assert nspill > 0
+
+
+# ------------------------------------------------------------------------------------
+# CRC
+# ------------------------------------------------------------------------------------
+CRC_CASES = [(0xea, 256), (0xc1acf, 512), (0x9960034c, 512), (0x9960034c, 4096), (0x5, 64), (0x3, 256),
+             (0x42F0E1EBA9EA3693 >> 1, 1024), (0x1021 >> 1, 4096)]
+
+
+@pytest.mark.parametrize("imp,bs", CRC_CASES, ids=lambda x: hex(x) if x > 4096 else str(x))
+def test_crc_encode_check_match_oracle(oracle, imp, bs):
+    P = oracle.crc_explicit(imp)
+    eng = EccEngine(ECC_CRC, bs, crc_polynomial_explicit=P)
+    ds = oracle.crc_data_size(bs, P)
+    assert (eng.raw_block_size, eng.data_size) == (bs, ds)
+    nb = 257 if bs >= 1024 else 1001
+    rng = rng_for("crc", imp, bs)
+    data = rng.integers(0, 256, nb * ds, dtype=np.uint8)
+    old = rng.integers(0, 256, nb * bs, dtype=np.uint8)  # tail bits must survive
+    exp = oracle.crc_encode(bs, P, data, raw_old=old)
+    raw_d = dev(old)
+    eng.encode(dev(data), raw_d, nblocks=nb)
+    got = host(raw_d)
+    assert np.array_equal(got, exp)
+    # flips: none / random bit / last payload bit (undetected) / CRC field bit
+    bad = got.reshape(nb, bs).copy()
+    for b in range(nb):
+        kind = b % 4
+        if kind == 1:
+            f = int(rng.integers(0, bs * 8))
+        elif kind == 2:
+            f = ds * 8 - 1
+        elif kind == 3:
+            f = ds * 8 + int(rng.integers(0, P.bit_length() - 1))
+        else:
+            continue
+        bad[b, f // 8] ^= 0x80 >> (f % 8)
+    bad = bad.reshape(-1)
+    o_data, o_st = oracle.crc_check(bs, P, bad)
+    data_d = torch.zeros(nb * ds, dtype=torch.uint8, device="cuda")
+    st_d = torch.full((nb,), 77, dtype=torch.uint8, device="cuda")
+    eng.decode(dev(bad), data_d, st_d, nblocks=nb)
+    assert np.array_equal(host(st_d), o_st)
+    assert np.array_equal(host(data_d), o_data)
+    assert (o_st[2::4] == 0).all()  # last payload bit flips pass the check (reference quirk)
+
+
+# ------------------------------------------------------------------------------------
+# Hamming
+# ------------------------------------------------------------------------------------
+@pytest.mark.parametrize("bs", [8, 16, 64, 256, 512, 4096])
+def test_hamming_matches_oracle(oracle, bs):
+    eng = EccEngine(ECC_HAMMING, bs)
+    ds = oracle.ham_data_size(bs)
+    assert (eng.raw_block_size, eng.data_size) == (bs, ds)
+    nb = 300 if bs >= 4096 else 1000
+    rng = rng_for("ham", bs)
+    data = rng.integers(0, 256, nb * ds, dtype=np.uint8)
+    old = rng.integers(0, 256, nb * bs, dtype=np.uint8)
+    exp = oracle.ham_encode(bs, data, raw_old=old)
+    raw_d = dev(old)
+    eng.encode(dev(data), raw_d, nblocks=nb)
+    got = host(raw_d)
+    assert np.array_equal(got, exp)
+    bad = got.reshape(nb, bs).copy()
+    for b in range(nb):
+        nf = b % 4
+        for f in rng.choice(bs * 8, nf, replace=False):
+            bad[b, f // 8] ^= 0x80 >> (f % 8)
+    bad = bad.reshape(-1)
+    o_data, o_st, o_fixed, _ = oracle.ham_decode(bs, bad)
+    raw_d = dev(bad)
+    data_d = torch.zeros(nb * ds, dtype=torch.uint8, device="cuda")
+    st_d = torch.full((nb,), 77, dtype=torch.uint8, device="cuda")
+    eng.decode(raw_d, data_d, st_d, write_back=True, nblocks=nb)
+    st = host(st_d)
+    assert np.array_equal(st, o_st)
+    assert np.array_equal(host(raw_d), o_fixed)
+    ok = st != 5
+    assert np.array_equal(host(data_d).reshape(nb, ds)[ok], o_data.reshape(nb, ds)[ok])
+
+
+# ------------------------------------------------------------------------------------
+# Parity and raw
+# ------------------------------------------------------------------------------------
+@pytest.mark.parametrize("bs", [2, 16, 255, 256, 4096])
+def test_parity_matches_oracle(oracle, bs):
+    eng = EccEngine(ECC_PARITY, bs)
+    nb = 999
+    rng = rng_for("par", bs)
+    data = rng.integers(0, 256, nb * (bs - 1), dtype=np.uint8)
+    old = rng.integers(0, 256, nb * bs, dtype=np.uint8)
+    exp = oracle.parity_encode(bs, data, raw_old=old)
+    raw_d = dev(old)
+    eng.encode(dev(data), raw_d, nblocks=nb)
+    got = host(raw_d)
+    assert np.array_equal(got, exp)
+    bad = got.reshape(nb, bs).copy()
+    bad[1::3, 0] ^= 0x10
+    bad = bad.reshape(-1)
+    o_data, o_st = oracle.parity_check(bs, bad)
+    data_d = torch.zeros(nb * (bs - 1), dtype=torch.uint8, device="cuda")
+    st_d = torch.full((nb,), 77, dtype=torch.uint8, device="cuda")
+    eng.decode(dev(bad), data_d, st_d, nblocks=nb)
+    assert np.array_equal(host(st_d), o_st)
+    assert np.array_equal(host(data_d), o_data)
+
+
+def test_raw_copy():
+    eng = EccEngine(ECC_NONE, 512)
+    x = torch.randint(0, 256, (512 * 10,), dtype=torch.uint8, device="cuda")
+    y = torch.zeros_like(x)
+    eng.encode(x, y)
+    assert torch.equal(x, y)
+
+
+# ------------------------------------------------------------------------------------
+# writeBlock (read-modify-write) batches
+# ------------------------------------------------------------------------------------
+@pytest.mark.parametrize("codec", ["rs", "crc", "hamming", "parity"])
+def test_write_rmw_matches_oracle(oracle, codec):
+    rng = rng_for("rmw", codec)
+    nb = 500
+    if codec == "rs":
+        bs, t = 512, 3
+        n, k, _ = oracle.rs_sizes(bs, t)
+        eng = EccEngine(ECC_REED_SOLOMON, bs, t)
+        old = inject_rs(rng, oracle.rs_encode(bs, t, rng.integers(0, 256, nb * k, dtype=np.uint8)), n, t, nb)
+        data = rng.integers(0, 256, nb * k, dtype=np.uint8)
+        _, o_st, _, _, _ = oracle.rs_decode(bs, t, old)
+        exp = oracle.rs_encode(bs, t, data)
+    elif codec == "crc":
+        bs, P = 512, oracle.crc_explicit(0xc1acf)  # degree 20: tail bits in play
+        ds = oracle.crc_data_size(bs, P)
+        eng = EccEngine(ECC_CRC, bs, crc_polynomial_explicit=P)
+        old = oracle.crc_encode(bs, P, rng.integers(0, 256, nb * ds, dtype=np.uint8),
+                                raw_old=rng.integers(0, 256, nb * bs, dtype=np.uint8)).reshape(nb, bs)
+        old[::3, 7] ^= 1
+        old = old.reshape(-1)
+        data = rng.integers(0, 256, nb * ds, dtype=np.uint8)
+        _, o_st = oracle.crc_check(bs, P, old)
+        enc = oracle.crc_encode(bs, P, data, raw_old=old).reshape(nb, bs)
+        exp = np.where((o_st == 5)[:, None], old.reshape(nb, bs), enc).reshape(-1)
+    elif codec == "hamming":
+        bs = 512
+        ds = oracle.ham_data_size(bs)
+        eng = EccEngine(ECC_HAMMING, bs)
+        old = oracle.ham_encode(bs, rng.integers(0, 256, nb * ds, dtype=np.uint8),
+                                raw_old=rng.integers(0, 256, nb * bs, dtype=np.uint8)).reshape(nb, bs)
+        for b in range(nb):
+            for f in rng.choice(bs * 8, b % 3, replace=False):
+                old[b, f // 8] ^= 0x80 >> (f % 8)
+        old = old.reshape(-1)
+        data = rng.integers(0, 256, nb * ds, dtype=np.uint8)
+        _, o_st, o_fixed, _ = oracle.ham_decode(bs, old)
+        enc = oracle.ham_encode(bs, data, raw_old=o_fixed).reshape(nb, bs)
+        exp = np.where((o_st == 5)[:, None], old.reshape(nb, bs), enc).reshape(-1)
+    else:
+        bs = 256
+        eng = EccEngine(ECC_PARITY, bs)
+        old = oracle.parity_encode(bs, rng.integers(0, 256, nb * (bs - 1), dtype=np.uint8)).reshape(nb, bs)
+        old[::4, 3] ^= 2
+        old = old.reshape(-1)
+        data = rng.integers(0, 256, nb * (bs - 1), dtype=np.uint8)
+        _, o_st = oracle.parity_check(bs, old)
+        enc = oracle.parity_encode(bs, data, raw_old=old).reshape(nb, bs)
+        exp = np.where((o_st == 5)[:, None], old.reshape(nb, bs), enc).reshape(-1)
+    raw_d = dev(old)
+    st_d = torch.full((nb,), 77, dtype=torch.uint8, device="cuda")
+    eng.write(dev(data), raw_d, st_d, nblocks=nb)
+    assert np.array_equal(host(st_d), o_st)
+    assert np.array_equal(host(raw_d), exp)
+
+
+# ------------------------------------------------------------------------------------
+# host-memory path (pinned staging, several chunks)
+# ------------------------------------------------------------------------------------
+def test_host_path_multichunk(oracle):
+    bs, t, nb = 512, 3, 70001
+    n, k, _ = oracle.rs_sizes(bs, t)
+    eng = EccEngine(ECC_REED_SOLOMON, bs, t)
+    rng = rng_for("host")
+    data = rng.integers(0, 256, nb * k, dtype=np.uint8)
+    raw = np.zeros(nb * n, np.uint8)
+    eng.encode_host(data, raw)
+    sample = rng.choice(nb, 2000, replace=False)
+    ref = oracle.rs_encode(bs, t, data.reshape(nb, k)[sample].reshape(-1)).reshape(-1, n)
+    assert np.array_equal(raw.reshape(nb, n)[sample], ref)
+    bad = raw.reshape(nb, n).copy()
+    bad[np.arange(nb), rng.integers(0, n, nb)] ^= rng.integers(1, 256, nb, dtype=np.uint8)
+    bad = bad.reshape(-1)
+    out = np.zeros(nb * k, np.uint8)
+    st = np.zeros(nb, np.uint8)
+    eng.decode_host(bad, out, st, write_back=True)
+    assert (st == 1).all()
+    assert np.array_equal(out, data)
+    assert np.array_equal(bad, raw)

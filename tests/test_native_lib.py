@@ -1,0 +1,66 @@
+"""CPU tests of the C-ABI library: it loads, exports every symbol include/*.h declares, and
+validates parameters without touching the GPU.  No compute calls (no GPU here)."""
+import ctypes
+import glob
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "paritypartyfs_amd", "_lib", "libppfs_ecc.so")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        subprocess.run(["make", "-j8", "-C", os.path.join(ROOT, "paritypartyfs_amd", "csrc")], check=True,
+                       capture_output=True)
+    from paritypartyfs_amd import _native
+    return _native.lib()
+
+
+def declared_functions():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b(ppfs_\w+)\s*\(", src, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_header_declares_the_abi():
+    names = declared_functions()
+    from paritypartyfs_amd._native import EXPORTED_SYMBOLS
+    assert names == set(EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol(lib):
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True).stdout
+    for name in declared_functions():
+        assert re.search(rf"\bT {name}$", out, flags=re.M), name
+
+
+def test_library_has_gfx950_code_object():
+    data = open(LIB, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    secs = subprocess.run(["readelf", "-S", LIB], capture_output=True, text=True).stdout
+    assert ".hip_fatbin" in secs
+
+
+def test_param_validation_without_gpu(lib):
+    from paritypartyfs_amd._native import EccParams
+    h = ctypes.c_void_p()
+    bad = [EccParams(4, 0, 3, 0, 0), EccParams(4, 8192, 3, 0, 0), EccParams(9, 512, 3, 0, 0),
+           EccParams(1, 512, 0, 0, 1), EccParams(2, 4, 0, 0, 0), EccParams(3, 1, 0, 0, 0)]
+    for p in bad:
+        assert lib.ppfs_ecc_create(ctypes.byref(p), 0, ctypes.byref(h)) == -22
+        assert lib.ppfs_ecc_last_error()
+
+
+def test_crc_implicit_to_explicit(lib):
+    assert lib.ppfs_ecc_crc_implicit_to_explicit(0xad0424f3) == 0x15a0849e7
