@@ -1,0 +1,284 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident RS encode+decode throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]/[2]): ecc_type=reed_solomon, block_size=512,
+rs_correctable_bytes=3 -> RS(255,249) (the reference clamps codewords to 255 B,
+rs_block_device.cpp:57), 2^20 blocks per GPU, synthetic uniform payloads.
+
+One step = encode(2^20 payloads -> codewords)            [rs255 encode kernel]
+         + inject exactly one byte error into every codeword (torch gather/scatter)
+         + decode(codewords -> payloads, status, in-place write-back)   [rs255 decode kernel]
+value = algorithmic bytes of all ranks (encode 504 B + decode 504 B per block) / step time.
+
+Multi-GPU: one process per GPU (torchrun).  Blocks are independent, so each rank owns its own
+2^20-block shard ("scaling": "weak"); the only collectives are the barrier around the timed
+region and the max-over-ranks of the elapsed time (not on the data path).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--blocks", type=int, default=1 << 20, help="blocks per GPU")
+    ap.add_argument("--block-size", type=int, default=512)
+    ap.add_argument("--t", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-blocks", type=int, default=1 << 18)
+    ap.add_argument("--host-inclusive", action="store_true", help="also time the pinned H2D+kernel+D2H path")
+    ap.add_argument("--verify", action="store_true", help="check a sample of outputs against the oracle")
+    return ap.parse_args()
+
+
+def cpu_baseline(bs, t, nblocks, seed=1234):
+    """Oracle ('port') timed on host cores over a bounded sample (rank 0, N=1 only)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from tests.oracle_lib import Oracle
+
+    o = Oracle()
+    n, k, _ = o.rs_sizes(bs, t)
+    rng = np.random.default_rng(seed)
+    data = rng.integers(0, 256, nblocks * k, dtype=np.uint8)
+    cores = min(16, os.cpu_count() or 1)
+    parts = np.array_split(np.arange(nblocks), cores)
+    bufs = []
+    for p in parts:
+        bufs.append(np.ascontiguousarray(data.reshape(nblocks, k)[p]).reshape(-1))
+    pos = rng.integers(0, n, nblocks)
+    val = rng.integers(1, 256, nblocks, dtype=np.uint8)
+    o.rs_encode(bs, t, data[:k])  # tables initialised before threads start
+
+    def enc(i):
+        return o.rs_encode(bs, t, bufs[i])
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(cores) as ex:
+        cws = list(ex.map(enc, range(cores)))
+    t_enc = time.perf_counter() - t0
+    bads = []
+    for i, p in enumerate(parts):
+        c = cws[i].reshape(-1, n).copy()
+        c[np.arange(len(p)), pos[p]] ^= val[p]
+        bads.append(c.reshape(-1))
+
+    def dec(i):
+        return o.rs_decode(bs, t, bads[i])
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(cores) as ex:
+        list(ex.map(dec, range(cores)))
+    t_dec = time.perf_counter() - t0
+    alg = (k + n) * nblocks
+    return {
+        "value": round(2 * alg / (t_enc + t_dec) / GIB, 4),
+        "unit": "GiB/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": f"{nblocks} RS(255,249) blocks: encode + 1-byte-error decode, oracle/ppfs_oracle.c "
+                  f"on {cores} host threads over disjoint block ranges",
+        "encode_blocks_per_s": round(nblocks / t_enc),
+        "decode_blocks_per_s": round(nblocks / t_dec),
+    }
+
+
+def load_traffic(path=os.path.join(ROOT, "profiles", "pmc_latest.json")):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from paritypartyfs_amd import ECC_REED_SOLOMON, EccEngine
+
+    eng = EccEngine(ECC_REED_SOLOMON, args.block_size, args.t, device=dev.index)
+    n, k = eng.raw_block_size, eng.data_size
+    nb = args.blocks
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(0x50504653 ^ rank)  # "PPFS" ^ rank
+    data = torch.randint(0, 256, (nb * k,), dtype=torch.uint8, device=dev, generator=gen)
+    cw = torch.empty(nb * n, dtype=torch.uint8, device=dev)
+    out = torch.empty(nb * k, dtype=torch.uint8, device=dev)
+    status = torch.empty(nb, dtype=torch.uint8, device=dev)
+    # one error per codeword: position uniform in [0,255), value uniform in [1,255]
+    err_pos = (torch.arange(nb, device=dev, dtype=torch.int64) * n
+               + torch.randint(0, n, (nb,), device=dev, generator=gen))
+    err_val = torch.randint(1, 256, (nb,), dtype=torch.uint8, device=dev, generator=gen)
+    stream = torch.cuda.current_stream()
+
+    def inject():
+        cw[err_pos] = cw[err_pos] ^ err_val
+
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+
+    def step(timed):
+        if timed:
+            ev[0].record(stream)
+        eng.encode(data, cw, nblocks=nb)
+        if timed:
+            ev[1].record(stream)
+        inject()
+        if timed:
+            ev[2].record(stream)
+        eng.decode(cw, out, status, write_back=True, nblocks=nb)
+        if timed:
+            ev[3].record(stream)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if args.warmup > 0:
+        # cheap device-side self-check of the last warmup step: every block corrected, payload restored
+        ok = bool(torch.equal(out, data)) and int(status.min()) == 1 and int(status.max()) == 1
+        if not ok:
+            print(json.dumps({"error": "verification failed"}), file=sys.stderr)
+            sys.exit(3)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(False)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # kernel durations: re-run K steps with events recorded around each phase (same stream)
+    enc_ms, inj_ms, dec_ms = [], [], []
+    for _ in range(args.steps):
+        step(True)
+        ev[3].synchronize()
+        enc_ms.append(ev[0].elapsed_time(ev[1]))
+        inj_ms.append(ev[1].elapsed_time(ev[2]))
+        dec_ms.append(ev[2].elapsed_time(ev[3]))
+    enc_avg, dec_avg, inj_avg = float(np.mean(enc_ms)), float(np.mean(dec_ms)), float(np.mean(inj_ms))
+
+    # device copy reference peak (same bytes as one encode: read k, write n per block)
+    cp_src = torch.empty(nb * (k + n) // 2, dtype=torch.uint8, device=dev)
+    cp_dst = torch.empty_like(cp_src)
+    for _ in range(3):
+        cp_dst.copy_(cp_src)
+    ev[4].record(stream)
+    for _ in range(10):
+        cp_dst.copy_(cp_src)
+    ev[5].record(stream)
+    ev[5].synchronize()
+    copy_gbs = 2 * cp_src.numel() / (ev[4].elapsed_time(ev[5]) / 10 * 1e-3) / 1e9
+    del cp_src, cp_dst
+
+    alg_per_block = k + n  # 504 B for RS(255,249), both for encode and decode
+    total_bytes = 2 * alg_per_block * nb * world * args.steps
+    value = total_bytes / elapsed / GIB
+    ms_per_step = elapsed / args.steps * 1e3
+
+    dom_ms = max(enc_avg, dec_avg)
+    dom_name = "rs255_decode_kernel<6>" if dec_avg >= enc_avg else "rs255_encode_kernel<6>"
+    achieved = alg_per_block * nb / (dom_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = load_traffic()
+    if pmc and pmc.get("kernel") == dom_name and pmc.get("blocks") == nb:
+        traffic = pmc.get("hbm_bytes_per_launch")
+
+    host_incl = None
+    if args.host_inclusive and rank == 0:
+        hd = data.cpu().numpy()
+        hraw = np.empty(nb * n, np.uint8)
+        hout = np.empty(nb * k, np.uint8)
+        hst = np.empty(nb, np.uint8)
+        eng.encode_host(hd, hraw)
+        t1 = time.perf_counter()
+        eng.encode_host(hd, hraw)
+        t2 = time.perf_counter()
+        eng.decode_host(hraw, hout, hst, write_back=True)
+        t3 = time.perf_counter()
+        host_incl = {"encode_GiBps": round(alg_per_block * nb / (t2 - t1) / GIB, 3),
+                     "decode_GiBps": round(alg_per_block * nb / (t3 - t2) / GIB, 3)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.block_size, args.t, min(args.cpu_sample_blocks, nb))
+
+    if rank == 0:
+        line = {
+            "metric": "device-resident GiB/s: RS encode+decode, 512 B blocks, 1 M-block batch",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {
+                "workload": f"RS(255,{k}) t={args.t} block_size={args.block_size}: encode + 1-byte-error "
+                            f"inject + decode with write-back, {nb} blocks per GPU (BASELINE configs[1]+[2])",
+                "blocks_per_gpu": nb,
+                "global_blocks": nb * world,
+                "parallelism": f"shard{world}",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": dom_name,
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": alg_per_block * nb,
+                "avg_launch_ms": round(dom_ms, 5),
+            },
+            "cpu_baseline": cpu,
+            "kernels_ms": {"encode": round(enc_avg, 5), "inject": round(inj_avg, 5), "decode": round(dec_avg, 5)},
+            "encode_GBps": round(alg_per_block * nb / (enc_avg * 1e-3) / 1e9, 1),
+            "decode_GBps": round(alg_per_block * nb / (dec_avg * 1e-3) / 1e9, 1),
+            "device_copy_GBps": round(copy_gbs, 1),
+            "host_inclusive": host_incl,
+            "kernel_path": eng.kernel_name,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
