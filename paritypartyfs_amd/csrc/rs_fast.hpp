@@ -1,5 +1,5 @@
 #pragma once
-// rs_fast.hpp -- Reed-Solomon GF(2^8) encode / syndrome / correct kernels for gfx950.
+// rs_fast.hpp -- Reed-Solomon GF(2^8) encode / syndrome / correct kernels for gfx950 (n = 255).
 //
 // Reference semantics: lib/blockdevice/src/rs_block_device.cpp
 //   encode  _encodeBlock :95-117   c(x) = m(x) x^2t + (m(x) x^2t mod g(x)); byte i = coeff of x^i,
@@ -7,20 +7,25 @@
 //   decode  _fixBlockAndExtract :119-183, _berlekampMassey :234-269, _errorLocations :271-280,
 //           _calculateOmega :224-232, _forney :210-222
 //
-// Fast path (n = 255, 2t in {2,4,...,32}): one workgroup = 4 waves = a tile of 256 blocks.
-//   - The tile's packed bytes are staged into LDS with LDS-DMA (global_load_lds_dwordx4).
-//   - Lane l of wave c owns block 4l+c, so every block of a wave has the same byte alignment
-//     in LDS; the wave's code is specialised on c (template) and every register index and
-//     funnel shift is a compile-time constant.
-//   - The parity / remainder is computed slicing-by-8 from the top: for 8 payload bytes e_i
-//     (XORed with the top of the running remainder), the new remainder is the XOR of 16 LDS
-//     table entries T[i][nibble] = nibble * (x^(2t+i) mod g), no dependency inside a chunk.
-//   - Decode recomputes the parity of the payload and compares it with the stored parity
-//     (c mod g == 0  <=>  all syndromes are zero).  Lanes with a non-zero remainder run the
-//     exact reference correction (syndromes -> Berlekamp-Massey -> roots over all 255 field
-//     values -> Omega -> Forney) in registers.
-//   - Output is rebuilt in place in the same LDS tile and streamed out with 16-byte stores.
-// Generic path (any n <= 255, any t): one thread per block, bytewise LFSR, private arrays.
+// Work decomposition (gfx950: 64-lane waves, 160 KiB LDS per CU):
+//   - A wave-tile is 64 consecutive blocks; lane l owns block l of the tile.  Each wave of a
+//     persistent 256-thread workgroup streams its own wave-tiles through a private 16 KiB LDS
+//     buffer -- no workgroup barriers on the hot path, so the 8 waves resident on a CU run
+//     their load / compute / store phases independently.  The codec tables (slicing tables,
+//     GF log/antilog) are loaded into LDS once per workgroup.
+//   - Packed input rows (249 B payloads, 255 B codewords) arrive by LDS-DMA
+//     (global_load_lds_dwordx4: one contiguous KiB per wave-instruction).  Each lane then
+//     reads its block as aligned dwords R[0..NR) and funnel-shifts (v_alignbit) by its own
+//     byte misalignment, so every register index is a compile-time constant.
+//   - Remainder: slicing-by-8 from the top chunk down.  For 8 bytes e_i (XORed with the top
+//     of the running remainder) the new remainder is the XOR of 16 LDS table entries
+//     T[i][nibble] = nibble * (x^(2t+i) mod g) -- no serial dependency inside a chunk.
+//   - Decode runs the same slicing over all 255 codeword bytes: r' = x^2t c(x) mod g, which is
+//     zero iff every syndrome is zero (g(0) != 0).  Lanes with r' != 0 run the reference's
+//     correction exactly (syndromes S_i = r'(a^i) a^(-2t i), Berlekamp-Massey, roots over all
+//     255 field values, Omega, Forney) in registers.
+//   - Output rows are rebuilt in place in the same LDS buffer (interior dwords + byte-wise
+//     row ends) and streamed out with 16-byte stores.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -28,100 +33,139 @@
 
 namespace ppfs {
 
-constexpr int RS_TILE = 256;                // blocks per workgroup tile
-constexpr int RS_N = 255;                   // fast-path codeword length
-constexpr int RS_TILE_BYTES = RS_TILE * RS_N; // 65280
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-template <int T2> struct RsCfg {
+constexpr int RS_N = 255;   // fast-path codeword length
+constexpr int RS_WT = 64;   // blocks per wave-tile (one per lane)
+constexpr int RS_WAVES = 4; // waves per workgroup
+
+// Variant knobs: NSEG_ = independent remainder chains per lane (0 = default policy),
+// PF = prefetch the next tile into VGPRs while computing (1) or not (0).
+template <int T2, int NSEG_ = 0> struct RsCfg {
     static constexpr int K = RS_N - T2;
     static constexpr int W = T2 <= 8 ? 2 : (T2 <= 16 ? 4 : 8); // remainder words (top aligned)
-    static constexpr int TBL_BYTES = W <= 4 ? 4096 : 8192;      // 16 nibble tables x 16 x 16 B (x2)
+    // independent remainder chains per lane (segments of 256/NSEG bytes), combined with
+    // x^64 / x^128 map tables: more LDS reads in flight per wave
+    // measured on MI355X (tools/rs_ablate.hip): one chain per lane is fastest at 2 waves/SIMD
+    static constexpr int NSEG = NSEG_ ? NSEG_ : 1;
+    static constexpr int SEGL = 256 / NSEG;
+    static constexpr int SLICE_BYTES = W <= 4 ? 4096 : 8192;    // 16 nibble tables x 16 x 16 B (x2)
+    static constexpr int NMAP = NSEG == 4 ? 2 : (NSEG == 2 ? 1 : 0);
+    static constexpr int MAP_BYTES = NMAP * T2 * 512;           // per map: 2t x 2 nibble tables x 16 x 16 B
+    static constexpr int OFF_MAP = SLICE_BYTES;
+    static constexpr int TBL_BYTES = SLICE_BYTES + MAP_BYTES;   // what encode loads
     static constexpr int OFF_GF = TBL_BYTES;
-    static constexpr int OFF_STATUS = OFF_GF + GF_BYTES;
-    static constexpr int OFF_TILE = OFF_STATUS + RS_TILE;
-    static constexpr int LDS_BYTES = OFF_TILE + RS_TILE_BYTES + 16;
-    static constexpr int NCHUNK = (K + 7) / 8;
+    static constexpr int OFF_WAVES = OFF_GF + GF_BYTES;
+    static constexpr int WAVE_BUF = RS_WT * RS_N + 16;          // 16336: codeword tile + slack
+    static constexpr int WAVE_STATUS = 64;
+    static constexpr int WAVE_BYTES = WAVE_BUF + WAVE_STATUS;   // 16400 (16-byte multiple)
+    static constexpr int LDS_BYTES = OFF_WAVES + RS_WAVES * WAVE_BYTES;
+    static_assert(2 * LDS_BYTES <= 163840, "two workgroups per CU");
 };
 
 // ------------------------------------------------------------------------------------
-// Tile staging: global <-> LDS
+// Wave-level staging: global <-> the wave's LDS buffer
 // ------------------------------------------------------------------------------------
-
-// Copy `bytes` bytes from global src (16-byte aligned) into LDS [dst, dst+bytes) using
-// LDS-DMA for whole 16-byte pieces (each wave-instruction moves one contiguous KiB) and
-// byte loads for the tail.  All 256 threads call it.
-__device__ __forceinline__ void stage_in(uint8_t* lds_dst, const uint8_t* __restrict__ src, uint32_t bytes)
+__device__ __forceinline__ void wave_stage_in(uint8_t* buf, const uint8_t* __restrict__ src, uint32_t bytes,
+    uint32_t lane)
 {
-    const uint32_t tid = threadIdx.x, lane = lane_id(), wave = wave_id();
-    const uint32_t npiece = bytes >> 4;     // whole 16-byte pieces
-    const uint32_t ngroup = (npiece + 63) >> 6; // 1 KiB groups
-    for (uint32_t g = wave; g < ngroup; g += 4) {
-        uint32_t piece = g * 64 + lane;
-        if (piece < npiece) {
-            __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)piece * 16),
-                (__attribute__((address_space(3))) void*)(lds_dst + g * 1024), 16, 0, 0);
-        }
-    }
-    uint32_t tail = bytes & 15u;
-    if (tid < tail)
-        lds_dst[npiece * 16 + tid] = src[npiece * 16 + tid];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-}
-
-// Copy LDS [src, src+bytes) to global dst (16-byte aligned): 16-byte stores + byte tail.
-__device__ __forceinline__ void stage_out(uint8_t* __restrict__ dst, const uint8_t* lds_src, uint32_t bytes)
-{
-    const uint32_t tid = threadIdx.x;
     const uint32_t npiece = bytes >> 4;
-    for (uint32_t p = tid; p < npiece; p += 256) {
-        uint4 v = *(const uint4*)(lds_src + p * 16);
-        *(uint4*)(dst + (size_t)p * 16) = v;
+    const uint32_t ngroup = (npiece + 63) >> 6;
+    for (uint32_t g = 0; g < ngroup; ++g) {
+        const uint32_t piece = g * 64 + lane;
+        if (piece < npiece)
+            __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)piece * 16),
+                (__attribute__((address_space(3))) void*)(buf + g * 1024), 16, 0, 0);
     }
-    uint32_t tail = bytes & 15u;
-    if (tid < tail)
-        dst[npiece * 16 + tid] = lds_src[npiece * 16 + tid];
+    const uint32_t tail = bytes & 15u;
+    if (lane < tail)
+        buf[npiece * 16 + lane] = src[npiece * 16 + lane];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
 }
 
-// Copy the context's tables (global, 16-byte multiple) into LDS.
+__device__ __forceinline__ void wave_stage_out(uint8_t* __restrict__ dst, const uint8_t* buf, uint32_t bytes,
+    uint32_t lane)
+{
+    const uint32_t npiece = bytes >> 4;
+    for (uint32_t p = lane; p < npiece; p += 64)
+        *(uint4*)(dst + (size_t)p * 16) = *(const uint4*)(buf + p * 16);
+    const uint32_t tail = bytes & 15u;
+    if (lane < tail)
+        dst[npiece * 16 + lane] = buf[npiece * 16 + lane];
+}
+
 __device__ __forceinline__ void load_tables(uint8_t* lds_dst, const uint8_t* __restrict__ src, uint32_t bytes)
 {
-    for (uint32_t p = threadIdx.x; p < (bytes >> 4); p += 256)
+    for (uint32_t p = threadIdx.x; p < (bytes >> 4); p += blockDim.x)
         *(uint4*)(lds_dst + p * 16) = *(const uint4*)(src + (size_t)p * 16);
+}
+
+// compiler + wave-level ordering point between LDS phases of one wave
+__device__ __forceinline__ void wave_fence()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
 }
 
 // ------------------------------------------------------------------------------------
 // Slicing-by-8 remainder step
 // ------------------------------------------------------------------------------------
-template <int W>
-__device__ __forceinline__ void tbl_acc(uint32_t (&acc)[W], const uint8_t* lds, uint32_t addr)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); // v_bitop3_b32: a ^ b ^ c
+}
+
+template <int W> struct Ent {
+    uint32_t w[W];
+};
+
+template <int W> __device__ __forceinline__ Ent<W> tbl_ld(const uint8_t* lds, uint32_t addr)
+{
+    Ent<W> e;
     if constexpr (W == 2) {
-        uint2 v = *(const uint2*)(lds + addr);
-        acc[0] ^= v.x;
-        acc[1] ^= v.y;
+        const uint2 v = *(const uint2*)(lds + addr);
+        e.w[0] = v.x;
+        e.w[1] = v.y;
     } else if constexpr (W == 4) {
-        uint4 v = *(const uint4*)(lds + addr);
-        acc[0] ^= v.x;
-        acc[1] ^= v.y;
-        acc[2] ^= v.z;
-        acc[3] ^= v.w;
+        const uint4 v = *(const uint4*)(lds + addr);
+        e.w[0] = v.x;
+        e.w[1] = v.y;
+        e.w[2] = v.z;
+        e.w[3] = v.w;
     } else {
-        uint4 v = *(const uint4*)(lds + addr);
-        uint4 u = *(const uint4*)(lds + addr + 4096);
-        acc[0] ^= v.x;
-        acc[1] ^= v.y;
-        acc[2] ^= v.z;
-        acc[3] ^= v.w;
-        acc[4] ^= u.x;
-        acc[5] ^= u.y;
-        acc[6] ^= u.z;
-        acc[7] ^= u.w;
+        const uint4 v = *(const uint4*)(lds + addr);
+        const uint4 u = *(const uint4*)(lds + addr + 4096);
+        e.w[0] = v.x;
+        e.w[1] = v.y;
+        e.w[2] = v.z;
+        e.w[3] = v.w;
+        e.w[4] = u.x;
+        e.w[5] = u.y;
+        e.w[6] = u.z;
+        e.w[7] = u.w;
+    }
+    return e;
+}
+
+// acc ^= XOR of N entries, three inputs per v_bitop3
+template <int W, int N> __device__ __forceinline__ void xor_into(uint32_t (&acc)[W], const Ent<W> (&e)[N])
+{
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        uint32_t a = acc[w];
+        int i = 0;
+#pragma unroll
+        for (; i + 1 < N; i += 2)
+            a = xor3(a, e[i].w[w], e[i + 1].w[w]);
+        if (i < N)
+            a ^= e[i].w[w];
+        acc[w] = a;
     }
 }
 
-// One 8-byte chunk: st <- (st * x^8 + sum_i chunk_i x^(2t+i)) mod g, state top-aligned.
-// NB = number of chunk bytes that can be non-zero when FIRST (state still zero).
+// st <- (st * x^8 + sum_i chunk_i x^(2t+i)) mod g, top-aligned state.
+// NB = number of chunk bytes that may be non-zero when FIRST (state still zero).
 template <int W, bool FIRST, int NB>
 __device__ __forceinline__ void slice8(uint32_t (&st)[W], uint32_t lo, uint32_t hi, const uint8_t* lds)
 {
@@ -137,89 +181,197 @@ __device__ __forceinline__ void slice8(uint32_t (&st)[W], uint32_t lo, uint32_t 
         acc[w] = FIRST ? 0u : st[w - 2];
     const uint32_t ll = (lo << 4) & 0xF0F0F0F0u, lh = lo & 0xF0F0F0F0u;
     const uint32_t hl = (hi << 4) & 0xF0F0F0F0u, hh = hi & 0xF0F0F0F0u;
+    constexpr int NL = FIRST ? (NB < 8 ? NB : 8) : 8;
+    Ent<W> e[2 * NL];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        if (!FIRST || p < NB) {
-            tbl_acc<W>(acc, lds, ((ll >> (8 * p)) & 0xFFu) + (2 * p) * 256);
-            tbl_acc<W>(acc, lds, ((lh >> (8 * p)) & 0xFFu) + (2 * p + 1) * 256);
-        }
+    for (int p = 0; p < NL; ++p) {
+        const uint32_t xl = p < 4 ? ll : hl, xh = p < 4 ? lh : hh;
+        const int sh = 8 * (p & 3);
+        e[2 * p] = tbl_ld<W>(lds, ((xl >> sh) & 0xFFu) + (2 * p) * 256);
+        e[2 * p + 1] = tbl_ld<W>(lds, ((xh >> sh) & 0xFFu) + (2 * p + 1) * 256);
     }
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        if (!FIRST || 4 + p < NB) {
-            tbl_acc<W>(acc, lds, ((hl >> (8 * p)) & 0xFFu) + (2 * (4 + p)) * 256);
-            tbl_acc<W>(acc, lds, ((hh >> (8 * p)) & 0xFFu) + (2 * (4 + p) + 1) * 256);
-        }
-    }
+    xor_into<W, 2 * NL>(acc, e);
 #pragma unroll
     for (int w = 0; w < W; ++w)
         st[w] = acc[w];
 }
 
-// 4 bytes starting at register-byte position s of the lane's register image R[0..NR).
-template <int NR>
-__device__ __forceinline__ uint32_t rdw(const uint32_t (&R)[NR], int s)
+// out = (r(x) x^E) mod g for a top-aligned remainder r, via the 2t x 2 nibble map tables at mapb
+template <int T2, int W>
+__device__ __forceinline__ void map_apply(uint32_t (&out)[W], const uint32_t (&r)[W], const uint8_t* lds, uint32_t mapb)
 {
-    const int q = s >> 2, sh = s & 3;
-    const uint32_t lo = (q < NR) ? R[q] : 0u;
-    if (sh == 0)
-        return lo;
-    const uint32_t hi = (q + 1 < NR) ? R[q + 1] : 0u;
-    return __builtin_amdgcn_alignbit(hi, lo, 8 * sh);
-}
-
-template <int NR> __device__ __forceinline__ uint32_t rbyte(const uint32_t (&R)[NR], int s)
-{
-    return (R[s >> 2] >> (8 * (s & 3))) & 0xFFu;
-}
-
-// Remainder of the K payload bytes held at register-byte offset BASE (payload byte j at
-// register byte BASE + j), processed from the top chunk down.
-template <int T2, int NR, int BASE>
-__device__ __forceinline__ void rs_remainder(uint32_t (&st)[RsCfg<T2>::W], const uint32_t (&R)[NR], const uint8_t* lds)
-{
-    using C = RsCfg<T2>;
-    constexpr int W = C::W, K = C::K, NC = C::NCHUNK;
-    constexpr int TOPN = K - 8 * (NC - 1); // valid bytes in the top chunk (1..8)
+    Ent<W> e[2 * T2];
+#pragma unroll
+    for (int i = 0; i < T2; ++i) {
+        const int P = 4 * W - T2 + i;
+        const uint32_t w = r[P >> 2] >> (8 * (P & 3));
+        e[2 * i] = tbl_ld<W>(lds, mapb + (2 * i) * 256 + ((w << 4) & 0xF0u));
+        e[2 * i + 1] = tbl_ld<W>(lds, mapb + (2 * i + 1) * 256 + (w & 0xF0u));
+    }
 #pragma unroll
     for (int w = 0; w < W; ++w)
-        st[w] = 0;
-    {
-        constexpr int J = 8 * (NC - 1);
-        uint32_t lo = rdw<NR>(R, BASE + J), hi = rdw<NR>(R, BASE + J + 4);
-        if constexpr (TOPN < 4) {
-            lo &= (1u << (8 * TOPN)) - 1u;
-            hi = 0;
-        } else if constexpr (TOPN == 4) {
-            hi = 0;
-        } else if constexpr (TOPN < 8) {
-            hi &= (1u << (8 * (TOPN - 4))) - 1u;
+        out[w] = 0;
+    xor_into<W, 2 * T2>(out, e);
+}
+
+template <int NR> __device__ __forceinline__ uint32_t rget(const uint32_t (&R)[NR], int q)
+{
+    return (q >= 0 && q < NR) ? R[q] : 0u;
+}
+
+// 4 bytes at register-byte position 4q + sh (sh = the lane's runtime misalignment 0..3)
+template <int NR> __device__ __forceinline__ uint32_t rdw(const uint32_t (&R)[NR], int q, uint32_t sh)
+{
+    return __builtin_amdgcn_alignbit(rget<NR>(R, q + 1), rget<NR>(R, q), 8 * sh);
+}
+
+template <int LEN, int SEGL, int S> struct SegInfo {
+    static constexpr int LO = SEGL * S;
+    static constexpr int LENS = (LEN - LO) < SEGL ? (LEN - LO) : SEGL;
+    static constexpr int NC = LENS > 0 ? (LENS + 7) / 8 : 0;
+    static constexpr int TOPN = LENS - 8 * (NC - 1);
+};
+
+// one chunk (index c, counted from the segment start) of segment S
+template <int T2, int NR, int LEN, int SEGL, int S, int C>
+__device__ __forceinline__ void seg_step(uint32_t (&st)[RsCfg<T2>::W], const uint32_t (&R)[NR], uint32_t sh,
+    const uint8_t* lds)
+{
+    using SI = SegInfo<LEN, SEGL, S>;
+    constexpr int W = RsCfg<T2>::W;
+    if constexpr (C < SI::NC) {
+        constexpr int J = SI::LO + 8 * C;
+        uint32_t lo = rdw<NR>(R, J / 4, sh), hi = rdw<NR>(R, J / 4 + 1, sh);
+        if constexpr (C == SI::NC - 1) {
+            constexpr int TOPN = SI::TOPN;
+            if constexpr (TOPN < 4) {
+                lo &= (1u << (8 * TOPN)) - 1u;
+                hi = 0;
+            } else if constexpr (TOPN == 4) {
+                hi = 0;
+            } else if constexpr (TOPN < 8) {
+                hi &= (1u << (8 * (TOPN - 4))) - 1u;
+            }
+            slice8<W, true, TOPN>(st, lo, hi, lds);
+        } else {
+            slice8<W, false, 8>(st, lo, hi, lds);
         }
-        slice8<W, true, TOPN>(st, lo, hi, lds);
-    }
-#pragma unroll
-    for (int c = NC - 2; c >= 0; --c) {
-        const int J = 8 * c;
-        uint32_t lo = rdw<NR>(R, BASE + J), hi = rdw<NR>(R, BASE + J + 4);
-        slice8<W, false, 8>(st, lo, hi, lds);
     }
 }
 
-// Byte q (0..2t-1) of a top-aligned remainder.
-template <int T2, int W> __device__ __forceinline__ uint32_t st_byte(const uint32_t (&st)[W], int q)
+template <int T2, int NR, int LEN, int SEGL, int C>
+__device__ __forceinline__ void seg_round(uint32_t (&s0)[RsCfg<T2>::W], uint32_t (&s1)[RsCfg<T2>::W],
+    uint32_t (&s2)[RsCfg<T2>::W], uint32_t (&s3)[RsCfg<T2>::W], const uint32_t (&R)[NR], uint32_t sh,
+    const uint8_t* lds)
 {
-    const int P = 4 * W - T2 + q;
-    return (st[P >> 2] >> (8 * (P & 3))) & 0xFFu;
+    seg_step<T2, NR, LEN, SEGL, 0, C>(s0, R, sh, lds);
+    if constexpr (256 / SEGL > 1)
+        seg_step<T2, NR, LEN, SEGL, 1, C>(s1, R, sh, lds);
+    if constexpr (256 / SEGL > 2) {
+        seg_step<T2, NR, LEN, SEGL, 2, C>(s2, R, sh, lds);
+        seg_step<T2, NR, LEN, SEGL, 3, C>(s3, R, sh, lds);
+    }
+    if constexpr (C > 0)
+        seg_round<T2, NR, LEN, SEGL, C - 1>(s0, s1, s2, s3, R, sh, lds);
+}
+
+// Remainder of LEN bytes (byte j at register byte sh + j), as NSEG independent chains.
+template <int T2, int NR, int LEN, int NS = 0>
+__device__ __forceinline__ void rs_remainder(uint32_t (&st)[RsCfg<T2>::W], const uint32_t (&R)[NR], uint32_t sh,
+    const uint8_t* lds)
+{
+    using Cf = RsCfg<T2, NS>;
+    constexpr int W = Cf::W, SEGL = Cf::SEGL;
+    uint32_t s0[W], s1[W], s2[W], s3[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+        s0[w] = s1[w] = s2[w] = s3[w] = 0;
+    seg_round<T2, NR, LEN, SEGL, SEGL / 8 - 1>(s0, s1, s2, s3, R, sh, lds);
+    if constexpr (Cf::NSEG == 4) {
+        uint32_t m1[W], m3[W], b[W], mb[W];
+        map_apply<T2, W>(m1, s1, lds, Cf::OFF_MAP);      // x^64
+        map_apply<T2, W>(m3, s3, lds, Cf::OFF_MAP);      // x^64
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+            b[w] = s2[w] ^ m3[w];
+        map_apply<T2, W>(mb, b, lds, Cf::OFF_MAP + T2 * 512); // x^128
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+            st[w] = xor3(s0[w], m1[w], mb[w]);
+    } else if constexpr (Cf::NSEG == 2) {
+        uint32_t m1[W];
+        map_apply<T2, W>(m1, s1, lds, Cf::OFF_MAP);      // x^128
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+            st[w] = s0[w] ^ m1[w];
+    } else {
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+            st[w] = s0[w];
+    }
 }
 
 // ------------------------------------------------------------------------------------
-// Exact reference correction for one block from its remainder r = c mod g.
-// Calls fix(pos, e) for every root of sigma found over all 255 field values.
+// Row emission: write LEN stream bytes to LDS [out, out+LEN) (any alignment), in place.
+// Stream byte p comes from register byte (cbase + p) of R, except bytes p < NPAR which come
+// from the parity function par(u, p_u) (only called for dwords that contain them).
+// Interior dwords are written whole; the first/last partial dwords byte by byte, so lanes
+// never write each other's bytes.
+// ------------------------------------------------------------------------------------
+template <int NR, int LEN, int CMIN, int CMAX, int NPAR, typename Par>
+__device__ __forceinline__ void emit_row(uint8_t* tile, uint32_t out, int cbase, const uint32_t (&R)[NR], Par&& par)
+{
+    const uint32_t m0 = (4u - (out & 3u)) & 3u;      // first stream byte of the first whole dword
+    const int cb = cbase + (int)m0;                  // register byte of stream byte m0
+    const int qoff = cb >> 2;                        // arithmetic: floor
+    const uint32_t sh = (uint32_t)cb & 3u;
+    constexpr int DMIN = (CMIN >= 0) ? CMIN / 4 : -((-CMIN + 3) / 4);
+    constexpr int DMAX = (CMAX + 3) / 4;
+    constexpr int UMAX = LEN / 4; // u in [-1, UMAX]
+    // X(u) = R[u + qoff] selected over the possible offsets
+    auto X = [&](int u) -> uint32_t {
+        uint32_t v = 0;
+#pragma unroll
+        for (int d = DMIN; d <= DMAX; ++d)
+            v = (qoff == d) ? rget<NR>(R, u + d) : v;
+        return v;
+    };
+    uint32_t xcur = X(-1);
+#pragma unroll
+    for (int u = -1; u <= UMAX; ++u) {
+        const uint32_t xnext = X(u + 1);
+        uint32_t v = __builtin_amdgcn_alignbit(xnext, xcur, 8 * sh);
+        xcur = xnext;
+        const int p = (int)m0 + 4 * u; // stream position of byte 0 of this dword
+        if constexpr (NPAR > 0) {
+            if (4 * u <= NPAR + 3) // only the first few dwords can hold parity bytes
+                v = par(v, p);
+        }
+        const bool full = p >= 0 && p + 4 <= LEN;
+        if (u >= 0 && 4 * u + 7 <= LEN) {
+            // always whole for every m0 in [0,3]
+            *(uint32_t*)(tile + out + m0 + 4 * u) = v;
+        } else if (full) {
+            *(uint32_t*)(tile + out + m0 + 4 * u) = v;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int pk = p + k;
+                if (pk >= 0 && pk < LEN)
+                    tile[out + (uint32_t)pk] = (uint8_t)(v >> (8 * k));
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Exact reference correction from r' = x^2t c(x) mod g.  Calls fix(pos, e) for every root of
+// sigma over all 255 field values.
 // ------------------------------------------------------------------------------------
 template <int T2, typename Fix>
 __device__ __forceinline__ void rs_correct(const uint32_t (&r)[T2], const Gf& gf, Fix&& fix)
 {
-    // syndromes S_i = c(alpha^i) = r(alpha^i), i = 1..2t   (rs_block_device.cpp:131-141)
+    // S_i = c(a^i) = r'(a^i) * a^(-2t i), i = 1..2t   (rs_block_device.cpp:131-141)
     uint32_t lr[T2];
 #pragma unroll
     for (int q = 0; q < T2; ++q)
@@ -230,7 +382,8 @@ __device__ __forceinline__ void rs_correct(const uint32_t (&r)[T2], const Gf& gf
         uint32_t s = 0;
 #pragma unroll
         for (int q = 0; q < T2; ++q) {
-            uint32_t v = gf.exp(lr[q] + (uint32_t)((i * q) % 255));
+            const uint32_t e = (uint32_t)(((i * q - i * T2) % 255 + 255) % 255);
+            const uint32_t v = gf.exp(lr[q] + e);
             s ^= r[q] ? v : 0u;
         }
         S[i - 1] = s;
@@ -249,12 +402,11 @@ __device__ __forceinline__ void rs_correct(const uint32_t (&r)[T2], const Gf& gf
         uint32_t d = S[n];
 #pragma unroll
         for (int i = 1; i <= n; ++i) {
-            uint32_t p = gf.mul(sig[i], S[n - i]);
+            const uint32_t p = gf.mul(sig[i], S[n - i]);
             d ^= (i <= L) ? p : 0u;
         }
         if (d != 0) {
-            const uint32_t coef = gf.div(d, b);
-            const uint32_t lc = gf.log(coef);
+            const uint32_t lc = gf.log(gf.div(d, b));
             uint32_t T[T2 + 1];
 #pragma unroll
             for (int i = 0; i <= T2; ++i) {
@@ -296,7 +448,7 @@ __device__ __forceinline__ void rs_correct(const uint32_t (&r)[T2], const Gf& gf
     for (int i = 1; i <= T2; ++i)
         deg = sig[i] ? i : deg;
 
-    // Omega(v) / sigma'(v) for a root v (given with its log)  (:210-222)
+    // Omega(v) / sigma'(v) for a root v given by its log  (:210-222)
     auto forney = [&](uint32_t lv, uint32_t dsig) -> uint32_t {
         uint32_t acc = om[T2 - 1];
 #pragma unroll
@@ -304,34 +456,33 @@ __device__ __forceinline__ void rs_correct(const uint32_t (&r)[T2], const Gf& gf
             acc = gf.mul_log(lv, acc) ^ om[j];
         return gf.div(acc, dsig);
     };
-    // position of the error for root v = alpha^lv : LOG[inv(v)]
+    // error position for root v = a^lv:  LOG[inv(v)]
     auto pos_of = [](uint32_t lv) -> uint32_t { return lv == 0 ? 0u : 255u - lv; };
 
     if (deg == 1) {
-        // sigma = 1 + s1 x: single root v = 1/s1; sigma' = s1
+        // sigma = 1 + s1 x: the single root v = 1/s1, sigma' = s1
         const uint32_t ls1 = gf.log(sig[1]);
         const uint32_t lv = ls1 == 0 ? 0u : 255u - ls1;
         fix(pos_of(lv), forney(lv, sig[1]));
     } else if (deg == 2) {
         if (sig[1] == 0) {
-            // x^2 = 1/s2: one (double) root, sigma' == 0 -> e = 0 (division by zero is 0)
+            // x^2 = 1/s2: one root, sigma' == 0 -> e = 0 (division by zero is 0 in GF256)
             const uint32_t u = (255u - gf.log(sig[2])) % 255u;
             const uint32_t lv = (u & 1u) ? (u + 255u) >> 1 : u >> 1;
             fix(pos_of(lv), 0u);
         } else {
-            // x = (s1/s2) y,  y^2 + y = s2 / s1^2
+            // x = (s1/s2) y with y^2 + y = s2 / s1^2: two roots or none
             const uint32_t c = gf.div(sig[2], gf.mul(sig[1], sig[1]));
             const uint32_t y0 = gf.qs(c);
             if (y0 != 0) {
                 const uint32_t k = gf.div(sig[1], sig[2]);
-                const uint32_t v1 = gf.mul(k, y0), v2 = gf.mul(k, y0 ^ 1u);
-                const uint32_t l1 = gf.log(v1), l2 = gf.log(v2);
+                const uint32_t l1 = gf.log(gf.mul(k, y0)), l2 = gf.log(gf.mul(k, y0 ^ 1u));
                 fix(pos_of(l1), forney(l1, sig[1]));
                 fix(pos_of(l2), forney(l2, sig[1]));
             }
         }
     } else if (deg >= 3) {
-        // exhaustive Chien over every v = alpha^m, m = 0..254 (:271-280)
+        // exhaustive search over every v = a^m, m = 0..254 (:271-280)
         uint32_t ls[T2 + 1];
 #pragma unroll
         for (int i = 0; i <= T2; ++i)
@@ -341,13 +492,9 @@ __device__ __forceinline__ void rs_correct(const uint32_t (&r)[T2], const Gf& gf
 #pragma unroll
             for (int i = 0; i <= T2; ++i) {
                 const uint32_t e = (ls[i] + (uint32_t)i * m) % 255u;
-                const uint32_t term = sig[i] ? gf.exp(e) : 0u; // sigma_i v^i
-                s ^= term;
-                if (i & 1) {
-                    // derivative term sigma_i v^(i-1) = term / v
-                    const uint32_t td = sig[i] ? gf.exp((e + 255u - m) % 255u) : 0u;
-                    ds ^= td;
-                }
+                s ^= sig[i] ? gf.exp(e) : 0u;
+                if (i & 1)
+                    ds ^= sig[i] ? gf.exp((e + 255u - m) % 255u) : 0u;
             }
             if (s == 0)
                 fix(pos_of(m), forney(m, ds));
@@ -356,184 +503,346 @@ __device__ __forceinline__ void rs_correct(const uint32_t (&r)[T2], const Gf& gf
 }
 
 // ------------------------------------------------------------------------------------
-// Per-wave bodies (C = wave index in the workgroup; the wave owns blocks 4*lane + C).
+// Per-lane bodies
 // ------------------------------------------------------------------------------------
-template <int T2, int C>
-__device__ __forceinline__ void rs_encode_wave(uint8_t* lds, uint32_t lane)
+template <int T2, int NS, typename Pre>
+__device__ __forceinline__ void rs_encode_lane(uint8_t* tile, const uint8_t* lds, uint32_t l, Pre&& prefetch)
 {
-    using Cf = RsCfg<T2>;
+    using Cf = RsCfg<T2, NS>;
     constexpr int K = Cf::K, W = Cf::W;
-    constexpr int A = (K * C) % 4;          // input alignment of this wave's blocks
-    constexpr int NR = (A + K + 3) / 4;
-    const uint32_t b = 4 * lane + C;
-    uint8_t* tile = lds + Cf::OFF_TILE;
-
+    constexpr int NR = (3 + K + 3) / 4;
+    const uint32_t ib = K * l, a = ib & 3u;
+    const uint32_t* tw = (const uint32_t*)(tile + (ib & ~3u));
     uint32_t R[NR];
-    const uint32_t inb = K * b - A;
 #pragma unroll
     for (int q = 0; q < NR; ++q)
-        R[q] = *(const uint32_t*)(tile + inb + 4 * q);
-
+        R[q] = tw[q];
+    prefetch();
     uint32_t st[W];
-    rs_remainder<T2, NR, A>(st, R, lds);
+    rs_remainder<T2, NR, K, NS>(st, R, a, lds);
+    wave_fence(); // every lane's block is in registers before the in-place rewrite
 
-    __syncthreads(); // every lane of every wave has its block in registers
-
-    // codeword byte m: parity m < 2t, payload byte m-2t otherwise
-    auto cw_byte = [&](int m) -> uint32_t { return m < T2 ? st_byte<T2, W>(st, m) : rbyte<NR>(R, A + m - T2); };
-    constexpr int OB = (RS_N * C) % 4;
-    constexpr int M0 = (4 - OB) % 4;
-    constexpr int NU = (RS_N - M0) / 4;
-    const uint32_t ob = RS_N * b;
+    // codeword stream: byte p < 2t parity (top-aligned state byte 4W-2t+p), else payload p-2t
+    auto par = [&](uint32_t v, int p) -> uint32_t {
+        // 4 parity-stream bytes at positions p..p+3 merged over the payload bytes
 #pragma unroll
-    for (int m = 0; m < M0; ++m)
-        tile[ob + m] = (uint8_t)cw_byte(m);
+        for (int k = 0; k < 4; ++k) {
+            const int pk = p + k;
+            uint32_t pb = 0;
 #pragma unroll
-    for (int u = 0; u < NU; ++u) {
-        const int m = M0 + 4 * u;
-        uint32_t v;
-        if (m >= T2) {
-            v = rdw<NR>(R, A + m - T2);
-        } else {
-            v = cw_byte(m) | (cw_byte(m + 1) << 8) | (cw_byte(m + 2) << 16) | (cw_byte(m + 3) << 24);
+            for (int q = 0; q < T2; ++q) {
+                const int P = 4 * W - T2 + q;
+                pb = (pk == q) ? ((st[P >> 2] >> (8 * (P & 3))) & 0xFFu) : pb;
+            }
+            const bool isp = pk >= 0 && pk < T2;
+            v = isp ? ((v & ~(0xFFu << (8 * k))) | (pb << (8 * k))) : v;
         }
-        *(uint32_t*)(tile + ob + m) = v;
-    }
-#pragma unroll
-    for (int m = M0 + 4 * NU; m < RS_N; ++m)
-        tile[ob + m] = (uint8_t)cw_byte(m);
+        return v;
+    };
+    // payload byte j at register byte a + j -> stream byte p at register byte a + p - 2t
+    emit_row<NR, RS_N, -T2, 3 - T2, T2>(tile, RS_N * l, (int)a - T2, R, par);
 }
 
-template <int T2, int C>
-__device__ __forceinline__ void rs_decode_wave(uint8_t* lds, uint32_t lane, uint32_t nb, uint8_t* __restrict__ raw_g,
-    size_t tile_block0, bool write_back, bool want_data)
+template <int T2, int NS, typename Pre>
+__device__ __forceinline__ void rs_decode_lane(uint8_t* tile, const uint8_t* lds, uint32_t l, bool valid,
+    uint8_t* __restrict__ raw_g, size_t blk, bool write_back, bool want_data, uint8_t* status_lds, Pre&& prefetch)
 {
-    using Cf = RsCfg<T2>;
+    using Cf = RsCfg<T2, NS>;
     constexpr int K = Cf::K, W = Cf::W;
-    constexpr int A = (RS_N * C) % 4;
-    constexpr int NR = (A + RS_N + 3) / 4;
-    const uint32_t b = 4 * lane + C;
-    const bool valid = b < nb;
-    uint8_t* tile = lds + Cf::OFF_TILE;
-
+    constexpr int NR = (3 + RS_N + 3) / 4;
+    const uint32_t ib = RS_N * l, a = ib & 3u;
+    const uint32_t* tw = (const uint32_t*)(tile + (ib & ~3u));
     uint32_t R[NR];
-    const uint32_t inb = RS_N * b - A;
 #pragma unroll
     for (int q = 0; q < NR; ++q)
-        R[q] = *(const uint32_t*)(tile + inb + 4 * q);
-
-    // remainder of the payload, then r = c mod g = parity(payload) ^ stored parity
+        R[q] = tw[q];
+    prefetch();
+    // r' = x^2t c(x) mod g over all 255 codeword bytes
     uint32_t st[W];
-    rs_remainder<T2, NR, A + T2>(st, R, lds);
+    rs_remainder<T2, NR, RS_N, NS>(st, R, a, lds);
     uint32_t any = 0;
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
-        const int s = A + 4 * w - (4 * W - T2); // register byte of stored-parity byte (4w - pad)
-        uint32_t v;
-        if (s >= A) {
-            v = rdw<NR>(R, s);
-        } else if (s + 4 > A) {
-            // partially padding: keep the bytes >= A
-            const int keep = s + 4 - A;
-            v = (rdw<NR>(R, A) << (8 * (4 - keep)));
-        } else {
-            v = 0;
-        }
-        st[w] ^= v;
+    for (int w = 0; w < W; ++w)
         any |= st[w];
-    }
     const bool err = valid && any != 0;
-
     if (__builtin_amdgcn_ballot_w64(err)) {
         if (err) {
             uint32_t r[T2];
 #pragma unroll
-            for (int q = 0; q < T2; ++q)
-                r[q] = st_byte<T2, W>(st, q);
+            for (int q = 0; q < T2; ++q) {
+                const int P = 4 * W - T2 + q;
+                r[q] = (st[P >> 2] >> (8 * (P & 3))) & 0xFFu;
+            }
             const Gf gf { lds + Cf::OFF_GF };
-            const size_t gblk = tile_block0 + b;
+            // corrections patch the lane's own row of the LDS tile (other lanes only ever use
+            // their own bytes of the words they share with this row); R is reloaded below.
             rs_correct<T2>(r, gf, [&](uint32_t pos, uint32_t e) {
                 if (e == 0)
                     return;
-                const uint32_t orig = tile[RS_N * b + pos];
+                const uint8_t fixed = (uint8_t)(tile[ib + pos] ^ e);
+                tile[ib + pos] = fixed;
                 if (write_back)
-                    raw_g[gblk * RS_N + pos] = (uint8_t)(orig ^ e);
-                const uint32_t idx = A + pos, q = idx >> 2, msk = e << (8 * (idx & 3));
-#pragma unroll
-                for (int qq = 0; qq < NR; ++qq)
-                    R[qq] ^= ((uint32_t)qq == q) ? msk : 0u;
+                    raw_g[blk * RS_N + pos] = fixed;
             });
         }
+        // whole-wave reload: R is dead throughout the (register-hungry) correction code
+#pragma unroll
+        for (int q = 0; q < NR; ++q)
+            R[q] = tw[q];
     }
-    lds[Cf::OFF_STATUS + b] = err ? 1 : 0;
+    status_lds[l] = err ? 1 : 0;
     if (!want_data)
         return;
-
-    __syncthreads();
-    constexpr int OB = (K * C) % 4;
-    constexpr int M0 = (4 - OB) % 4;
-    constexpr int NU = (K - M0) / 4;
-    const uint32_t ob = K * b;
-    constexpr int D = A + T2; // register byte of payload byte 0
-#pragma unroll
-    for (int m = 0; m < M0; ++m)
-        tile[ob + m] = (uint8_t)rbyte<NR>(R, D + m);
-#pragma unroll
-    for (int u = 0; u < NU; ++u)
-        *(uint32_t*)(tile + ob + M0 + 4 * u) = rdw<NR>(R, D + M0 + 4 * u);
-#pragma unroll
-    for (int m = M0 + 4 * NU; m < K; ++m)
-        tile[ob + m] = (uint8_t)rbyte<NR>(R, D + m);
+    wave_fence();
+    // payload byte j = codeword byte 2t + j at register byte a + 2t + j
+    emit_row<NR, K, T2, T2 + 3, 0>(tile, K * l, (int)a + T2, R, [](uint32_t v, int) { return v; });
 }
 
 // ------------------------------------------------------------------------------------
-// Kernels
+// Kernels (persistent: each wave walks wave-tiles wt = global_wave, += total waves).
+// Pipelining per wave: the out-tile is read into VGPRs, then the NEXT tile's LDS-DMA is issued
+// into the (now free) buffer, then the global stores -- so the wait for the next tile's data
+// (a counted vmcnt) does not wait for this tile's stores.
 // ------------------------------------------------------------------------------------
-template <int T2>
+__device__ __forceinline__ void wave_dma_issue(uint8_t* buf, const uint8_t* __restrict__ src, uint32_t npiece,
+    uint32_t lane)
+{
+    const uint32_t ngroup = (npiece + 63) >> 6;
+    for (uint32_t g = 0; g < ngroup; ++g) {
+        const uint32_t piece = g * 64 + lane;
+        if (piece < npiece)
+            __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)piece * 16),
+                (__attribute__((address_space(3))) void*)(buf + g * 1024), 16, 0, 0);
+    }
+}
+
+// s_waitcnt vmcnt(n) (gfx9 simm16: vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt[5:4] at [15:14]).
+// The builtin form is visible to the compiler's waitcnt pass, unlike inline asm.
+#define PPFS_VMCNT(n) (((n)&15) | (((n) >> 4) << 14) | 0x70 | 0xF00)
+__device__ __forceinline__ void wait_vmcnt(int n)
+{
+    switch (n) {
+    case 0: __builtin_amdgcn_s_waitcnt(PPFS_VMCNT(0)); break;
+    case 1: __builtin_amdgcn_s_waitcnt(PPFS_VMCNT(1)); break;
+    case 16: __builtin_amdgcn_s_waitcnt(PPFS_VMCNT(16)); break;
+    case 17: __builtin_amdgcn_s_waitcnt(PPFS_VMCNT(17)); break;
+    default: __builtin_amdgcn_s_waitcnt(PPFS_VMCNT(0)); break;
+    }
+}
+
+// stores of one full out-tile region from VGPRs: returns the number of store instructions
+template <int NPIECE, int NT = 0>
+__device__ __forceinline__ void store_tile(uint8_t* __restrict__ dst, const uint4 (&o)[(NPIECE + 63) / 64], uint32_t lane)
+{
+#pragma unroll
+    for (int k = 0; k < (NPIECE + 63) / 64; ++k) {
+        const uint32_t p = lane + 64 * k;
+        if (k < NPIECE / 64 || p < NPIECE) {
+            uint4* q = (uint4*)(dst + (size_t)p * 16);
+            if constexpr (NT) {
+                const u32x4 v = { o[k].x, o[k].y, o[k].z, o[k].w };
+                __builtin_nontemporal_store(v, (u32x4*)q);
+            } else {
+                *q = o[k];
+            }
+        }
+    }
+}
+
+template <int NPIECE>
+__device__ __forceinline__ void read_tile(uint4 (&o)[(NPIECE + 63) / 64], const uint8_t* buf, uint32_t lane)
+{
+#pragma unroll
+    for (int k = 0; k < (NPIECE + 63) / 64; ++k) {
+        const uint32_t p = lane + 64 * k;
+        o[k] = (k < NPIECE / 64 || p < NPIECE) ? *(const uint4*)(buf + p * 16) : make_uint4(0, 0, 0, 0);
+    }
+}
+
+// next-tile prefetch into VGPRs (register staging): 16-byte coalesced loads
+template <int NPIECE, int NT = 0>
+__device__ __forceinline__ void load_regs(uint4 (&L)[(NPIECE + 63) / 64], const uint8_t* __restrict__ src, uint32_t lane)
+{
+#pragma unroll
+    for (int k = 0; k < (NPIECE + 63) / 64; ++k) {
+        const uint32_t p = lane + 64 * k;
+        const uint4* q = (const uint4*)(src + (size_t)p * 16);
+        if (k < NPIECE / 64 || p < NPIECE) {
+            if constexpr (NT) {
+                const u32x4 v = __builtin_nontemporal_load((const u32x4*)q);
+                L[k] = make_uint4(v.x, v.y, v.z, v.w);
+            } else {
+                L[k] = *q;
+            }
+        } else {
+            L[k] = make_uint4(0, 0, 0, 0);
+        }
+    }
+}
+
+// conditional prefetch that defines L on both paths: a conditionally-kept L would stay live
+// (and be spilled) through the whole loop body
+template <int NPIECE, int NT = 0>
+__device__ __forceinline__ void load_regs_if(bool cond, uint4 (&L)[(NPIECE + 63) / 64], const uint8_t* __restrict__ src,
+    uint32_t lane)
+{
+    if (cond) {
+        load_regs<NPIECE, NT>(L, src, lane);
+    } else {
+#pragma unroll
+        for (int k = 0; k < (NPIECE + 63) / 64; ++k)
+            L[k] = make_uint4(0, 0, 0, 0);
+    }
+}
+
+template <int NPIECE>
+__device__ __forceinline__ void write_regs(uint8_t* buf, const uint4 (&L)[(NPIECE + 63) / 64], uint32_t lane)
+{
+#pragma unroll
+    for (int k = 0; k < (NPIECE + 63) / 64; ++k) {
+        const uint32_t p = lane + 64 * k;
+        if (k < NPIECE / 64 || p < NPIECE)
+            *(uint4*)(buf + p * 16) = L[k];
+    }
+}
+
+// Defaults = fastest measured variant: one chain, next-tile prefetch during compute,
+// non-temporal (streaming) global loads and stores.
+template <int T2, int NS = 0, int PF = 1, int NT = 1, int MEMONLY = 0>
 __global__ __launch_bounds__(256, 2) void rs255_encode_kernel(const uint8_t* __restrict__ data,
     uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables)
 {
-    using Cf = RsCfg<T2>;
+    using Cf = RsCfg<T2, NS>;
+    constexpr int K = Cf::K;
+    constexpr int IN_PIECES = RS_WT * K / 16;     // full tile: 64*K bytes (multiple of 16)
+    constexpr int OUT_PIECES = RS_WT * RS_N / 16; // 1020
+    static_assert((RS_WT * K) % 16 == 0, "full input tiles are whole 16-byte pieces");
     __shared__ __attribute__((aligned(16))) uint8_t lds[Cf::LDS_BYTES];
-    const uint64_t tile0 = (uint64_t)blockIdx.x * RS_TILE;
-    const uint32_t nb = (uint32_t)min((uint64_t)RS_TILE, nblocks - tile0);
     load_tables(lds, tables, Cf::TBL_BYTES);
-    stage_in(lds + Cf::OFF_TILE, data + tile0 * Cf::K, nb * Cf::K);
-    const uint32_t lane = lane_id();
-    switch (wave_id()) {
-    case 0: rs_encode_wave<T2, 0>(lds, lane); break;
-    case 1: rs_encode_wave<T2, 1>(lds, lane); break;
-    case 2: rs_encode_wave<T2, 2>(lds, lane); break;
-    default: rs_encode_wave<T2, 3>(lds, lane); break;
-    }
     __syncthreads();
-    stage_out(raw + tile0 * RS_N, lds + Cf::OFF_TILE, nb * RS_N);
+    const uint32_t lane = lane_id(), wave = wave_id();
+    uint8_t* tile = lds + Cf::OFF_WAVES + wave * Cf::WAVE_BYTES;
+    const uint64_t ntiles = (nblocks + RS_WT - 1) / RS_WT;
+    const uint64_t nfull = nblocks / RS_WT;
+    const uint64_t stride = (uint64_t)gridDim.x * RS_WAVES;
+    uint64_t wt = (uint64_t)blockIdx.x * RS_WAVES + wave;
+    uint4 L[(IN_PIECES + 63) / 64];
+    load_regs_if<IN_PIECES, NT>(wt < nfull, L, data + wt * RS_WT * K, lane);
+    for (; wt < ntiles; wt += stride) {
+        const uint64_t b0 = wt * RS_WT;
+        const uint32_t nb = (uint32_t)min((uint64_t)RS_WT, nblocks - b0);
+        if (nb == RS_WT)
+            write_regs<IN_PIECES>(tile, L, lane); // loads issued one tile earlier
+        else
+            wave_stage_in(tile, data + b0 * K, nb * K, lane);
+        wave_fence();
+        const uint64_t nx = wt + stride;
+        if constexpr (!MEMONLY) {
+            rs_encode_lane<T2, NS>(tile, lds, lane, [&]() {
+                // block is in registers: prefetch the next tile now, its latency hides under compute
+                if (PF)
+                    load_regs_if<IN_PIECES, NT>(nx < nfull, L, data + nx * RS_WT * K, lane);
+            });
+        } else {
+            if (PF)
+                load_regs_if<IN_PIECES, NT>(nx < nfull, L, data + nx * RS_WT * K, lane);
+        }
+        wave_fence();
+        if (nb == RS_WT) {
+            uint4 o[(OUT_PIECES + 63) / 64];
+            read_tile<OUT_PIECES>(o, tile, lane);
+            if (!PF)
+                load_regs_if<IN_PIECES, NT>(nx < nfull, L, data + nx * RS_WT * K, lane);
+            store_tile<OUT_PIECES, NT>(raw + b0 * RS_N, o, lane);
+        } else {
+            wave_stage_out(raw + b0 * RS_N, tile, nb * RS_N, lane);
+        }
+        wave_fence();
+    }
 }
 
-template <int T2>
+// Input staging of the decode kernel (STAGE):
+//   0  next tile -> VGPRs after this tile's out-tile is read, before its stores
+//   1  next tile -> VGPRs after this tile's stores
+//   2  next tile -> VGPRs during the syndrome pass (prefetch, as encode)
+//   3  next tile -> LDS by DMA after this tile's stores
+template <int T2, int NS = 0, int STAGE = 1, int NT = 1>
 __global__ __launch_bounds__(256, 2) void rs255_decode_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
     uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables, int write_back)
 {
-    using Cf = RsCfg<T2>;
+    using Cf = RsCfg<T2, NS>;
+    constexpr int K = Cf::K;
+    constexpr int IN_PIECES = RS_WT * RS_N / 16; // 1020
+    constexpr int OUT_PIECES = RS_WT * K / 16;
+    constexpr bool REGS = STAGE != 3;
+    static_assert((RS_WT * K) % 16 == 0, "full output tiles are whole 16-byte pieces");
     __shared__ __attribute__((aligned(16))) uint8_t lds[Cf::LDS_BYTES];
-    const uint64_t tile0 = (uint64_t)blockIdx.x * RS_TILE;
-    const uint32_t nb = (uint32_t)min((uint64_t)RS_TILE, nblocks - tile0);
     load_tables(lds, tables, Cf::TBL_BYTES + GF_BYTES);
-    stage_in(lds + Cf::OFF_TILE, raw + tile0 * RS_N, nb * RS_N);
-    const uint32_t lane = lane_id();
-    const bool wb = write_back != 0, want = data != nullptr;
-    switch (wave_id()) {
-    case 0: rs_decode_wave<T2, 0>(lds, lane, nb, raw, tile0, wb, want); break;
-    case 1: rs_decode_wave<T2, 1>(lds, lane, nb, raw, tile0, wb, want); break;
-    case 2: rs_decode_wave<T2, 2>(lds, lane, nb, raw, tile0, wb, want); break;
-    default: rs_decode_wave<T2, 3>(lds, lane, nb, raw, tile0, wb, want); break;
-    }
     __syncthreads();
-    if (want)
-        stage_out(data + tile0 * Cf::K, lds + Cf::OFF_TILE, nb * Cf::K);
-    if (status)
-        stage_out(status + tile0, lds + Cf::OFF_STATUS, nb);
+    const uint32_t lane = lane_id(), wave = wave_id();
+    uint8_t* tile = lds + Cf::OFF_WAVES + wave * Cf::WAVE_BYTES;
+    uint8_t* st_lds = tile + Cf::WAVE_BUF;
+    const bool wb = write_back != 0, want = data != nullptr;
+    const uint64_t ntiles = (nblocks + RS_WT - 1) / RS_WT;
+    const uint64_t nfull = nblocks / RS_WT;
+    const uint64_t stride = (uint64_t)gridDim.x * RS_WAVES;
+    uint64_t wt = (uint64_t)blockIdx.x * RS_WAVES + wave;
+    uint4 L[REGS ? (IN_PIECES + 63) / 64 : 1];
+    bool staged = false; // STAGE 3: the current tile already sits in LDS
+    if constexpr (REGS) {
+        load_regs_if<IN_PIECES, NT>(wt < nfull, L, raw + wt * RS_WT * RS_N, lane);
+    } else if (wt < nfull) {
+        wave_dma_issue(tile, raw + wt * RS_WT * RS_N, IN_PIECES, lane);
+        staged = true;
+    }
+    for (; wt < ntiles; wt += stride) {
+        const uint64_t b0 = wt * RS_WT;
+        const uint32_t nb = (uint32_t)min((uint64_t)RS_WT, nblocks - b0);
+        if constexpr (REGS) {
+            if (nb == RS_WT)
+                write_regs<IN_PIECES>(tile, L, lane);
+            else
+                wave_stage_in(tile, raw + b0 * RS_N, nb * RS_N, lane);
+        } else {
+            if (staged)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            else
+                wave_stage_in(tile, raw + b0 * RS_N, nb * RS_N, lane);
+        }
+        wave_fence();
+        const uint64_t nx = wt + stride;
+        const bool nfullx = nx < nfull;
+        rs_decode_lane<T2, NS>(tile, lds, lane, lane < nb, raw, b0 + lane, wb, want, st_lds, [&]() {
+            if constexpr (STAGE == 2)
+                load_regs_if<IN_PIECES, NT>(nfullx, L, raw + nx * RS_WT * RS_N, lane);
+        });
+        wave_fence();
+        if (nb == RS_WT) {
+            uint4 o[(OUT_PIECES + 63) / 64];
+            if (want)
+                read_tile<OUT_PIECES>(o, tile, lane);
+            const uint4 sv = (lane < 4) ? *(const uint4*)(st_lds + 16 * lane) : make_uint4(0, 0, 0, 0);
+            if constexpr (STAGE == 0)
+                load_regs_if<IN_PIECES, NT>(nfullx, L, raw + nx * RS_WT * RS_N, lane);
+            if (want)
+                store_tile<OUT_PIECES, NT>(data + b0 * K, o, lane);
+            if (status && lane < 4)
+                *(uint4*)(status + b0 + 16 * lane) = sv;
+        } else {
+            if (want)
+                wave_stage_out(data + b0 * K, tile, nb * K, lane);
+            if (status)
+                wave_stage_out(status + b0, st_lds, nb, lane);
+        }
+        if constexpr (STAGE == 1)
+            load_regs_if<IN_PIECES, NT>(nfullx, L, raw + nx * RS_WT * RS_N, lane);
+        wave_fence();
+        if constexpr (STAGE == 3) {
+            staged = nfullx;
+            if (nfullx)
+                wave_dma_issue(tile, raw + nx * RS_WT * RS_N, IN_PIECES, lane);
+        }
+    }
 }
-
 
 } // namespace ppfs
