@@ -6,7 +6,7 @@ rs_correctable_bytes=3 -> RS(255,249) (the reference clamps codewords to 255 B,
 rs_block_device.cpp:57), 2^20 blocks per GPU, synthetic uniform payloads.
 
 One step = encode(2^20 payloads -> codewords)            [rs255 encode kernel]
-         + inject exactly one byte error into every codeword (torch gather/scatter)
+         + inject exactly one byte error into every codeword (one torch scatter of wrong bytes)
          + decode(codewords -> payloads, status, in-place write-back)   [rs255 decode kernel]
 value = algorithmic bytes of all ranks (encode 504 B + decode 504 B per block) / step time.
 
@@ -137,9 +137,15 @@ def main():
                + torch.randint(0, n, (nb,), device=dev, generator=gen))
     err_val = torch.randint(1, 256, (nb,), dtype=torch.uint8, device=dev, generator=gen)
     stream = torch.cuda.current_stream()
+    # The payloads never change, so every step's clean codewords are identical: the corrupted
+    # byte of block b is always clean[b, pos_b] ^ val_b.  Precompute it once; the per-step
+    # injection is then a single scatter of 2^20 wrong bytes into the fresh codewords.
+    eng.encode(data, cw, nblocks=nb)
+    bad_bytes = cw[err_pos] ^ err_val
+    torch.cuda.synchronize()
 
     def inject():
-        cw[err_pos] = cw[err_pos] ^ err_val
+        cw.index_put_((err_pos,), bad_bytes)
 
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
 
@@ -213,8 +219,9 @@ def main():
     achieved = alg_per_block * nb / (dom_ms * 1e-3) / 1e9
     traffic = None
     pmc = load_traffic()
-    if pmc and pmc.get("kernel") == dom_name and pmc.get("blocks") == nb:
-        traffic = pmc.get("hbm_bytes_per_launch")
+    kp = (pmc or {}).get("kernels", {}).get(dom_name)
+    if kp and kp.get("blocks") == nb:
+        traffic = round(kp["hbm_bytes_per_launch"])  # profiles/pmc_latest.json, tools/pmc_summary.py
 
     host_incl = None
     if args.host_inclusive and rank == 0:

@@ -388,6 +388,28 @@ __device__ __forceinline__ void rs_correct(const uint32_t (&r)[T2], const Gf& gf
         }
         S[i - 1] = s;
     }
+    // Geometric syndromes S_i = S_1 X^(i-1) (all non-zero): the shortest LFSR of the sequence is
+    // 1 + X x, which is what Berlekamp-Massey returns for it (its output depends on S only), so
+    // the reference corrects exactly one byte: root v = 1/X -> pos = LOG[X],
+    // Omega = S_1 (higher terms cancel), e = Omega(v) / sigma'(v) = S_1 / X.
+    // This is the single-error case; it skips BM / Omega / Forney.
+    {
+        uint32_t ls[T2];
+        bool geo = true;
+#pragma unroll
+        for (int i = 0; i < T2; ++i) {
+            ls[i] = gf.log(S[i]);
+            geo = geo && S[i] != 0;
+        }
+        const uint32_t lx = (ls[1] + 255u - ls[0]) % 255u;
+#pragma unroll
+        for (int i = 1; i + 1 < T2; ++i)
+            geo = geo && (ls[i + 1] + 255u - ls[i]) % 255u == lx;
+        if (geo) {
+            fix(lx, gf.exp(ls[0] + 255u - lx));
+            return;
+        }
+    }
     // Berlekamp-Massey (rs_block_device.cpp:234-269) with Bs = x^m * B kept pre-shifted.
     uint32_t sig[T2 + 1], Bs[T2 + 1];
 #pragma unroll
@@ -766,7 +788,9 @@ __global__ __launch_bounds__(256, 2) void rs255_encode_kernel(const uint8_t* __r
 //   1  next tile -> VGPRs after this tile's stores
 //   2  next tile -> VGPRs during the syndrome pass (prefetch, as encode)
 //   3  next tile -> LDS by DMA after this tile's stores
-template <int T2, int NS = 0, int STAGE = 1, int NT = 1>
+// NT: bit 0 = non-temporal codeword loads, bit 1 = non-temporal payload stores.  Codeword
+// loads stay temporal by default: the write-back RMWs bytes of lines just read.
+template <int T2, int NS = 0, int STAGE = 1, int NT = 0>
 __global__ __launch_bounds__(256, 2) void rs255_decode_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
     uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables, int write_back)
 {
@@ -790,7 +814,7 @@ __global__ __launch_bounds__(256, 2) void rs255_decode_kernel(uint8_t* __restric
     uint4 L[REGS ? (IN_PIECES + 63) / 64 : 1];
     bool staged = false; // STAGE 3: the current tile already sits in LDS
     if constexpr (REGS) {
-        load_regs_if<IN_PIECES, NT>(wt < nfull, L, raw + wt * RS_WT * RS_N, lane);
+        load_regs_if<IN_PIECES, NT & 1>(wt < nfull, L, raw + wt * RS_WT * RS_N, lane);
     } else if (wt < nfull) {
         wave_dma_issue(tile, raw + wt * RS_WT * RS_N, IN_PIECES, lane);
         staged = true;
@@ -814,7 +838,7 @@ __global__ __launch_bounds__(256, 2) void rs255_decode_kernel(uint8_t* __restric
         const bool nfullx = nx < nfull;
         rs_decode_lane<T2, NS>(tile, lds, lane, lane < nb, raw, b0 + lane, wb, want, st_lds, [&]() {
             if constexpr (STAGE == 2)
-                load_regs_if<IN_PIECES, NT>(nfullx, L, raw + nx * RS_WT * RS_N, lane);
+                load_regs_if<IN_PIECES, NT & 1>(nfullx, L, raw + nx * RS_WT * RS_N, lane);
         });
         wave_fence();
         if (nb == RS_WT) {
@@ -823,9 +847,9 @@ __global__ __launch_bounds__(256, 2) void rs255_decode_kernel(uint8_t* __restric
                 read_tile<OUT_PIECES>(o, tile, lane);
             const uint4 sv = (lane < 4) ? *(const uint4*)(st_lds + 16 * lane) : make_uint4(0, 0, 0, 0);
             if constexpr (STAGE == 0)
-                load_regs_if<IN_PIECES, NT>(nfullx, L, raw + nx * RS_WT * RS_N, lane);
+                load_regs_if<IN_PIECES, NT & 1>(nfullx, L, raw + nx * RS_WT * RS_N, lane);
             if (want)
-                store_tile<OUT_PIECES, NT>(data + b0 * K, o, lane);
+                store_tile<OUT_PIECES, (NT >> 1) & 1>(data + b0 * K, o, lane);
             if (status && lane < 4)
                 *(uint4*)(status + b0 + 16 * lane) = sv;
         } else {
@@ -835,7 +859,7 @@ __global__ __launch_bounds__(256, 2) void rs255_decode_kernel(uint8_t* __restric
                 wave_stage_out(status + b0, st_lds, nb, lane);
         }
         if constexpr (STAGE == 1)
-            load_regs_if<IN_PIECES, NT>(nfullx, L, raw + nx * RS_WT * RS_N, lane);
+            load_regs_if<IN_PIECES, NT & 1>(nfullx, L, raw + nx * RS_WT * RS_N, lane);
         wave_fence();
         if constexpr (STAGE == 3) {
             staged = nfullx;

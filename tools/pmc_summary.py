@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile_box.sh run (rocprofv3 kernel trace + separate PMC passes).
+
+usage: python3 tools/pmc_summary.py gpurun_out/prof_<tag> <tag> [--blocks N]
+
+Writes profiles/<tag>_kernel_stats.csv (the rocprofv3 --stats table), profiles/<tag>_summary.md
+(per-kernel duration, HBM bytes per launch, counters) and profiles/pmc_latest.json (what
+bench.py reports as roofline.traffic).
+
+HBM bytes per launch follow MI355X_MICROARCH.md's rocprofv3 section: FETCH_SIZE and WRITE_SIZE
+are in KiB; on gfx950 FETCH_SIZE reports half of the bytes of a wide coalesced streaming read,
+so it is doubled; WRITE_SIZE is exact for 16-byte-per-lane streaming stores.
+"""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    # "void ppfs::rs255_encode_kernel<6, 0, 1, 1, 0>(unsigned char const*, ...)" -> rs255_encode_kernel<6, 0, 1, 1, 0>
+    n = name.replace("void ", "")
+    n = n.split("(")[0]
+    return n.replace("ppfs::", "")
+
+
+def counters(path):
+    per = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> [values per dispatch]
+    if not os.path.exists(path):
+        return per
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            per[short(row["Kernel_Name"])][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return per
+
+
+def main():
+    d, tag = sys.argv[1], sys.argv[2]
+    blocks = 1 << 20
+    if "--blocks" in sys.argv:
+        blocks = int(sys.argv[sys.argv.index("--blocks") + 1])
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    stats = os.path.join(d, "trace", "trace_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    rows = list(csv.DictReader(open(stats)))
+    merged = defaultdict(dict)
+    for sub in ("fetch", "write", "sq", "sq2"):
+        for k, cs in counters(os.path.join(d, sub, f"{sub}_counter_collection.csv")).items():
+            for c, v in cs.items():
+                merged[k][c] = statistics.median(v)
+    lines = [f"# rocprofv3 summary: {tag}", "",
+             "Command: `tools/profile_box.sh` (bench.py --steps 10 --warmup 3 --no-cpu-baseline, 2^20 blocks)", "",
+             "| kernel | calls | avg us | min us | HBM read MB (2xFETCH) | HBM write MB | traffic MB/launch |",
+             "|---|---|---|---|---|---|---|"]
+    latest = {}
+    for r in rows:
+        k = short(r["Name"])
+        if not k.startswith("rs255") and not k.startswith("crc") and not k.startswith("ham") \
+                and not k.startswith("parity") and not k.startswith("rs_generic"):
+            continue
+        c = merged.get(k, {})
+        fetch = 2 * c.get("FETCH_SIZE", float("nan")) * 1024
+        write = c.get("WRITE_SIZE", float("nan")) * 1024
+        lines.append(f"| `{k}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | {float(r['MinNs']) / 1e3:.1f} "
+                     f"| {fetch / 1e6:.1f} | {write / 1e6:.1f} | {(fetch + write) / 1e6:.1f} |")
+        base = k.split(",")[0] + ">" if "," in k else k
+        latest[base] = {"kernel": base, "kernel_full": k, "blocks": blocks,
+                        "avg_launch_ns": float(r["AverageNs"]),
+                        "hbm_read_bytes_per_launch": fetch, "hbm_write_bytes_per_launch": write,
+                        "hbm_bytes_per_launch": fetch + write, "counters": c}
+    lines += ["", "Counters (median per dispatch):", ""]
+    for k, v in latest.items():
+        lines.append(f"- `{v['kernel_full']}`: " + ", ".join(f"{a}={b:.4g}" for a, b in sorted(v["counters"].items())))
+    open(os.path.join(prof, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
+    json.dump({"tag": tag, "kernels": latest}, open(os.path.join(prof, "pmc_latest.json"), "w"), indent=1)
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()

@@ -49,7 +49,8 @@ __global__ void inject(uint8_t* cw, uint64_t nb)
     }
 }
 
-template <int STAGE, int NT = 1> float t_dec(const Bufs& b, bool check)
+static bool g_inject = true;
+template <int STAGE, int NT = 1, int WB = 1> float t_dec(const Bufs& b, bool check)
 {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
@@ -57,10 +58,11 @@ template <int STAGE, int NT = 1> float t_dec(const Bufs& b, bool check)
     float tot = 0;
     for (int i = 0; i < 10; ++i) {
         hipMemcpy(b.bad, b.cw, b.nb * 255, hipMemcpyDeviceToDevice);
-        hipLaunchKernelGGL(inject, dim3((b.nb + 255) / 256), dim3(256), 0, 0, b.bad, b.nb);
+        if (g_inject)
+            hipLaunchKernelGGL(inject, dim3((b.nb + 255) / 256), dim3(256), 0, 0, b.bad, b.nb);
         hipEventRecord(e0);
         hipLaunchKernelGGL((rs255_decode_kernel<6, 0, STAGE, NT>), dim3(b.grid), dim3(256), 0, 0, b.bad, b.out, b.st,
-            b.nb, b.tab, 1);
+            b.nb, b.tab, WB);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
         float ms = 0;
@@ -73,7 +75,7 @@ template <int STAGE, int NT = 1> float t_dec(const Bufs& b, bool check)
         hipMemcpy(y.data(), b.d, y.size(), hipMemcpyDeviceToHost);
         hipMemcpy(c.data(), b.bad, c.size(), hipMemcpyDeviceToHost);
         hipMemcpy(c2.data(), b.cw, c2.size(), hipMemcpyDeviceToHost);
-        if (x != y || c != c2)
+        if (x != y || (WB && c != c2))
             printf("STAGE %d NT %d: MISMATCH (payload %d, write-back %d)\n", STAGE, NT, x != y, c != c2);
     }
     return tot / 10 * 1e3f;
@@ -119,25 +121,37 @@ int main()
     b.grid = 2 * cus;
     const double bytes = b.nb * 504.0;
     printf("encode (default) %.1f us\n", t_enc(b));
-    t_dec<0>(b, true);
-    t_dec<1>(b, true);
-    t_dec<2>(b, true);
-    t_dec<3>(b, true);
     t_dec<1, 0>(b, true);
-    const char* names[] = { "S0 late-regs", "S1 regs-after-store", "S2 regs-prefetch", "S3 dma-after-store",
-        "S1 NT0" };
-    constexpr int NV = 5;
+    t_dec<1, 1>(b, true);
+    t_dec<1, 2>(b, true);
+    t_dec<1, 3>(b, true);
+    t_dec<2, 0>(b, true);
+    t_dec<2, 2>(b, true);
+    t_dec<0, 0>(b, true);
+    t_dec<1, 0, 0>(b, true);
+    t_dec<1, 2, 0>(b, true);
+    const char* names[] = { "S1 NT0", "S1 NTload", "S1 NTstore", "S2 NTstore", "S2 NT0", "S0 NT0",
+        "S1 NT0 no-wb", "S1 NTstore no-wb", "encode default", "S1 NT0 clean", "S1 NTstore clean" };
+    constexpr int NV = 11;
     std::vector<float> dec[NV];
     for (int rep = 0; rep < 5; ++rep) {
-        dec[0].push_back(t_dec<0>(b, false));
-        dec[1].push_back(t_dec<1>(b, false));
-        dec[2].push_back(t_dec<2>(b, false));
-        dec[3].push_back(t_dec<3>(b, false));
-        dec[4].push_back(t_dec<1, 0>(b, false));
+        dec[0].push_back(t_dec<1, 0>(b, false));
+        dec[1].push_back(t_dec<1, 1>(b, false));
+        dec[2].push_back(t_dec<1, 2>(b, false));
+        dec[3].push_back(t_dec<2, 2>(b, false));
+        dec[4].push_back(t_dec<2, 0>(b, false));
+        dec[5].push_back(t_dec<0, 0>(b, false));
+        dec[6].push_back(t_dec<1, 0, 0>(b, false));
+        dec[7].push_back(t_dec<1, 2, 0>(b, false));
+        dec[8].push_back(t_enc(b));
+        g_inject = false;
+        dec[9].push_back(t_dec<1, 0>(b, false));
+        dec[10].push_back(t_dec<1, 2>(b, false));
+        g_inject = true;
     }
     for (int v = 0; v < NV; ++v) {
         std::sort(dec[v].begin(), dec[v].end());
-        printf("%-22s decode %.1f us (%.0f GB/s)  [min %.1f max %.1f]\n", names[v], dec[v][2],
+        printf("%-22s %.1f us (%.0f GB/s)  [min %.1f max %.1f]\n", names[v], dec[v][2],
             bytes / (dec[v][2] * 1e-6) / 1e9, dec[v][0], dec[v][4]);
     }
     return 0;
