@@ -98,6 +98,29 @@ def cpu_baseline(bs, t, nblocks, seed=1234):
     }
 
 
+def timed_steps(step, steps, world, sync, device=None):
+    """Time exactly `steps` calls of step() between barrier + sync on both sides; returns the
+    MAX elapsed seconds over ranks (every rank gets the same value).  The barrier and the
+    max-reduce are the only collectives: nothing on the data path."""
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    return elapsed
+
+
 def load_traffic(path=os.path.join(ROOT, "profiles", "pmc_latest.json")):
     try:
         with open(path) as f:
@@ -172,19 +195,7 @@ def main():
             print(json.dumps({"error": "verification failed"}), file=sys.stderr)
             sys.exit(3)
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(False)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = timed_steps(lambda: step(False), args.steps, world, torch.cuda.synchronize, dev)
 
     # kernel durations: re-run K steps with events recorded around each phase (same stream)
     enc_ms, inj_ms, dec_ms = [], [], []

@@ -1,0 +1,47 @@
+"""N>1 path on CPU: two gloo ranks run bench.py's timed region (tests the barrier / max-over-ranks
+timing the driver's multi-GPU bench relies on; the data path has no collective to test)."""
+import os
+import socket
+import sys
+import time
+
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, q):
+    import torch.distributed as dist
+
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+
+    # rank r's step sleeps (r+1) * 20 ms: the reported time must be the slowest rank's
+    el = bench.timed_steps(lambda: time.sleep(0.02 * (rank + 1)), 3, world, lambda: None, None)
+    q.put((rank, el))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_max_over_ranks():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(120)
+        assert p.exitcode == 0
+    res = dict(q.get() for _ in range(world))
+    assert abs(res[0] - res[1]) < 1e-9  # every rank reports the max
+    assert res[0] >= 3 * 0.02 * world * 0.95

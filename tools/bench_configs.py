@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""Per-configuration kernel throughput (device-resident), one JSON line per config.
+
+BASELINE.json configs: cfg2/cfg3 RS(255,249) t=3 encode / 1-error decode, cfg4 Hamming and
+CRC 0x9960034c at block_size 4096, cfg5 RS(255,223) t=16 (per-GPU shard of 2^20 blocks), plus
+parity.  Each line: median kernel time over --reps launches (hipEvents on the launch stream),
+algorithmic bytes per launch, GB/s and fraction of the 8 TB/s HBM peak.  A device-side round
+trip check (decode(encode(x)) == x, status as expected) guards every config; bit-exactness vs
+the oracle is tests/test_gpu_parity.py's job.
+
+usage: python3 tools/bench_configs.py [--blocks N] [--reps R] [--only NAME]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+PEAK = 8000.0
+
+
+def med_ms(fn, reps, stream):
+    import torch
+
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
+    for _ in range(3):
+        fn()
+    ts = []
+    for i in range(reps):
+        ev[2 * i].record(stream)
+        fn()
+        ev[2 * i + 1].record(stream)
+    torch.cuda.synchronize()
+    for i in range(reps):
+        ts.append(ev[2 * i].elapsed_time(ev[2 * i + 1]))
+    return float(np.median(ts))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--blocks", type=int, default=1 << 20)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", default=None)
+    a = ap.parse_args()
+    import torch
+
+    from paritypartyfs_amd import ECC_CRC, ECC_HAMMING, ECC_PARITY, ECC_REED_SOLOMON, EccEngine, crc_implicit_to_explicit
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream()
+    cfgs = [
+        ("cfg2-3 rs255_t3 bs512", ECC_REED_SOLOMON, 512, 3, 0),
+        ("cfg5 rs255_t16 bs4096", ECC_REED_SOLOMON, 4096, 16, 0),
+        ("cfg4 hamming bs4096", ECC_HAMMING, 4096, 0, 0),
+        ("cfg4 crc32 0x9960034c bs4096", ECC_CRC, 4096, 0, crc_implicit_to_explicit(0x9960034C)),
+        ("parity bs4096", ECC_PARITY, 4096, 0, 0),
+        ("rs255_t8 bs255", ECC_REED_SOLOMON, 255, 8, 0),
+    ]
+    for name, typ, bs, t, poly in cfgs:
+        if a.only and a.only not in name:
+            continue
+        eng = EccEngine(typ, bs, t, crc_polynomial_explicit=poly)
+        n, k, nb = eng.raw_block_size, eng.data_size, a.blocks
+        g = torch.Generator(device=dev)
+        g.manual_seed(0x50504653)
+        data = torch.randint(0, 256, (nb * k,), dtype=torch.uint8, device=dev, generator=g)
+        raw = torch.zeros(nb * n, dtype=torch.uint8, device=dev)
+        out = torch.empty(nb * k, dtype=torch.uint8, device=dev)
+        st = torch.empty(nb, dtype=torch.uint8, device=dev)
+        enc_ms = med_ms(lambda: eng.encode(data, raw, nblocks=nb), a.reps, stream)
+        clean = raw.clone()
+        dec_clean_ms = med_ms(lambda: eng.decode(raw, out, st, write_back=True, nblocks=nb), a.reps, stream)
+        ok = bool(torch.equal(out, data)) and int(st.max()) == 0
+        line = {"config": name, "blocks": nb, "raw": n, "data": k, "kernel_path": eng.kernel_name,
+                "encode_ms": round(enc_ms, 4), "encode_GBps": round((k + n) * nb / enc_ms / 1e6, 1),
+                "decode_clean_ms": round(dec_clean_ms, 4),
+                "decode_clean_GBps": round((k + n) * nb / dec_clean_ms / 1e6, 1)}
+        if typ == ECC_REED_SOLOMON or typ == ECC_HAMMING:
+            # one correctable error per block, restored before every launch (copy not timed)
+            pos = torch.arange(nb, device=dev, dtype=torch.int64) * n + torch.randint(0, n, (nb,), device=dev,
+                                                                                     generator=g)
+            if typ == ECC_HAMMING:
+                val = (1 << torch.randint(0, 8, (nb,), device=dev, generator=g)).to(torch.uint8)
+            else:
+                val = torch.randint(1, 256, (nb,), dtype=torch.uint8, device=dev, generator=g)
+            bad = clean.clone()
+            bad[pos] ^= val
+            ts = []
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            for i in range(a.reps + 2):
+                raw.copy_(bad)
+                e0.record(stream)
+                eng.decode(raw, out, st, write_back=True, nblocks=nb)
+                e1.record(stream)
+                e1.synchronize()
+                if i >= 2:
+                    ts.append(e0.elapsed_time(e1))
+            dec_ms = float(np.median(ts))
+            if typ == ECC_HAMMING:
+                # a flip in an unused tail bit is not an error (status 0); every other one is
+                ok = ok and bool(torch.equal(out, data)) and int(st.max()) <= 1
+            else:
+                ok = ok and bool(torch.equal(out, data)) and int(st.min()) == 1 and bool(torch.equal(raw, clean))
+            line.update({"decode_1err_ms": round(dec_ms, 4), "decode_1err_GBps": round((k + n) * nb / dec_ms / 1e6, 1)})
+        best = max(v for kk, v in line.items() if kk.endswith("GBps"))
+        line["roofline_frac_encode"] = round(line["encode_GBps"] / PEAK, 4)
+        line["roofline_frac_best"] = round(best / PEAK, 4)
+        line["roundtrip_ok"] = ok
+        print(json.dumps(line), flush=True)
+        del data, raw, out, st, clean
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
