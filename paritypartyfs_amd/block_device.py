@@ -181,7 +181,8 @@ class IBlockDevice:
     def numOfBlocks(self) -> int:
         return self._disk.size() // self.rawBlockSize()
 
-    # batch API: whole blocks [first, first+count)
+    # batch API: whole blocks [first, first+count); the per-block loop (codecs override it with
+    # one engine call per range)
     def readBlocks(self, first: int, count: int) -> Tuple[np.ndarray, np.ndarray]:
         """Decode `count` whole blocks; returns (payloads [count, dataSize], FsError-or-0 per block)."""
         out = np.zeros((count, self.dataSize()), dtype=np.uint8)
@@ -265,6 +266,79 @@ class _EngineDevice(IBlockDevice):
         r = self._disk.write(block_index * self._raw, bytes(self._raw))
         return Expected(None) if r else Expected.unexpected(r.error())
 
+    # ---- batched whole-block I/O: one engine call per contiguous range ----
+    def _has_spill(self) -> bool:
+        return self._engine.ecc_type == ECC_REED_SOLOMON and self._raw < 255
+
+    def _write_back(self, block_index: int, old: np.ndarray, fixed: np.ndarray, spill) -> Optional[FsError]:
+        raise NotImplementedError
+
+    def readBlocks(self, first: int, count: int) -> Tuple[np.ndarray, np.ndarray]:
+        """== readBlock(DataLocation(i, 0), dataSize()) for i in [first, first+count), in order:
+        same payloads, per-block errors, disk contents and correction log."""
+        out = np.zeros((count, self._ds), dtype=np.uint8)
+        err = np.zeros(count, dtype=np.uint8)
+        e = self._engine
+        wb = e.ecc_type in (ECC_REED_SOLOMON, ECC_HAMMING)
+        done = 0
+        while done < count:
+            nb = count - done
+            r = self._disk.read((first + done) * self._raw, nb * self._raw)
+            if not r:
+                # range not on the disk: per-block calls report it block by block
+                for i in range(done, count):
+                    rr = self.readBlock(DataLocation(first + i, 0), self._ds)
+                    if rr:
+                        out[i] = np.frombuffer(rr.value(), dtype=np.uint8)
+                    else:
+                        err[i] = int(rr.error())
+                break
+            raw = np.frombuffer(r.value(), dtype=np.uint8).copy()
+            fixed = raw.copy()
+            status = np.zeros(nb, dtype=np.uint8)
+            spill = np.zeros(nb * e.spill_bytes_per_block(), dtype=np.uint8) if self._has_spill() else None
+            e.decode_host(fixed, out[done:].reshape(-1), status, write_back=wb, spill=spill)
+            i = 0
+            while i < nb:
+                st = int(status[i])
+                if st == STATUS_CORRECTION_ERROR:
+                    err[done + i] = int(FsError.BlockDevice_CorrectionError)
+                    out[done + i] = 0
+                elif st == STATUS_CORRECTED and wb:
+                    sp = spill[i * e.spill_bytes_per_block():(i + 1) * e.spill_bytes_per_block()] \
+                        if spill is not None else None
+                    fe = self._write_back(first + done + i, raw[i * self._raw:(i + 1) * self._raw],
+                                          fixed[i * self._raw:(i + 1) * self._raw], sp)
+                    if fe is not None:
+                        err[done + i] = int(fe)
+                    if sp is not None and int(sp[0]) and i + 1 < nb:
+                        i += 1  # the write-back ran into the next block: re-read from there
+                        break
+                i += 1
+            done += i
+        return out, err
+
+    def writeBlocks(self, first: int, payloads: np.ndarray) -> np.ndarray:
+        """== writeBlock(payload_i, DataLocation(first+i, 0)) in order (full-block writes)."""
+        payloads = np.ascontiguousarray(payloads, dtype=np.uint8).reshape(-1, self._ds)
+        count = payloads.shape[0]
+        err = np.zeros(count, dtype=np.uint8)
+        r = self._disk.read(first * self._raw, count * self._raw)
+        if self._has_spill() or not r:
+            return super().writeBlocks(first, payloads)  # per-block order (spill / out of range)
+        raw = np.frombuffer(r.value(), dtype=np.uint8).copy()
+        status = np.zeros(count, dtype=np.uint8)
+        self._engine.write_host(payloads.reshape(-1), raw, status)
+        for i in range(count):
+            if status[i] == STATUS_CORRECTION_ERROR:
+                err[i] = int(FsError.BlockDevice_CorrectionError)  # block left untouched
+            elif status[i] == STATUS_CORRECTED:
+                self._log(first + i)  # the old block's write-back is overwritten below
+        w = self._disk.write(first * self._raw, raw.tobytes())
+        if not w:
+            err[:] = int(w.error())
+        return err
+
     def readBlock(self, loc: DataLocation, bytes_to_read: int, capacity: Optional[int] = None) -> Expected[bytes]:
         if capacity is not None and capacity < bytes_to_read:
             return Expected.unexpected(FsError.Disk_InvalidRequest)
@@ -311,11 +385,15 @@ class ReedSolomonBlockDevice(_EngineDevice):  # rs_block_device.cpp
         fixed = raw.copy()
         e.decode_host(fixed, data, status, write_back=True, spill=spill)
         if status[0] == STATUS_CORRECTED:
-            self._log(block_index)  # :171-173
-            extra = int(spill[0]) if self._raw < 255 else 0
-            wb = fixed.tobytes() + (spill[1:1 + extra].tobytes() if extra else b"")
-            self._disk.write(block_index * self._raw, wb)  # result ignored (:180)
+            self._write_back(block_index, raw, fixed, spill)
         return Expected(data)
+
+    def _write_back(self, block_index, old, fixed, spill) -> Optional[FsError]:
+        self._log(block_index)  # :171-173
+        extra = int(spill[0]) if (spill is not None and self._raw < 255) else 0
+        wb = fixed.tobytes() + (spill[1:1 + extra].tobytes() if extra else b"")
+        self._disk.write(block_index * self._raw, wb)  # result ignored (:180)
+        return None
 
     def writeBlock(self, data, loc: DataLocation) -> Expected[int]:
         # the new codeword depends only on the patched payload (:61-93)
@@ -359,14 +437,20 @@ class HammingBlockDevice(_EngineDevice):  # hamming_block_device.cpp
         if status[0] == STATUS_CORRECTION_ERROR:
             return Expected.unexpected(FsError.BlockDevice_CorrectionError)
         if status[0] == STATUS_CORRECTED:
-            diff = np.nonzero(fixed != raw)[0]
-            byte = int(diff[0]) if diff.size else 0
-            w = self._disk.write(block_index * self._raw + byte, fixed[byte:byte + 1].tobytes())  # :41-51
-            if not w:
-                return Expected.unexpected(w.error())
+            fe = self._write_back(block_index, raw, fixed, None)
+            if fe is not None:
+                return Expected.unexpected(fe)
             raw[:] = fixed
-            self._log(block_index)  # :53-57
         return Expected(data)
+
+    def _write_back(self, block_index, old, fixed, spill) -> Optional[FsError]:
+        diff = np.nonzero(fixed != old)[0]
+        byte = int(diff[0]) if diff.size else 0
+        w = self._disk.write(block_index * self._raw + byte, fixed[byte:byte + 1].tobytes())  # :41-51
+        if not w:
+            return w.error()
+        self._log(block_index)  # :53-57
+        return None
 
 
 class ParityBlockDevice(_EngineDevice):  # parity_block_device.cpp
