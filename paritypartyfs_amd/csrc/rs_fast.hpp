@@ -164,6 +164,45 @@ template <int W, int N> __device__ __forceinline__ void xor_into(uint32_t (&acc)
     }
 }
 
+#ifndef PPFS_SDWA_ADDR
+#define PPFS_SDWA_ADDR 1
+#endif
+#ifndef PPFS_ENC_DIRECT_EMIT
+#define PPFS_ENC_DIRECT_EMIT 1
+#endif
+// (x >> 8K) & 0xF0 in one VALU op (SDWA byte select; LLVM only forms it for K = 2, 3)
+template <int K> __device__ __forceinline__ uint32_t nib16(uint32_t x)
+{
+    if constexpr (K == 0) {
+        return x & 0xF0u;
+    } else {
+        uint32_t r;
+        if constexpr (K == 1)
+            asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+                : "=v"(r) : "v"(x), "s"(0xF0u));
+        else if constexpr (K == 2)
+            asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD"
+                : "=v"(r) : "v"(x), "s"(0xF0u));
+        else
+            asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD"
+                : "=v"(r) : "v"(x), "s"(0xF0u));
+        return r;
+    }
+}
+
+// the 2 NL table reads of one slicing step (compile-time byte positions P..NL-1)
+template <int W, int NL, int P>
+__device__ __forceinline__ void slice_lookups(Ent<W> (&e)[2 * NL], uint32_t lo, uint32_t hi, uint32_t lo4, uint32_t hi4,
+    const uint8_t* lds)
+{
+    if constexpr (P < NL) {
+        const uint32_t x = P < 4 ? lo : hi, x4 = P < 4 ? lo4 : hi4;
+        e[2 * P] = tbl_ld<W>(lds, nib16<P & 3>(x4) + (2 * P) * 256);
+        e[2 * P + 1] = tbl_ld<W>(lds, nib16<P & 3>(x) + (2 * P + 1) * 256);
+        slice_lookups<W, NL, P + 1>(e, lo, hi, lo4, hi4, lds);
+    }
+}
+
 // st <- (st * x^8 + sum_i chunk_i x^(2t+i)) mod g, top-aligned state.
 // NB = number of chunk bytes that may be non-zero when FIRST (state still zero).
 template <int W, bool FIRST, int NB>
@@ -179,10 +218,15 @@ __device__ __forceinline__ void slice8(uint32_t (&st)[W], uint32_t lo, uint32_t 
 #pragma unroll
     for (int w = 2; w < W; ++w)
         acc[w] = FIRST ? 0u : st[w - 2];
-    const uint32_t ll = (lo << 4) & 0xF0F0F0F0u, lh = lo & 0xF0F0F0F0u;
-    const uint32_t hl = (hi << 4) & 0xF0F0F0F0u, hh = hi & 0xF0F0F0F0u;
     constexpr int NL = FIRST ? (NB < 8 ? NB : 8) : 8;
     Ent<W> e[2 * NL];
+#if PPFS_SDWA_ADDR
+    // slot address of a nibble = nibble * 16: the high nibble of byte k is (x >> 8k) & 0xF0,
+    // the low one (x << 4 >> 8k) & 0xF0 -- one v_and_b32_sdwa (byte select) each
+    slice_lookups<W, NL, 0>(e, lo, hi, lo << 4, hi << 4, lds);
+#else
+    const uint32_t ll = (lo << 4) & 0xF0F0F0F0u, lh = lo & 0xF0F0F0F0u;
+    const uint32_t hl = (hi << 4) & 0xF0F0F0F0u, hh = hi & 0xF0F0F0F0u;
 #pragma unroll
     for (int p = 0; p < NL; ++p) {
         const uint32_t xl = p < 4 ? ll : hl, xh = p < 4 ? lh : hh;
@@ -190,6 +234,7 @@ __device__ __forceinline__ void slice8(uint32_t (&st)[W], uint32_t lo, uint32_t 
         e[2 * p] = tbl_ld<W>(lds, ((xl >> sh) & 0xFFu) + (2 * p) * 256);
         e[2 * p + 1] = tbl_ld<W>(lds, ((xh >> sh) & 0xFFu) + (2 * p + 1) * 256);
     }
+#endif
     xor_into<W, 2 * NL>(acc, e);
 #pragma unroll
     for (int w = 0; w < W; ++w)
@@ -368,15 +413,14 @@ __device__ __forceinline__ void emit_row(uint8_t* tile, uint32_t out, int cbase,
 // Exact reference correction from r' = x^2t c(x) mod g.  Calls fix(pos, e) for every root of
 // sigma over all 255 field values.
 // ------------------------------------------------------------------------------------
-template <int T2, typename Fix>
-__device__ __forceinline__ void rs_correct(const uint32_t (&r)[T2], const Gf& gf, Fix&& fix)
+// S_i = c(a^i) = r'(a^i) * a^(-2t i), i = 1..2t   (rs_block_device.cpp:131-141)
+template <int T2>
+__device__ __forceinline__ void rs_syndromes(const uint32_t (&r)[T2], const Gf& gf, uint32_t (&S)[T2])
 {
-    // S_i = c(a^i) = r'(a^i) * a^(-2t i), i = 1..2t   (rs_block_device.cpp:131-141)
     uint32_t lr[T2];
 #pragma unroll
     for (int q = 0; q < T2; ++q)
         lr[q] = gf.log(r[q]);
-    uint32_t S[T2];
 #pragma unroll
     for (int i = 1; i <= T2; ++i) {
         uint32_t s = 0;
@@ -388,28 +432,39 @@ __device__ __forceinline__ void rs_correct(const uint32_t (&r)[T2], const Gf& gf
         }
         S[i - 1] = s;
     }
-    // Geometric syndromes S_i = S_1 X^(i-1) (all non-zero): the shortest LFSR of the sequence is
-    // 1 + X x, which is what Berlekamp-Massey returns for it (its output depends on S only), so
-    // the reference corrects exactly one byte: root v = 1/X -> pos = LOG[X],
-    // Omega = S_1 (higher terms cancel), e = Omega(v) / sigma'(v) = S_1 / X.
-    // This is the single-error case; it skips BM / Omega / Forney.
-    {
-        uint32_t ls[T2];
-        bool geo = true;
+}
+
+// Geometric syndromes S_i = S_1 X^(i-1) (all non-zero): the shortest LFSR of the sequence is
+// 1 + X x, which is what Berlekamp-Massey returns for it (its output depends on S only), so
+// the reference corrects exactly one byte: root v = 1/X -> pos = LOG[X],
+// Omega = S_1 (higher terms cancel), e = Omega(v) / sigma'(v) = S_1 / X.
+// This is the single-error case; it skips BM / Omega / Forney.
+template <int T2>
+__device__ __forceinline__ bool rs_geometric(const uint32_t (&S)[T2], const Gf& gf, uint32_t& pos, uint32_t& e)
+{
+    uint32_t ls[T2];
+    bool geo = true;
 #pragma unroll
-        for (int i = 0; i < T2; ++i) {
-            ls[i] = gf.log(S[i]);
-            geo = geo && S[i] != 0;
-        }
-        const uint32_t lx = (ls[1] + 255u - ls[0]) % 255u;
-#pragma unroll
-        for (int i = 1; i + 1 < T2; ++i)
-            geo = geo && (ls[i + 1] + 255u - ls[i]) % 255u == lx;
-        if (geo) {
-            fix(lx, gf.exp(ls[0] + 255u - lx));
-            return;
-        }
+    for (int i = 0; i < T2; ++i) {
+        ls[i] = gf.log(S[i]);
+        geo = geo && S[i] != 0;
     }
+    const uint32_t lx = (ls[1] + 255u - ls[0]) % 255u;
+#pragma unroll
+    for (int i = 1; i + 1 < T2; ++i)
+        geo = geo && (ls[i + 1] + 255u - ls[i]) % 255u == lx;
+    pos = lx;
+    e = gf.exp(ls[0] + 255u - lx);
+    return geo;
+}
+
+// ------------------------------------------------------------------------------------
+// Exact reference correction from the syndromes (general case).  Calls fix(pos, e) for every
+// root of sigma over all 255 field values.
+// ------------------------------------------------------------------------------------
+template <int T2, typename Fix>
+__device__ __forceinline__ void rs_correct_general(const uint32_t (&S)[T2], const Gf& gf, Fix&& fix)
+{
     // Berlekamp-Massey (rs_block_device.cpp:234-269) with Bs = x^m * B kept pre-shifted.
     uint32_t sig[T2 + 1], Bs[T2 + 1];
 #pragma unroll
@@ -561,9 +616,85 @@ __device__ __forceinline__ void rs_encode_lane(uint8_t* tile, const uint8_t* lds
         }
         return v;
     };
+#if PPFS_ENC_DIRECT_EMIT
+    if constexpr (T2 >= 4) {
+        // Direct emission: v_q = funnel(R[q+1], R[q]) by sh = 8 * ((2a - 2t) mod 4) bits holds
+        // payload bytes 4q + sh/8 - a .. +3, whose output position ob + 2t + 4q + sh/8 - a is
+        // 4-aligned (ob = 255 l = -a mod 4, and 2t is even): one v_alignbit + one ds_write_b32
+        // per dword, no per-lane register selection.  The first and last dwords may carry up to
+        // 3 stray bytes into this row's / the next row's parity field (2t >= 4 >= 3 bytes);
+        // the parity bytes are written after every lane's payload dwords, over them.
+        const uint32_t ob = RS_N * l;
+        const uint32_t sb = ((2u * a) - (uint32_t)T2) & 3u; // sh / 8, 0 or 2
+        const uint32_t shb = 8u * sb;
+        const int qlo = (int)sb > (int)a ? -1 : 0;         // 4q + sb - a <= 0
+        uint8_t* dst = tile + ob + T2 + sb - a;            // + 4q
+        if (qlo < 0)
+            *(uint32_t*)(dst - 4) = __builtin_amdgcn_alignbit(R[0], 0u, shb);
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+            // dword q starts at payload byte 4q + sb - a: written iff that is <= K - 1, so a
+            // row's last dword reaches at most 3 bytes past the row (into the next parity field)
+            const uint32_t v = __builtin_amdgcn_alignbit(rget<NR>(R, q + 1), R[q], shb);
+            if (4 * q + 3 <= K - 1)
+                *(uint32_t*)(dst + 4 * q) = v;
+            else if (4 * q + (int)sb - (int)a <= K - 1)
+                *(uint32_t*)(dst + 4 * q) = v;
+        }
+        asm volatile("" ::: "memory"); // every lane's payload dwords precede any parity byte
+#pragma unroll
+        for (int q = 0; q < T2; ++q) {
+            const int P = 4 * W - T2 + q;
+            tile[ob + q] = (uint8_t)(st[P >> 2] >> (8 * (P & 3)));
+        }
+        return;
+    }
+#endif
     // payload byte j at register byte a + j -> stream byte p at register byte a + p - 2t
     emit_row<NR, RS_N, -T2, 3 - T2, T2>(tile, RS_N * l, (int)a - T2, R, par);
 }
+
+// Decode emission: payload row of lane l at ob = K l from the codeword dwords R (codeword byte c
+// at register byte a + c).  v_q = funnel(R[q+1], R[q]) by sb bytes holds payload bytes
+// 4q + sb - 2t - a .. +3 at ob + 4q + sb - 2t - a, 4-aligned for sb = 2t (1 - a) mod 4.  Dwords
+// inside the row for every lane are plain ds_write_b32; the few that may straddle a row end
+// (classified at compile time) write only their in-row bytes.
+template <int T2, int NR>
+__device__ __forceinline__ void emit_payload_direct(uint8_t* tile, uint32_t l, uint32_t a, const uint32_t (&R)[NR])
+{
+    constexpr int K = RS_N - T2;
+    const uint32_t ob = (uint32_t)K * l;
+    const uint32_t sb = ((uint32_t)T2 * (1u - a)) & 3u;
+    const uint32_t shb = 8u * sb;
+    const int off = (int)sb - T2 - (int)a; // dest(q) - ob = 4q + off, off in [-T2-3, -T2+2]
+    uint8_t* dst = tile + (int)ob + off;
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+        constexpr int dummy = 0;
+        (void)dummy;
+        const int lo = 4 * q - T2 - 3, hi = 4 * q - T2 + 2; // range of 4q + off over lanes
+        if (hi + 3 < 0 || lo > K - 1)
+            continue; // never touches the row
+        const uint32_t v = __builtin_amdgcn_alignbit(rget<NR>(R, q + 1), R[q], shb);
+        if (lo >= 0 && hi + 3 <= K - 1) {
+            *(uint32_t*)(dst + 4 * q) = v;
+        } else {
+            const int d0 = 4 * q + off; // row offset of byte 0 of v
+            if (d0 >= 0 && d0 + 3 <= K - 1) {
+                *(uint32_t*)(dst + 4 * q) = v;
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (d0 + k >= 0 && d0 + k <= K - 1)
+                        dst[4 * q + k] = (uint8_t)(v >> (8 * k));
+            }
+        }
+    }
+}
+
+#ifndef PPFS_DEC_DIRECT_EMIT
+#define PPFS_DEC_DIRECT_EMIT 1
+#endif
 
 template <int T2, int NS, typename Pre>
 __device__ __forceinline__ void rs_decode_lane(uint8_t* tile, const uint8_t* lds, uint32_t l, bool valid,
@@ -587,7 +718,13 @@ __device__ __forceinline__ void rs_decode_lane(uint8_t* tile, const uint8_t* lds
     for (int w = 0; w < W; ++w)
         any |= st[w];
     const bool err = valid && any != 0;
+    // a single corrected payload byte, applied to the output row after emission
+    uint32_t fpos = 0xFFFFFFFFu, fval = 0;
     if (__builtin_amdgcn_ballot_w64(err)) {
+        const Gf gf { lds + Cf::OFF_GF };
+        uint32_t S[T2];
+        bool geo = false;
+        uint32_t gpos = 0, ge = 0;
         if (err) {
             uint32_t r[T2];
 #pragma unroll
@@ -595,29 +732,52 @@ __device__ __forceinline__ void rs_decode_lane(uint8_t* tile, const uint8_t* lds
                 const int P = 4 * W - T2 + q;
                 r[q] = (st[P >> 2] >> (8 * (P & 3))) & 0xFFu;
             }
-            const Gf gf { lds + Cf::OFF_GF };
-            // corrections patch the lane's own row of the LDS tile (other lanes only ever use
-            // their own bytes of the words they share with this row); R is reloaded below.
-            rs_correct<T2>(r, gf, [&](uint32_t pos, uint32_t e) {
+            rs_syndromes<T2>(r, gf, S);
+            geo = rs_geometric<T2>(S, gf, gpos, ge);
+        }
+        if (__builtin_amdgcn_ballot_w64(err && !geo)) {
+            // general path somewhere in the wave: corrections patch each lane's own row of the
+            // LDS tile (other lanes only use their own bytes of shared words), then the whole
+            // wave reloads R, which is therefore dead through the register-hungry BM code
+            auto fix = [&](uint32_t pos, uint32_t e) {
                 if (e == 0)
                     return;
                 const uint8_t fixed = (uint8_t)(tile[ib + pos] ^ e);
                 tile[ib + pos] = fixed;
                 if (write_back)
                     raw_g[blk * RS_N + pos] = fixed;
-            });
-        }
-        // whole-wave reload: R is dead throughout the (register-hungry) correction code
+            };
+            if (err) {
+                if (geo)
+                    fix(gpos, ge);
+                else
+                    rs_correct_general<T2>(S, gf, fix);
+            }
 #pragma unroll
-        for (int q = 0; q < NR; ++q)
-            R[q] = tw[q];
+            for (int q = 0; q < NR; ++q)
+                R[q] = tw[q];
+        } else if (geo && ge != 0) {
+            // single-error lanes only: R stays as read; the byte is patched after emission
+            const uint8_t fixed = (uint8_t)(tile[ib + gpos] ^ ge);
+            if (write_back)
+                raw_g[blk * RS_N + gpos] = fixed;
+            fpos = gpos;
+            fval = fixed;
+        }
     }
     status_lds[l] = err ? 1 : 0;
     if (!want_data)
         return;
     wave_fence();
+#if PPFS_DEC_DIRECT_EMIT
+    emit_payload_direct<T2, NR>(tile, l, a, R);
+#else
     // payload byte j = codeword byte 2t + j at register byte a + 2t + j
     emit_row<NR, K, T2, T2 + 3, 0>(tile, K * l, (int)a + T2, R, [](uint32_t v, int) { return v; });
+#endif
+    // the row's own bytes only: ordered after this lane's emission stores
+    if (fpos >= (uint32_t)T2 && fpos != 0xFFFFFFFFu)
+        tile[K * l + fpos - T2] = (uint8_t)fval;
 }
 
 // ------------------------------------------------------------------------------------
@@ -704,10 +864,35 @@ __device__ __forceinline__ void load_regs(uint4 (&L)[(NPIECE + 63) / 64], const 
 
 // conditional prefetch that defines L on both paths: a conditionally-kept L would stay live
 // (and be spilled) through the whole loop body
+#ifndef PPFS_BRANCHLESS_PF
+#define PPFS_BRANCHLESS_PF 1
+#endif
 template <int NPIECE, int NT = 0>
 __device__ __forceinline__ void load_regs_if(bool cond, uint4 (&L)[(NPIECE + 63) / 64], const uint8_t* __restrict__ src,
-    uint32_t lane)
+    uint32_t lane, const uint8_t* __restrict__ dummy = nullptr)
 {
+#if PPFS_BRANCHLESS_PF
+    if (dummy) {
+        // branch-free: without a next tile the loads re-read a 1 KiB L2-resident region, so the
+        // loads are unconditional and the waitcnt pass can count them (a branch around them
+        // makes it fall back to vmcnt(0), which also waits for this tile's stores)
+        const uint8_t* base = cond ? src : dummy;
+        const uint32_t wrap = cond ? 0xFFFFFFFFu : 1023u;
+#pragma unroll
+        for (int k = 0; k < (NPIECE + 63) / 64; ++k) {
+            const uint32_t p = lane + 64 * k;
+            const uint32_t off = ((k < NPIECE / 64 || p < NPIECE) ? p * 16u : 0u) & wrap;
+            const uint4* q = (const uint4*)(base + off);
+            if constexpr (NT) {
+                const u32x4 v = __builtin_nontemporal_load((const u32x4*)q);
+                L[k] = make_uint4(v.x, v.y, v.z, v.w);
+            } else {
+                L[k] = *q;
+            }
+        }
+        return;
+    }
+#endif
     if (cond) {
         load_regs<NPIECE, NT>(L, src, lane);
     } else {
@@ -748,38 +933,46 @@ __global__ __launch_bounds__(256, 2) void rs255_encode_kernel(const uint8_t* __r
     const uint64_t nfull = nblocks / RS_WT;
     const uint64_t stride = (uint64_t)gridDim.x * RS_WAVES;
     uint64_t wt = (uint64_t)blockIdx.x * RS_WAVES + wave;
+    // Full tiles: a straight-line body (fixed numbers of loads and stores), so the compiler's
+    // waitcnt pass counts the in-flight prefetch instead of draining this tile's stores.
+    // PF = 2: one-shot (grid covers every tile, no prefetch: other waves hide the latency)
     uint4 L[(IN_PIECES + 63) / 64];
-    load_regs_if<IN_PIECES, NT>(wt < nfull, L, data + wt * RS_WT * K, lane);
-    for (; wt < ntiles; wt += stride) {
+    if (PF != 2)
+        load_regs_if<IN_PIECES, NT>(wt < nfull, L, data + wt * RS_WT * K, lane, tables);
+    for (; wt < nfull; wt += stride) {
         const uint64_t b0 = wt * RS_WT;
-        const uint32_t nb = (uint32_t)min((uint64_t)RS_WT, nblocks - b0);
-        if (nb == RS_WT)
-            write_regs<IN_PIECES>(tile, L, lane); // loads issued one tile earlier
-        else
-            wave_stage_in(tile, data + b0 * K, nb * K, lane);
+        if (PF == 2)
+            load_regs<IN_PIECES, NT>(L, data + b0 * K, lane);
+        write_regs<IN_PIECES>(tile, L, lane); // loads issued one tile earlier
         wave_fence();
         const uint64_t nx = wt + stride;
         if constexpr (!MEMONLY) {
             rs_encode_lane<T2, NS>(tile, lds, lane, [&]() {
                 // block is in registers: prefetch the next tile now, its latency hides under compute
-                if (PF)
-                    load_regs_if<IN_PIECES, NT>(nx < nfull, L, data + nx * RS_WT * K, lane);
+                if (PF == 1)
+                    load_regs_if<IN_PIECES, NT>(nx < nfull, L, data + nx * RS_WT * K, lane, tables);
             });
         } else {
-            if (PF)
-                load_regs_if<IN_PIECES, NT>(nx < nfull, L, data + nx * RS_WT * K, lane);
+            if (PF == 1)
+                load_regs_if<IN_PIECES, NT>(nx < nfull, L, data + nx * RS_WT * K, lane, tables);
         }
         wave_fence();
-        if (nb == RS_WT) {
-            uint4 o[(OUT_PIECES + 63) / 64];
-            read_tile<OUT_PIECES>(o, tile, lane);
-            if (!PF)
-                load_regs_if<IN_PIECES, NT>(nx < nfull, L, data + nx * RS_WT * K, lane);
-            store_tile<OUT_PIECES, NT>(raw + b0 * RS_N, o, lane);
-        } else {
-            wave_stage_out(raw + b0 * RS_N, tile, nb * RS_N, lane);
-        }
+        uint4 o[(OUT_PIECES + 63) / 64];
+        read_tile<OUT_PIECES>(o, tile, lane);
+        if (PF == 0)
+            load_regs_if<IN_PIECES, NT>(nx < nfull, L, data + nx * RS_WT * K, lane, tables);
+        store_tile<OUT_PIECES, NT>(raw + b0 * RS_N, o, lane);
         wave_fence();
+    }
+    // the one partial tile (nblocks % 64 blocks), by the wave whose walk reaches it
+    if (wt == nfull && nfull < ntiles) {
+        const uint64_t b0 = wt * RS_WT;
+        const uint32_t nb = (uint32_t)(nblocks - b0);
+        wave_stage_in(tile, data + b0 * K, nb * K, lane);
+        wave_fence();
+        rs_encode_lane<T2, NS>(tile, lds, lane, []() {});
+        wave_fence();
+        wave_stage_out(raw + b0 * RS_N, tile, nb * RS_N, lane);
     }
 }
 
@@ -788,6 +981,7 @@ __global__ __launch_bounds__(256, 2) void rs255_encode_kernel(const uint8_t* __r
 //   1  next tile -> VGPRs after this tile's stores
 //   2  next tile -> VGPRs during the syndrome pass (prefetch, as encode)
 //   3  next tile -> LDS by DMA after this tile's stores
+//   4  one-shot: no prefetch (launch one wave per tile; other waves hide the load latency)
 // NT: bit 0 = non-temporal codeword loads, bit 1 = non-temporal payload stores.  Codeword
 // loads stay temporal by default: the write-back RMWs bytes of lines just read.
 template <int T2, int NS = 0, int STAGE = 1, int NT = 0>
@@ -812,60 +1006,57 @@ __global__ __launch_bounds__(256, 2) void rs255_decode_kernel(uint8_t* __restric
     const uint64_t stride = (uint64_t)gridDim.x * RS_WAVES;
     uint64_t wt = (uint64_t)blockIdx.x * RS_WAVES + wave;
     uint4 L[REGS ? (IN_PIECES + 63) / 64 : 1];
-    bool staged = false; // STAGE 3: the current tile already sits in LDS
-    if constexpr (REGS) {
-        load_regs_if<IN_PIECES, NT & 1>(wt < nfull, L, raw + wt * RS_WT * RS_N, lane);
+    if constexpr (STAGE == 4) {
+        // one-shot: loaded at the loop top
+    } else if constexpr (REGS) {
+        load_regs_if<IN_PIECES, NT & 1>(wt < nfull, L, raw + wt * RS_WT * RS_N, lane, tables);
     } else if (wt < nfull) {
         wave_dma_issue(tile, raw + wt * RS_WT * RS_N, IN_PIECES, lane);
-        staged = true;
     }
-    for (; wt < ntiles; wt += stride) {
+    for (; wt < nfull; wt += stride) {
         const uint64_t b0 = wt * RS_WT;
-        const uint32_t nb = (uint32_t)min((uint64_t)RS_WT, nblocks - b0);
-        if constexpr (REGS) {
-            if (nb == RS_WT)
-                write_regs<IN_PIECES>(tile, L, lane);
-            else
-                wave_stage_in(tile, raw + b0 * RS_N, nb * RS_N, lane);
-        } else {
-            if (staged)
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            else
-                wave_stage_in(tile, raw + b0 * RS_N, nb * RS_N, lane);
-        }
+        if constexpr (STAGE == 4)
+            load_regs<IN_PIECES, NT & 1>(L, raw + b0 * RS_N, lane);
+        if constexpr (REGS)
+            write_regs<IN_PIECES>(tile, L, lane);
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         wave_fence();
         const uint64_t nx = wt + stride;
         const bool nfullx = nx < nfull;
-        rs_decode_lane<T2, NS>(tile, lds, lane, lane < nb, raw, b0 + lane, wb, want, st_lds, [&]() {
+        rs_decode_lane<T2, NS>(tile, lds, lane, true, raw, b0 + lane, wb, want, st_lds, [&]() {
             if constexpr (STAGE == 2)
-                load_regs_if<IN_PIECES, NT & 1>(nfullx, L, raw + nx * RS_WT * RS_N, lane);
+                load_regs_if<IN_PIECES, NT & 1>(nfullx, L, raw + nx * RS_WT * RS_N, lane, tables);
         });
         wave_fence();
-        if (nb == RS_WT) {
-            uint4 o[(OUT_PIECES + 63) / 64];
-            if (want)
-                read_tile<OUT_PIECES>(o, tile, lane);
-            const uint4 sv = (lane < 4) ? *(const uint4*)(st_lds + 16 * lane) : make_uint4(0, 0, 0, 0);
-            if constexpr (STAGE == 0)
-                load_regs_if<IN_PIECES, NT & 1>(nfullx, L, raw + nx * RS_WT * RS_N, lane);
-            if (want)
-                store_tile<OUT_PIECES, (NT >> 1) & 1>(data + b0 * K, o, lane);
-            if (status && lane < 4)
-                *(uint4*)(status + b0 + 16 * lane) = sv;
-        } else {
-            if (want)
-                wave_stage_out(data + b0 * K, tile, nb * K, lane);
-            if (status)
-                wave_stage_out(status + b0, st_lds, nb, lane);
-        }
+        uint4 o[(OUT_PIECES + 63) / 64];
+        if (want)
+            read_tile<OUT_PIECES>(o, tile, lane);
+        const uint4 sv = (lane < 4) ? *(const uint4*)(st_lds + 16 * lane) : make_uint4(0, 0, 0, 0);
+        if constexpr (STAGE == 0)
+            load_regs_if<IN_PIECES, NT & 1>(nfullx, L, raw + nx * RS_WT * RS_N, lane, tables);
+        if (want)
+            store_tile<OUT_PIECES, (NT >> 1) & 1>(data + b0 * K, o, lane);
+        if (status && lane < 4)
+            *(uint4*)(status + b0 + 16 * lane) = sv;
         if constexpr (STAGE == 1)
-            load_regs_if<IN_PIECES, NT & 1>(nfullx, L, raw + nx * RS_WT * RS_N, lane);
+            load_regs_if<IN_PIECES, NT & 1>(nfullx, L, raw + nx * RS_WT * RS_N, lane, tables);
         wave_fence();
-        if constexpr (STAGE == 3) {
-            staged = nfullx;
+        if constexpr (STAGE == 3)
             if (nfullx)
                 wave_dma_issue(tile, raw + nx * RS_WT * RS_N, IN_PIECES, lane);
-        }
+    }
+    if (wt == nfull && nfull < ntiles) {
+        const uint64_t b0 = wt * RS_WT;
+        const uint32_t nb = (uint32_t)(nblocks - b0);
+        wave_stage_in(tile, raw + b0 * RS_N, nb * RS_N, lane);
+        wave_fence();
+        rs_decode_lane<T2, NS>(tile, lds, lane, lane < nb, raw, b0 + lane, wb, want, st_lds, []() {});
+        wave_fence();
+        if (want)
+            wave_stage_out(data + b0 * K, tile, nb * K, lane);
+        if (status)
+            wave_stage_out(status + b0, st_lds, nb, lane);
     }
 }
 

@@ -35,6 +35,7 @@ struct Bufs {
     uint8_t *d, *cw, *bad, *out, *st, *tab;
     uint64_t nb;
     int grid;
+    int grid1; // one wave per tile
 };
 
 __global__ void inject(uint8_t* cw, uint64_t nb)
@@ -61,7 +62,7 @@ template <int STAGE, int NT = 1, int WB = 1> float t_dec(const Bufs& b, bool che
         if (g_inject)
             hipLaunchKernelGGL(inject, dim3((b.nb + 255) / 256), dim3(256), 0, 0, b.bad, b.nb);
         hipEventRecord(e0);
-        hipLaunchKernelGGL((rs255_decode_kernel<6, 0, STAGE, NT>), dim3(b.grid), dim3(256), 0, 0, b.bad, b.out, b.st,
+        hipLaunchKernelGGL((rs255_decode_kernel<6, 0, STAGE, NT>), dim3(STAGE == 4 ? b.grid1 : b.grid), dim3(256), 0, 0, b.bad, b.out, b.st,
             b.nb, b.tab, WB);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
@@ -81,19 +82,61 @@ template <int STAGE, int NT = 1, int WB = 1> float t_dec(const Bufs& b, bool che
     return tot / 10 * 1e3f;
 }
 
-float t_enc(const Bufs& b)
+template <int PF, int NT, int MO> float t_enc(const Bufs& b)
 {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
+    hipLaunchKernelGGL((rs255_encode_kernel<6, 0, PF, NT, MO>), dim3(PF == 2 ? b.grid1 : b.grid), dim3(256), 0, 0, b.d, b.cw, b.nb, b.tab);
     hipEventRecord(e0);
     for (int i = 0; i < 10; ++i)
+        hipLaunchKernelGGL((rs255_encode_kernel<6, 0, PF, NT, MO>), dim3(PF == 2 ? b.grid1 : b.grid), dim3(256), 0, 0, b.d,
+            b.cw, b.nb, b.tab);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    // MEMONLY leaves cw garbage: restore real codewords
+    if (MO)
         hipLaunchKernelGGL((rs255_encode_kernel<6>), dim3(b.grid), dim3(256), 0, 0, b.d, b.cw, b.nb, b.tab);
+    return ms / 10 * 1e3f;
+}
+
+template <int PF, int NT> float t_enc_grid(const Bufs& b, int grid)
+{
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipLaunchKernelGGL((rs255_encode_kernel<6, 0, PF, NT, 0>), dim3(grid), dim3(256), 0, 0, b.d, b.cw, b.nb, b.tab);
+    hipEventRecord(e0);
+    for (int i = 0; i < 10; ++i)
+        hipLaunchKernelGGL((rs255_encode_kernel<6, 0, PF, NT, 0>), dim3(grid), dim3(256), 0, 0, b.d, b.cw, b.nb, b.tab);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float ms = 0;
     hipEventElapsedTime(&ms, e0, e1);
     return ms / 10 * 1e3f;
+}
+
+template <int STAGE, int NT> float t_dec_grid(const Bufs& b, int grid)
+{
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    float tot = 0;
+    for (int i = 0; i < 10; ++i) {
+        hipMemcpy(b.bad, b.cw, b.nb * 255, hipMemcpyDeviceToDevice);
+        hipLaunchKernelGGL(inject, dim3((b.nb + 255) / 256), dim3(256), 0, 0, b.bad, b.nb);
+        hipEventRecord(e0);
+        hipLaunchKernelGGL((rs255_decode_kernel<6, 0, STAGE, NT>), dim3(grid), dim3(256), 0, 0, b.bad, b.out, b.st,
+            b.nb, b.tab, 1);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms = 0;
+        hipEventElapsedTime(&ms, e0, e1);
+        tot += ms;
+    }
+    return tot / 10 * 1e3f;
 }
 
 int main()
@@ -119,40 +162,31 @@ int main()
     int cus = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     b.grid = 2 * cus;
+    b.grid1 = (int)((b.nb / 64 + 3) / 4);
     const double bytes = b.nb * 504.0;
-    printf("encode (default) %.1f us\n", t_enc(b));
-    t_dec<1, 0>(b, true);
-    t_dec<1, 1>(b, true);
-    t_dec<1, 2>(b, true);
-    t_dec<1, 3>(b, true);
-    t_dec<2, 0>(b, true);
-    t_dec<2, 2>(b, true);
-    t_dec<0, 0>(b, true);
-    t_dec<1, 0, 0>(b, true);
-    t_dec<1, 2, 0>(b, true);
-    const char* names[] = { "S1 NT0", "S1 NTload", "S1 NTstore", "S2 NTstore", "S2 NT0", "S0 NT0",
-        "S1 NT0 no-wb", "S1 NTstore no-wb", "encode default", "S1 NT0 clean", "S1 NTstore clean" };
-    constexpr int NV = 11;
-    std::vector<float> dec[NV];
-    for (int rep = 0; rep < 5; ++rep) {
-        dec[0].push_back(t_dec<1, 0>(b, false));
-        dec[1].push_back(t_dec<1, 1>(b, false));
-        dec[2].push_back(t_dec<1, 2>(b, false));
-        dec[3].push_back(t_dec<2, 2>(b, false));
-        dec[4].push_back(t_dec<2, 0>(b, false));
-        dec[5].push_back(t_dec<0, 0>(b, false));
-        dec[6].push_back(t_dec<1, 0, 0>(b, false));
-        dec[7].push_back(t_dec<1, 2, 0>(b, false));
-        dec[8].push_back(t_enc(b));
-        g_inject = false;
-        dec[9].push_back(t_dec<1, 0>(b, false));
-        dec[10].push_back(t_dec<1, 2>(b, false));
-        g_inject = true;
+    printf("encode (default) %.1f us\n", t_enc<1, 1, 0>(b));
+    for (int mult : { 2, 4, 8, 16, 32, 64 }) {
+        const int g = std::min(mult * cus, b.grid1);
+        std::vector<float> e, d1, d2;
+        for (int rep = 0; rep < 5; ++rep) {
+            e.push_back(t_enc_grid<1, 1>(b, g));
+            d1.push_back(t_dec_grid<1, 2>(b, g));
+            d2.push_back(t_dec_grid<2, 2>(b, g));
+        }
+        std::sort(e.begin(), e.end());
+        std::sort(d1.begin(), d1.end());
+        std::sort(d2.begin(), d2.end());
+        printf("grid %5d (%4.1f tiles/wave): enc PF1 %.1f us | dec S1 NTstore %.1f us | dec S2 NTstore %.1f us\n", g,
+            (double)(b.nb / 64) / (4.0 * g), e[2], d1[2], d2[2]);
     }
-    for (int v = 0; v < NV; ++v) {
-        std::sort(dec[v].begin(), dec[v].end());
-        printf("%-22s %.1f us (%.0f GB/s)  [min %.1f max %.1f]\n", names[v], dec[v][2],
-            bytes / (dec[v][2] * 1e-6) / 1e9, dec[v][0], dec[v][4]);
+    // oneshot encode correctness: codewords equal the persistent kernel's
+    {
+        std::vector<uint8_t> c1(b.nb * 255), c2(b.nb * 255);
+        hipLaunchKernelGGL((rs255_encode_kernel<6>), dim3(b.grid), dim3(256), 0, 0, b.d, b.cw, b.nb, b.tab);
+        hipMemcpy(c1.data(), b.cw, c1.size(), hipMemcpyDeviceToHost);
+        hipLaunchKernelGGL((rs255_encode_kernel<6, 0, 2, 1, 0>), dim3(b.grid1), dim3(256), 0, 0, b.d, b.cw, b.nb, b.tab);
+        hipMemcpy(c2.data(), b.cw, c2.size(), hipMemcpyDeviceToHost);
+        printf("oneshot encode %s\n", c1 == c2 ? "matches" : "MISMATCH");
     }
     return 0;
 }
