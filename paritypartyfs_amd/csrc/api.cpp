@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/ppfs_ecc.h"
+#include "rs_layout.hpp"
 
 // kernels (rs_kernels.hip / bit_kernels.hip)
 extern "C" {
@@ -178,6 +179,63 @@ std::vector<uint8_t> build_rs_slice_tables(int t2)
     return out;
 }
 
+// tables of the workgroup-cooperative RS path, 2t <= 8 (layout: rs_layout.hpp)
+template <int T2> std::vector<uint8_t> build_rs_wg_tables_t()
+{
+    using L = ppfs::RsWgLayout<T2>;
+    const GfHost& G = gf();
+    std::vector<uint8_t> out((size_t)L::TABLE_BYTES, 0);
+    const std::vector<uint8_t> g = rs_generator(T2);
+    // top-aligned 8-byte entry of a remainder r (coefficient q at byte 8 - 2t + q)
+    auto put = [&](int off, int table, int v, const std::vector<uint8_t>& r, uint8_t scale) {
+        for (int q = 0; q < T2; ++q)
+            out[(size_t)off + (size_t)table * L::TBL + (size_t)v * L::ES + (8 - T2 + q)] = G.mul(scale, r[q]);
+    };
+    for (int i = 0; i < 8; ++i) {
+        const std::vector<uint8_t> xi = rs_xpow_mod(T2 + i, g, T2);
+        for (int h = 0; h < 2; ++h)
+            for (int v = 0; v < 16; ++v)
+                put(L::OFF_SL, 2 * i + h, v, xi, (uint8_t)(v << (4 * h)));
+    }
+    for (int m = 0; m < 3; ++m)
+        for (int q = 0; q < T2; ++q) {
+            const std::vector<uint8_t> xq = rs_xpow_mod(q + 64 * (m + 1), g, T2);
+            for (int h = 0; h < 2; ++h)
+                for (int v = 0; v < 16; ++v)
+                    put(L::OFF_MAP + m * L::MAP_STRIDE, 2 * q + h, v, xq, (uint8_t)(v << (4 * h)));
+        }
+    for (int q = 0; q < T2; ++q)
+        for (int h = 0; h < 2; ++h)
+            for (int v = 0; v < 16; ++v)
+                for (int i = 1; i <= T2; ++i) {
+                    const int e = ((i * (q - T2)) % 255 + 255) % 255;
+                    out[(size_t)L::OFF_SYN + (size_t)(2 * q + h) * L::TBL + (size_t)v * L::ES + (i - 1)] =
+                        G.mul((uint8_t)(v << (4 * h)), G.exp[e]);
+                }
+    build_gf_block(out.data() + L::OFF_GF);
+    return out;
+}
+
+std::vector<uint8_t> build_rs_fast_tables(int t2)
+{
+    switch (t2) {
+    case 2:
+        return build_rs_wg_tables_t<2>();
+    case 4:
+        return build_rs_wg_tables_t<4>();
+    case 6:
+        return build_rs_wg_tables_t<6>();
+    case 8:
+        return build_rs_wg_tables_t<8>();
+    default: {
+        std::vector<uint8_t> s = build_rs_slice_tables(t2);
+        s.resize(s.size() + 1024);
+        build_gf_block(s.data() + s.size() - 1024);
+        return s;
+    }
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // CRC host maths over GF(2)[x] / P  (P explicit, degree n <= 63)
 // ---------------------------------------------------------------------------------------
@@ -317,11 +375,8 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
         c->rs_fast = ppfs_rs_fast_supported(c->rs_n, c->rs_t2) != 0;
         tables.resize(4096 + 8192 + 1024, 0);
         if (c->rs_fast) {
-            std::vector<uint8_t> s = build_rs_slice_tables(c->rs_t2);
-            tables.assign(s.begin(), s.end());
-            tables.resize(s.size() + 1024);
-            build_gf_block(tables.data() + s.size());
-            c->kname = "rs255-slice8-lds";
+            tables = build_rs_fast_tables(c->rs_t2);
+            c->kname = c->rs_t2 <= 8 ? "rs255-wg-seg4-lds" : "rs255-slice8-lds";
         } else {
             tables.assign(1024 + 256, 0);
             build_gf_block(tables.data());

@@ -1,5 +1,6 @@
 // rs_fast_inst.hip -- one fast-path instantiation (2t = PPFS_T2), compiled once per 2t.
 #include "rs_fast.hpp"
+#include "rs_wg.hpp"
 
 #ifndef PPFS_T2
 #error "compile with -DPPFS_T2=<2t>"
@@ -30,18 +31,40 @@ static uint32_t rs_grid(uint64_t nb)
     return (uint32_t)(want < cap ? (want ? want : 1) : cap);
 }
 
+// workgroup path (2t <= 8): one 256-thread workgroup per 64-block tile, three resident per CU
+static uint32_t rs_wg_grid(uint64_t nb)
+{
+    rs_grid(1); // caches the CU count
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+        c = 256;
+    const uint64_t tiles = (nb + wg::TB - 1) / wg::TB;
+    const uint64_t cap = 3ull * (uint64_t)c;
+    return (uint32_t)(tiles < cap ? (tiles ? tiles : 1) : cap);
+}
+
 extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d, uint8_t* r, uint64_t nb,
     const uint8_t* tab, hipStream_t s)
 {
+#if PPFS_T2 <= 8
+    hipLaunchKernelGGL(wg::rs_wg_encode_kernel<PPFS_T2>, dim3(rs_wg_grid(nb)), dim3(256), 0, s, d, r, nb, tab);
+#else
     const uint32_t grid = rs_grid(nb);
     hipLaunchKernelGGL(rs255_encode_kernel<PPFS_T2>, dim3(grid), dim3(256), 0, s, d, r, nb, tab);
+#endif
     return hipGetLastError();
 }
 
 extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb,
     const uint8_t* tab, int wb, hipStream_t s)
 {
+#if PPFS_T2 <= 8
+    hipLaunchKernelGGL(wg::rs_wg_decode_kernel<PPFS_T2>, dim3(rs_wg_grid(nb)), dim3(256), 0, s, r, d, st, nb, tab, wb);
+#else
     const uint32_t grid = rs_grid(nb);
     hipLaunchKernelGGL(rs255_decode_kernel<PPFS_T2>, dim3(grid), dim3(256), 0, s, r, d, st, nb, tab, wb);
+#endif
     return hipGetLastError();
 }

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "gf_common.hpp"
+#include "rs_layout.hpp"
 
 namespace ppfs {
 
@@ -198,7 +199,12 @@ extern "C" int ppfs_rs_fast_supported(int n, int t2)
     }
 }
 
-extern "C" int ppfs_rs_fast_tables_bytes(int t2) { return t2 <= 16 ? 4096 : 8192; }
+// device table blob of the fast path: workgroup layout (rs_layout.hpp) for 2t <= 8, else the
+// lane-per-block slicing tables (4 or 8 KiB) followed by the 1 KiB GF block
+extern "C" int ppfs_rs_fast_tables_bytes(int t2)
+{
+    return t2 <= 8 ? rs_wg_table_bytes(t2) : (t2 <= 16 ? 4096 : 8192);
+}
 
 extern "C" hipError_t ppfs_rs_fast_encode(int t2, const uint8_t* d, uint8_t* r, uint64_t nb, const uint8_t* tab,
     hipStream_t s)

@@ -1,0 +1,566 @@
+#pragma once
+// rs_wg.hpp -- workgroup-cooperative Reed-Solomon RS(255, 255-2t) encode / decode for gfx950, 2t <= 8.
+//
+// Reference semantics: lib/blockdevice/src/rs_block_device.cpp
+//   encode  _encodeBlock :95-117   c(x) = m(x) x^2t + (m(x) x^2t mod g(x)); byte i = coeff of x^i,
+//                                  parity in bytes [0,2t), payload in [2t,n)
+//   decode  _fixBlockAndExtract :119-183 (syndromes :131-141, all-zero fast return :143-146,
+//           Berlekamp-Massey :234-269, roots over all 255 field values :271-280, Omega :224-232,
+//           Forney :210-222, whole-codeword write-back :175-180)
+//
+// Work decomposition (one 256-thread workgroup = 4 waves per 64-block tile):
+//   - The tile's packed rows (64 x 249 B payloads or 64 x 255 B codewords, contiguous in HBM) are
+//     brought into LDS by LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave-instruction, 4 per
+//     lane), double-buffered: tile i+1 is in flight while tile i is computed.  Waits are counted
+//     (vmcnt) and the barriers are raw s_barrier, so the prefetch stays in flight across them.
+//   - Phase 1, remainder: lane l of wave s owns block l and computes the remainder of bytes
+//     [64s, 64s+64) of its row (slicing-by-8 over nibble tables), then moves it to its place with
+//     the x^(64 s) map, and XOR-accumulates it into the block's 8-byte slot in LDS (ds_xor_b64).
+//     The four segment chains run in parallel in four waves: 8 slicing steps per lane, not 32.
+//   - Phase 2 (decode only, wave 0): blocks with a non-zero remainder run the reference's
+//     correction (syndromes by nibble tables, single-error closed form, else BM / roots / Forney)
+//     and patch their bytes in the LDS tile and, with write-back, in HBM.
+//   - Phase 3, emission: every thread assembles 16-byte pieces of the OUTPUT tile straight from
+//     the LDS input rows (funnel shifts; parity bytes inserted at block starts) and stores them
+//     with 16-byte non-temporal stores.  No output staging in LDS.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gf_common.hpp"
+#include "rs_fast.hpp"
+#include "rs_layout.hpp"
+
+namespace ppfs {
+namespace wg {
+
+constexpr int TB = 64;      // blocks per tile
+constexpr int NTHR = 256;   // threads per workgroup
+constexpr int PAD = 16;     // front pad of a tile buffer (emission reads up to 2t bytes before row 0)
+constexpr int BUF = 16448;  // PAD + 64*255 + slack for over-reads, 16-byte multiple
+
+template <int T2> struct Lds {
+    using L = RsWgLayout<T2>;
+    static constexpr int OFF_PAR = L::TABLE_BYTES;        // 2 x 64 x 8 B remainder slots
+    static constexpr int OFF_BUF = OFF_PAR + 1024 + 64;  // + slack: par[b+1] over-read
+    static constexpr int BYTES = OFF_BUF + 2 * BUF;
+    static_assert(OFF_BUF % 16 == 0, "aligned buffers");
+    static_assert(3 * BYTES <= 163840, "three workgroups per CU");
+};
+
+__device__ __forceinline__ void barrier_lds()
+{
+    // every wave's LDS ops done, then the workgroup barrier; no vmcnt: LDS-DMA may stay in flight
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// One LDS-DMA wave-instruction (global_load_lds_dwordx4: 16 B per lane to lds_base + 16 * lane).
+// Issued from inline asm on purpose: hipcc tracks a builtin LDS-DMA and then waits vmcnt(0) before
+// every later LDS read, which would drain the next tile's prefetch.  The waits for these loads are
+// the explicit counted vmcnt in the kernels.  (M0 write -> LDS-DMA needs one wait state.)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm" // m0 is reserved; nothing else in these kernels uses it
+__device__ __forceinline__ void dma16(const uint8_t* g, uint32_t lds_base)
+{
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(lds_base)
+                 : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+__device__ __forceinline__ uint32_t lds_addr(const uint8_t* p)
+{
+    return (uint32_t)(size_t)(const __attribute__((address_space(3))) uint8_t*)p;
+}
+
+// LDS-DMA of NPIECE 16-byte pieces: piece p = tid + 256k lands at dst + 16p (wave-uniform base
+// dst + 1024 * (4k + wave), + 16 * lane implicit).  Exactly 4 instructions per wave.
+template <int NPIECE>
+__device__ __forceinline__ void dma_tile(uint8_t* dst, const uint8_t* __restrict__ src, uint32_t tid)
+{
+    static_assert(NPIECE > 768 && NPIECE <= 1024, "4 pieces per thread, every wave active in each");
+    const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(dst) + (tid & ~63u) * 16u);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t p = tid + 256u * k;
+        if (k < 3 || p < (uint32_t)NPIECE)
+            dma16(src + (size_t)p * 16, base + 4096u * k);
+    }
+}
+
+__device__ __forceinline__ uint2 ld8(const uint8_t* p) { return *(const uint2*)p; }
+
+// (x >> 8k) & 0x78: byte k of x, masked to a nibble * 8 (one v_and_b32_sdwa for k > 0)
+__device__ __forceinline__ uint32_t sel78(uint32_t x, int k)
+{
+    uint32_t r;
+    switch (k & 3) {
+    case 0:
+        return x & 0x78u;
+    case 1:
+        asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+            : "=v"(r) : "v"(x), "s"(0x78u));
+        return r;
+    case 2:
+        asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD"
+            : "=v"(r) : "v"(x), "s"(0x78u));
+        return r;
+    default:
+        asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD"
+            : "=v"(r) : "v"(x), "s"(0x78u));
+        return r;
+    }
+}
+
+// s ^= XOR of N 8-byte entries
+template <int N> __device__ __forceinline__ void xor_entries(uint32_t (&s)[2], const uint2 (&e)[N])
+{
+    uint32_t a = s[0], b = s[1];
+    int i = 0;
+#pragma unroll
+    for (; i + 1 < N; i += 2) {
+        a = xor3(a, e[i].x, e[i + 1].x);
+        b = xor3(b, e[i].y, e[i + 1].y);
+    }
+    if (i < N) {
+        a ^= e[i].x;
+        b ^= e[i].y;
+    }
+    s[0] = a;
+    s[1] = b;
+}
+
+// One slicing step: s <- (s x^8 + sum_i byte_i x^(2t+i)) mod g, top-aligned 8-byte state.
+// NB = bytes of the chunk that may be non-zero when FIRST (state still zero).
+template <bool FIRST, int NB>
+__device__ __forceinline__ void step8(uint32_t (&s)[2], uint32_t lo, uint32_t hi, const uint8_t* sl)
+{
+    if constexpr (!FIRST) {
+        lo ^= s[0];
+        hi ^= s[1];
+    }
+    constexpr int NL = FIRST ? NB : 8;
+    const uint32_t ll = lo << 3, lh = lo >> 1, hl = hi << 3, hh = hi >> 1;
+    uint2 e[2 * NL];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+        const uint32_t xl = i < 4 ? ll : hl, xh = i < 4 ? lh : hh;
+        e[2 * i] = ld8(sl + (2 * i) * 128 + sel78(xl, i));
+        e[2 * i + 1] = ld8(sl + (2 * i + 1) * 128 + sel78(xh, i));
+    }
+    // the whole 8-byte state was folded into the chunk: the new state is the XOR of the entries
+    s[0] = 0;
+    s[1] = 0;
+    xor_entries<2 * NL>(s, e);
+}
+
+// r = sum_j B[64S + j] x^(2t + j) mod g over segment S of a LEN-byte row at LDS byte `row`
+template <int T2, int LEN, int S>
+__device__ __forceinline__ void seg_remainder(uint32_t (&s)[2], const uint8_t* lds, uint32_t row)
+{
+    constexpr int LO = 64 * S;
+    constexpr int LS = (LEN - LO) < 64 ? (LEN - LO) : 64;
+    constexpr int NC = (LS + 7) / 8;
+    constexpr int TOPN = LS - 8 * (NC - 1);
+    constexpr int NR = 2 * NC + 1;
+    const uint32_t a0 = row + LO;
+    const uint32_t sh = (a0 & 3u) * 8u;
+    const uint32_t* w = (const uint32_t*)(lds + (a0 & ~3u));
+    uint32_t R[NR];
+#pragma unroll
+    for (int q = 0; q < NR; ++q)
+        R[q] = w[q];
+    const uint8_t* sl = lds + RsWgLayout<T2>::OFF_SL;
+#pragma unroll
+    for (int c = NC - 1; c >= 0; --c) {
+        uint32_t lo = __builtin_amdgcn_alignbit(R[2 * c + 1], R[2 * c], sh);
+        uint32_t hi = __builtin_amdgcn_alignbit(R[2 * c + 2], R[2 * c + 1], sh);
+        if (c == NC - 1) {
+            if constexpr (TOPN < 4) {
+                lo &= (1u << (8 * TOPN)) - 1u;
+                hi = 0;
+            } else if constexpr (TOPN == 4) {
+                hi = 0;
+            } else if constexpr (TOPN < 8) {
+                hi &= (1u << (8 * (TOPN - 4))) - 1u;
+            }
+            step8<true, TOPN>(s, lo, hi, sl);
+        } else {
+            step8<false, 8>(s, lo, hi, sl);
+        }
+    }
+}
+
+// s <- s(x) * x^(64 S) mod g through the segment's map tables (S >= 1)
+template <int T2, int S> __device__ __forceinline__ void seg_map(uint32_t (&s)[2], const uint8_t* lds)
+{
+    using L = RsWgLayout<T2>;
+    const uint8_t* mp = lds + L::OFF_MAP + (S - 1) * L::MAP_STRIDE;
+    uint2 e[2 * T2];
+#pragma unroll
+    for (int q = 0; q < T2; ++q) {
+        const int P = 8 - T2 + q;
+        const uint32_t x = s[P >> 2];
+        e[2 * q] = ld8(mp + (2 * q) * 128 + sel78(x << 3, P & 3));
+        e[2 * q + 1] = ld8(mp + (2 * q + 1) * 128 + sel78(x >> 1, P & 3));
+    }
+    s[0] = 0;
+    s[1] = 0;
+    xor_entries<2 * T2>(s, e);
+}
+
+// Phase 1 for this wave's segment: XOR its remainder into the block's slot
+template <int T2, int LEN>
+__device__ __forceinline__ void phase_remainder(uint8_t* lds, uint32_t buf, uint32_t par, uint32_t wave, uint32_t lane)
+{
+    const uint32_t row = buf + PAD + (uint32_t)LEN * lane;
+    uint32_t s[2];
+    switch (wave) {
+    case 0:
+        seg_remainder<T2, LEN, 0>(s, lds, row);
+        break;
+    case 1:
+        seg_remainder<T2, LEN, 1>(s, lds, row);
+        seg_map<T2, 1>(s, lds);
+        break;
+    case 2:
+        seg_remainder<T2, LEN, 2>(s, lds, row);
+        seg_map<T2, 2>(s, lds);
+        break;
+    default:
+        seg_remainder<T2, LEN, 3>(s, lds, row);
+        seg_map<T2, 3>(s, lds);
+        break;
+    }
+    const uint64_t v = ((uint64_t)s[1] << 32) | s[0];
+    __hip_atomic_fetch_xor((unsigned long long*)(lds + par + 8u * lane), (unsigned long long)v, __ATOMIC_RELAXED,
+        __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// bytes [lo, hi) of a 16-byte piece as a 128-bit mask (lo <= hi, both in [0, 16])
+struct M128 {
+    uint64_t lo, hi;
+};
+__device__ __forceinline__ uint64_t ones_below(uint32_t nbytes) // bytes [0, n) of a u64, n in [0, 8]
+{
+    return nbytes >= 8 ? ~0ull : ((1ull << (8 * nbytes)) - 1ull);
+}
+__device__ __forceinline__ M128 range_mask(uint32_t lo, uint32_t hi)
+{
+    const uint32_t l0 = lo < 8 ? lo : 8, h0 = hi < 8 ? hi : 8;
+    const uint32_t l1 = lo > 8 ? lo - 8 : 0, h1 = hi > 8 ? hi - 8 : 0;
+    return M128 { ones_below(h0) & ~ones_below(l0), ones_below(h1 < 8 ? h1 : 8) & ~ones_below(l1 < 8 ? l1 : 8) };
+}
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+
+// Encode emission: 16 bytes of the codeword tile at piece p, from the LDS payload rows and the
+// combined parity slots.  Codeword byte j of block b = j / 255 (off = j % 255): parity byte off if
+// off < 2t, else payload byte K b + off - 2t.  A piece may run into block b+1 (off > 239).
+template <int T2>
+__device__ __forceinline__ uint4 enc_piece(const uint8_t* lds, uint32_t buf, uint32_t par, uint32_t p)
+{
+    constexpr uint32_t K = 255 - T2;
+    const uint32_t j0 = p * 16u, b = j0 / 255u, off = j0 - 255u * b;
+    const uint32_t S = buf + PAD + K * b + off - T2; // LDS byte of output byte 0's payload source
+    const uint32_t* w = (const uint32_t*)(lds + (S & ~3u));
+    const uint32_t sh = (S & 3u) * 8u;
+    uint32_t d[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+        d[i] = w[i];
+    uint32_t X[4], Y[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+        X[m] = __builtin_amdgcn_alignbit(d[m + 1], d[m], sh);
+    // after the block boundary the source runs 2t bytes behind: Y byte k = X byte k - 2t
+    constexpr int q2 = T2 / 4, r2 = T2 % 4;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const uint32_t hi = (m - q2 >= 0) ? X[m - q2 >= 0 ? m - q2 : 0] : 0u;
+        const uint32_t lo = (m - q2 - 1 >= 0) ? X[m - q2 - 1 >= 0 ? m - q2 - 1 : 0] : 0u;
+        Y[m] = r2 ? __builtin_amdgcn_alignbit(hi, lo, 16) : hi;
+    }
+    // parity bytes of blocks b and b+1, byte q at byte q
+    const uint64_t P0 = *(const uint64_t*)(lds + par + 8u * b) >> (8 * (8 - T2));
+    const uint64_t P1 = *(const uint64_t*)(lds + par + 8u * b + 8u) >> (8 * (8 - T2));
+    const uint32_t kb = off > 239u ? 255u - off : 16u;    // first byte of block b+1 in the piece
+    const uint32_t c0 = off < (uint32_t)T2 ? T2 - off : 0u; // leading parity bytes of block b
+    // parity of b: bytes [0, c0) = P0 bytes off.. ; parity of b+1: bytes [kb, kb+2t) = P1 << 8 kb
+    const uint64_t pb0 = P0 >> (8 * (c0 ? off : 0u));
+    const uint64_t p1lo = kb < 8 ? (P1 << (8 * kb)) : 0ull;
+    const uint64_t p1hi = kb < 8 ? (kb ? (P1 >> (64 - 8 * kb)) : 0ull) : (kb < 16 ? (P1 << (8 * (kb - 8))) : 0ull);
+    const M128 mY = range_mask(kb + T2 < 16 ? kb + T2 : 16, 16);
+    const M128 mP1 = range_mask(kb, kb + T2 < 16 ? kb + T2 : 16);
+    const uint64_t mP0 = ones_below(c0);
+    uint32_t o[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const uint64_t my = m < 2 ? mY.lo : mY.hi, mp = m < 2 ? mP1.lo : mP1.hi, pp = m < 2 ? p1lo : p1hi;
+        const int sh32 = (m & 1) * 32;
+        uint32_t v = bfi((uint32_t)(my >> sh32), Y[m], X[m]);
+        v = bfi((uint32_t)(mp >> sh32), (uint32_t)(pp >> sh32), v);
+        if (m < 2)
+            v = bfi((uint32_t)(mP0 >> sh32), (uint32_t)(pb0 >> sh32), v);
+        o[m] = v;
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// Decode emission: 16 bytes of the payload tile at piece p from the (corrected) LDS codeword rows:
+// payload byte j of block b = j / K (off = j % K) is codeword byte 255 b + 2t + off.
+template <int T2> __device__ __forceinline__ uint4 dec_piece(const uint8_t* lds, uint32_t buf, uint32_t p)
+{
+    constexpr uint32_t K = 255 - T2;
+    const uint32_t j0 = p * 16u, b = j0 / K, off = j0 - K * b;
+    const uint32_t S = buf + PAD + 255u * b + T2 + off;
+    const uint32_t* w = (const uint32_t*)(lds + (S & ~3u));
+    const uint32_t sh = (S & 3u) * 8u;
+    uint32_t d[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+        d[i] = w[i];
+    uint32_t X[6];
+#pragma unroll
+    for (int m = 0; m < 6; ++m)
+        X[m] = __builtin_amdgcn_alignbit(d[m + 1], d[m], sh);
+    // past the block end the source skips block b+1's 2t parity bytes: Z byte k = X byte k + 2t
+    constexpr int q2 = T2 / 4, r2 = T2 % 4;
+    const uint32_t kb = off > K - 16u ? K - off : 16u;
+    const M128 mZ = range_mask(kb, 16);
+    uint32_t o[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        uint32_t Z;
+        if constexpr (r2 != 0)
+            Z = __builtin_amdgcn_alignbit(X[m + q2 + 1], X[m + q2], 8 * r2);
+        else
+            Z = X[m + q2];
+        const uint64_t mz = m < 2 ? mZ.lo : mZ.hi;
+        o[m] = bfi((uint32_t)(mz >> ((m & 1) * 32)), Z, X[m]);
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+__device__ __forceinline__ void st_nt(uint8_t* dst, uint4 v)
+{
+    const u32x4 u = { v.x, v.y, v.z, v.w };
+    __builtin_nontemporal_store(u, (u32x4*)dst);
+}
+
+// byte-bounded store of a piece (partial tiles): bytes [0, n) of v
+__device__ __forceinline__ void st_bytes(uint8_t* dst, uint4 v, uint32_t n)
+{
+    const uint32_t w[4] = { v.x, v.y, v.z, v.w };
+    for (uint32_t k = 0; k < n && k < 16; ++k)
+        dst[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+}
+
+// partial-tile staging (nbytes < one tile): plain loads into the LDS buffer
+__device__ __forceinline__ void stage_bytes(uint8_t* dst, const uint8_t* __restrict__ src, uint32_t nbytes, uint32_t tid)
+{
+    for (uint32_t i = tid; i < nbytes; i += NTHR)
+        dst[i] = src[i];
+}
+
+// Decode phase 2 (wave 0, lane = block): the reference correction for blocks with r' != 0.
+// fix(pos, e) patches codeword byte pos of the lane's row (LDS) and, with write-back, in HBM.
+template <int T2>
+__device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, uint32_t par, uint32_t lane, bool valid,
+    uint8_t* __restrict__ raw_g, uint64_t blk, bool wb)
+{
+    using L = RsWgLayout<T2>;
+    const uint64_t rem = *(const uint64_t*)(lds + par + 8u * lane);
+    const bool err = valid && rem != 0;
+    if (__builtin_amdgcn_ballot_w64(err)) {
+        const Gf gf { lds + L::OFF_GF };
+        uint32_t S[T2];
+        bool geo = false;
+        uint32_t gpos = 0, ge = 0;
+        const uint32_t row = buf + PAD + 255u * lane;
+        if (err) {
+            // syndromes as a linear map of r' (nibble tables)
+            uint32_t s[2] = { 0, 0 };
+            uint2 e[2 * T2];
+            const uint8_t* sy = lds + L::OFF_SYN;
+            const uint32_t r0 = (uint32_t)rem, r1 = (uint32_t)(rem >> 32);
+#pragma unroll
+            for (int q = 0; q < T2; ++q) {
+                const int P = 8 - T2 + q;
+                const uint32_t x = P < 4 ? r0 : r1;
+                e[2 * q] = ld8(sy + (2 * q) * 128 + sel78(x << 3, P & 3));
+                e[2 * q + 1] = ld8(sy + (2 * q + 1) * 128 + sel78(x >> 1, P & 3));
+            }
+            xor_entries<2 * T2>(s, e);
+#pragma unroll
+            for (int i = 0; i < T2; ++i)
+                S[i] = (s[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+            geo = rs_geometric<T2>(S, gf, gpos, ge);
+        }
+        auto fix = [&](uint32_t pos, uint32_t e) {
+            if (e == 0)
+                return;
+            const uint8_t fixed = (uint8_t)(lds[row + pos] ^ e);
+            lds[row + pos] = fixed;
+            if (wb)
+                raw_g[blk * 255u + pos] = fixed;
+        };
+        if (__builtin_amdgcn_ballot_w64(err && !geo)) {
+            if (err) {
+                if (geo)
+                    fix(gpos, ge);
+                else
+                    rs_correct_general<T2>(S, gf, fix);
+            }
+        } else if (err && geo) {
+            fix(gpos, ge);
+        }
+    }
+    return err ? 1u : 0u;
+}
+
+// ------------------------------------------------------------------------------------
+// Kernels: persistent workgroups walk 64-block tiles t = blockIdx.x, += gridDim.x.
+// ------------------------------------------------------------------------------------
+template <int T2>
+__global__ __launch_bounds__(256, 3) void rs_wg_encode_kernel(const uint8_t* __restrict__ data,
+    uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables)
+{
+    using L = RsWgLayout<T2>;
+    using D = Lds<T2>;
+    constexpr int K = L::K;
+    constexpr int IN_PIECES = TB * K / 16;   // 996 for 2t = 6
+    constexpr int OUT_PIECES = TB * 255 / 16; // 1020
+    __shared__ __attribute__((aligned(16))) uint8_t lds[D::BYTES];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
+    for (uint32_t p = tid; p < (uint32_t)L::TABLE_BYTES / 16; p += NTHR)
+        *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
+    if (tid < 128)
+        *(uint64_t*)(lds + D::OFF_PAR + 8 * tid) = 0;
+    const uint64_t nfull = nblocks / TB, ntiles = (nblocks + TB - 1) / TB;
+    uint64_t t = blockIdx.x;
+    uint32_t cur = 0;
+    if (t < nfull)
+        dma_tile<IN_PIECES>(lds + D::OFF_BUF + PAD, data + t * (TB * K), tid);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (; t < nfull; t += gridDim.x, cur ^= 1u) {
+        barrier_lds(); // A: tile t in LDS (every wave's pieces), last tile's emission reads done
+        const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + cur * 512u;
+        const uint64_t nx = t + gridDim.x;
+        if (nx < nfull)
+            dma_tile<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, data + nx * (TB * K), tid);
+        if (wave == 0)
+            *(uint64_t*)(lds + D::OFF_PAR + (cur ^ 1u) * 512u + 8u * lane) = 0;
+        phase_remainder<T2, K>(lds, buf, par, wave, lane);
+        barrier_lds(); // B: parity slots complete
+        uint8_t* dst = raw + t * (TB * 255);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t p = tid + 256u * k;
+            if (k < 3 || p < (uint32_t)OUT_PIECES)
+                st_nt(dst + 16u * p, enc_piece<T2>(lds, buf, par, p));
+        }
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); // next tile's DMA landed; stores may fly
+    }
+    if (t == nfull && nfull < ntiles) {
+        // the one partial tile (nblocks % 64 blocks)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier_lds();
+        const uint32_t nb = (uint32_t)(nblocks - t * TB);
+        const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + cur * 512u;
+        stage_bytes(lds + buf + PAD, data + t * (TB * K), nb * K, tid);
+        barrier_lds();
+        phase_remainder<T2, K>(lds, buf, par, wave, lane);
+        barrier_lds();
+        uint8_t* dst = raw + t * (TB * 255);
+        const uint32_t nout = nb * 255u;
+        for (uint32_t p = tid; 16u * p < nout; p += NTHR) {
+            const uint4 v = enc_piece<T2>(lds, buf, par, p);
+            if (16u * p + 16u <= nout)
+                *(uint4*)(dst + 16u * p) = v;
+            else
+                st_bytes(dst + 16u * p, v, nout - 16u * p);
+        }
+    }
+}
+
+template <int T2>
+__global__ __launch_bounds__(256, 3) void rs_wg_decode_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
+    uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables, int write_back)
+{
+    using L = RsWgLayout<T2>;
+    using D = Lds<T2>;
+    constexpr int K = L::K;
+    constexpr int IN_PIECES = TB * 255 / 16; // 1020
+    constexpr int OUT_PIECES = TB * K / 16;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[D::BYTES];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
+    const bool wb = write_back != 0, want = data != nullptr;
+    for (uint32_t p = tid; p < (uint32_t)L::TABLE_BYTES / 16; p += NTHR)
+        *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
+    if (tid < 128)
+        *(uint64_t*)(lds + D::OFF_PAR + 8 * tid) = 0;
+    const uint64_t nfull = nblocks / TB, ntiles = (nblocks + TB - 1) / TB;
+    uint64_t t = blockIdx.x;
+    uint32_t cur = 0;
+    if (t < nfull)
+        dma_tile<IN_PIECES>(lds + D::OFF_BUF + PAD, raw + t * (TB * 255), tid);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (; t < nfull; t += gridDim.x, cur ^= 1u) {
+        barrier_lds(); // A
+        const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + cur * 512u;
+        const uint64_t nx = t + gridDim.x;
+        if (nx < nfull)
+            dma_tile<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, raw + nx * (TB * 255), tid);
+        if (wave == 0)
+            *(uint64_t*)(lds + D::OFF_PAR + (cur ^ 1u) * 512u + 8u * lane) = 0;
+        phase_remainder<T2, 255>(lds, buf, par, wave, lane);
+        barrier_lds(); // B: remainders complete
+        if (wave == 0) {
+            const uint32_t st = phase_correct<T2>(lds, buf, par, lane, true, raw, t * TB + lane, wb);
+            if (status)
+                status[t * TB + lane] = (uint8_t)st;
+        }
+        barrier_lds(); // C: corrections patched into the LDS rows
+        if (want) {
+            uint8_t* dst = data + t * (TB * K);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t p = tid + 256u * k;
+                if (k < 3 || p < (uint32_t)OUT_PIECES)
+                    st_nt(dst + 16u * p, dec_piece<T2>(lds, buf, p));
+            }
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    if (t == nfull && nfull < ntiles) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier_lds();
+        const uint32_t nb = (uint32_t)(nblocks - t * TB);
+        const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + cur * 512u;
+        stage_bytes(lds + buf + PAD, raw + t * (TB * 255), nb * 255u, tid);
+        barrier_lds();
+        phase_remainder<T2, 255>(lds, buf, par, wave, lane);
+        barrier_lds();
+        if (wave == 0) {
+            const bool valid = lane < nb;
+            const uint32_t st = phase_correct<T2>(lds, buf, par, lane, valid, raw, t * TB + lane, wb);
+            if (status && valid)
+                status[t * TB + lane] = (uint8_t)st;
+        }
+        barrier_lds();
+        if (want) {
+            uint8_t* dst = data + t * (TB * K);
+            const uint32_t nout = nb * (uint32_t)K;
+            for (uint32_t p = tid; 16u * p < nout; p += NTHR) {
+                const uint4 v = dec_piece<T2>(lds, buf, p);
+                if (16u * p + 16u <= nout)
+                    *(uint4*)(dst + 16u * p) = v;
+                else
+                    st_bytes(dst + 16u * p, v, nout - 16u * p);
+            }
+        }
+    }
+}
+
+} // namespace wg
+} // namespace ppfs

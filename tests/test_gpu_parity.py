@@ -109,6 +109,70 @@ def test_rs_decode_no_writeback_and_status_only(oracle):
     assert np.array_equal(host(raw_d), bad)
 
 
+def inject_rs_fast(rng, cw, n, t, nblocks):
+    """Vectorised inject_rs for large batches: block b gets b % (t + 4) distinct error bytes."""
+    bad = cw.copy().reshape(nblocks, n)
+    ne = np.arange(nblocks) % (t + 4)
+    start = rng.integers(0, n, nblocks)
+    for j in range(t + 3):
+        rows = np.nonzero(ne > j)[0]
+        pos = (start[rows] + 37 * j) % n  # 37 is a unit mod 255: distinct positions per block
+        bad[rows, pos] ^= rng.integers(1, 256, rows.size, dtype=np.uint8)
+    return bad.reshape(-1)
+
+
+@pytest.mark.parametrize("bs,t", [(512, 3), (256, 4), (255, 1), (1024, 5)], ids=lambda x: str(x))
+def test_rs_many_tiles_per_workgroup(oracle, bs, t):
+    """Batches past one resident grid (3 workgroups/CU x 256 CUs x 64 blocks): every workgroup walks
+    several tiles, so the double-buffered prefetch of the next tile and the ragged last tile run."""
+    n, k, _ = oracle.rs_sizes(bs, t)
+    nb = 3 * 768 * 64 + 37
+    eng = EccEngine(ECC_REED_SOLOMON, bs, t)
+    rng = rng_for("rsbig", bs, t)
+    data = rng.integers(0, 256, nb * k, dtype=np.uint8)
+    raw_d = torch.zeros(nb * n, dtype=torch.uint8, device="cuda")
+    eng.encode(dev(data), raw_d, nblocks=nb)
+    cw = oracle.rs_encode(bs, t, data)
+    assert np.array_equal(host(raw_d), cw)
+    bad = inject_rs_fast(rng, cw, n, t, nb)
+    o_data, o_st, o_fixed, _, _ = oracle.rs_decode(bs, t, bad)
+    raw_d = dev(bad)
+    data_d = torch.zeros(nb * k, dtype=torch.uint8, device="cuda")
+    st_d = torch.full((nb,), 77, dtype=torch.uint8, device="cuda")
+    eng.decode(raw_d, data_d, st_d, write_back=True, nblocks=nb)
+    assert np.array_equal(host(st_d), o_st)
+    assert np.array_equal(host(data_d), o_data)
+    assert np.array_equal(host(raw_d), o_fixed)
+
+
+def test_rs_full_batch_roundtrip_properties():
+    """BASELINE configs[1]/[2] at full size (2^20 RS(255,249) blocks): encode, one byte error per
+    block, decode with write-back.  Size-independent properties: every payload restored, every
+    status 'corrected', the write-back restores the exact codewords, and a clean re-decode reports
+    nothing.  (Bit-exactness vs the oracle at this size: test_rs_many_tiles_per_workgroup.)"""
+    bs, t, nb = 512, 3, 1 << 20
+    n, k = 255, 249
+    eng = EccEngine(ECC_REED_SOLOMON, bs, t)
+    g = torch.Generator(device="cuda").manual_seed(7)
+    data = torch.randint(0, 256, (nb * k,), dtype=torch.uint8, device="cuda", generator=g)
+    raw = torch.empty(nb * n, dtype=torch.uint8, device="cuda")
+    eng.encode(data, raw, nblocks=nb)
+    clean = raw.clone()
+    pos = torch.randint(0, n, (nb,), device="cuda", generator=g) + torch.arange(nb, device="cuda") * n
+    val = torch.randint(1, 256, (nb,), dtype=torch.uint8, device="cuda", generator=g)
+    raw[pos] ^= val
+    out = torch.empty(nb * k, dtype=torch.uint8, device="cuda")
+    st = torch.full((nb,), 77, dtype=torch.uint8, device="cuda")
+    eng.decode(raw, out, st, write_back=True, nblocks=nb)
+    torch.cuda.synchronize()
+    assert torch.equal(out, data)
+    assert bool((st == 1).all())
+    assert torch.equal(raw, clean)
+    eng.decode(raw, out, st, write_back=True, nblocks=nb)
+    torch.cuda.synchronize()
+    assert bool((st == 0).all()) and torch.equal(out, data) and torch.equal(raw, clean)
+
+
 def test_rs_generic_spill_matches_oracle(oracle):
     """Shortened code (n = 64): miscorrections past the block are reported in the spill."""
     bs, t, nb = 64, 3, 600
