@@ -36,16 +36,8 @@ namespace wg {
 constexpr int TB = 64;      // blocks per tile
 constexpr int NTHR = 256;   // threads per workgroup
 constexpr int PAD = 16;     // front pad of a tile buffer (emission reads up to 2t bytes before row 0)
-constexpr int BUF = 16448;  // PAD + 64*255 + slack for over-reads, 16-byte multiple
+constexpr int BUF = 16368;  // PAD + 64*255 + 32: decode emission reads up to 28 B past a piece start
 
-template <int T2> struct Lds {
-    using L = RsWgLayout<T2>;
-    static constexpr int OFF_PAR = L::TABLE_BYTES;        // 2 x 64 x 8 B remainder slots
-    static constexpr int OFF_BUF = OFF_PAR + 1024 + 64;  // + slack: par[b+1] over-read
-    static constexpr int BYTES = OFF_BUF + 2 * BUF;
-    static_assert(OFF_BUF % 16 == 0, "aligned buffers");
-    static_assert(3 * BYTES <= 163840, "three workgroups per CU");
-};
 
 __device__ __forceinline__ void barrier_lds()
 {
@@ -207,11 +199,17 @@ template <int T2, int S> __device__ __forceinline__ void seg_map(uint32_t (&s)[2
     xor_entries<2 * T2>(s, e);
 }
 
-// Phase 1 for this wave's segment: XOR its remainder into the block's slot
+// Block (row of the tile) owned by a lane in phases 1 and 2: lanes 0-31 take the even rows, 32-63
+// the odd ones.  Rows sit 255 (or 249) bytes apart, so consecutive rows start in nearly the same
+// LDS bank; a 32-lane half reading every other row hits each bank at most twice (4-way -> 2-way
+// for 255-byte rows).
+__device__ __forceinline__ uint32_t lane_row(uint32_t lane) { return ((lane & 31u) << 1) | (lane >> 5); }
+
+// Phase 1 for this wave's segment of block `blk`: XOR its remainder into the block's slot
 template <int T2, int LEN>
-__device__ __forceinline__ void phase_remainder(uint8_t* lds, uint32_t buf, uint32_t par, uint32_t wave, uint32_t lane)
+__device__ __forceinline__ void phase_remainder(uint8_t* lds, uint32_t buf, uint32_t par, uint32_t wave, uint32_t blk)
 {
-    const uint32_t row = buf + PAD + (uint32_t)LEN * lane;
+    const uint32_t row = buf + PAD + (uint32_t)LEN * blk;
     uint32_t s[2];
     switch (wave) {
     case 0:
@@ -231,7 +229,7 @@ __device__ __forceinline__ void phase_remainder(uint8_t* lds, uint32_t buf, uint
         break;
     }
     const uint64_t v = ((uint64_t)s[1] << 32) | s[0];
-    __hip_atomic_fetch_xor((unsigned long long*)(lds + par + 8u * lane), (unsigned long long)v, __ATOMIC_RELAXED,
+    __hip_atomic_fetch_xor((unsigned long long*)(lds + par + 8u * blk), (unsigned long long)v, __ATOMIC_RELAXED,
         __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
@@ -339,10 +337,14 @@ template <int T2> __device__ __forceinline__ uint4 dec_piece(const uint8_t* lds,
     return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
-__device__ __forceinline__ void st_nt(uint8_t* dst, uint4 v)
+template <int NT = 1> __device__ __forceinline__ void st_nt(uint8_t* dst, uint4 v)
 {
-    const u32x4 u = { v.x, v.y, v.z, v.w };
-    __builtin_nontemporal_store(u, (u32x4*)dst);
+    if constexpr (NT) {
+        const u32x4 u = { v.x, v.y, v.z, v.w };
+        __builtin_nontemporal_store(u, (u32x4*)dst);
+    } else {
+        *(uint4*)dst = v;
+    }
 }
 
 // byte-bounded store of a piece (partial tiles): bytes [0, n) of v
@@ -363,18 +365,18 @@ __device__ __forceinline__ void stage_bytes(uint8_t* dst, const uint8_t* __restr
 // Decode phase 2 (wave 0, lane = block): the reference correction for blocks with r' != 0.
 // fix(pos, e) patches codeword byte pos of the lane's row (LDS) and, with write-back, in HBM.
 template <int T2>
-__device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, uint32_t par, uint32_t lane, bool valid,
+__device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, uint32_t par, uint32_t r, bool valid,
     uint8_t* __restrict__ raw_g, uint64_t blk, bool wb)
 {
     using L = RsWgLayout<T2>;
-    const uint64_t rem = *(const uint64_t*)(lds + par + 8u * lane);
+    const uint64_t rem = *(const uint64_t*)(lds + par + 8u * r);
     const bool err = valid && rem != 0;
     if (__builtin_amdgcn_ballot_w64(err)) {
         const Gf gf { lds + L::OFF_GF };
         uint32_t S[T2];
         bool geo = false;
         uint32_t gpos = 0, ge = 0;
-        const uint32_t row = buf + PAD + 255u * lane;
+        const uint32_t row = buf + PAD + 255u * r;
         if (err) {
             // syndromes as a linear map of r' (nibble tables)
             uint32_t s[2] = { 0, 0 };
@@ -418,56 +420,103 @@ __device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, ui
 
 // ------------------------------------------------------------------------------------
 // Kernels: persistent workgroups walk 64-block tiles t = blockIdx.x, += gridDim.x.
+// NBUF = LDS tile buffers: 2 = the next tile's DMA is issued at the top of an iteration (a whole
+// tile of compute ahead); 1 = it is issued after this tile's emission reads (cross-workgroup
+// overlap hides it).  WPC = resident workgroups per CU (the launch bound; the grid is WPC x CUs).
 // ------------------------------------------------------------------------------------
-template <int T2>
-__global__ __launch_bounds__(256, 3) void rs_wg_encode_kernel(const uint8_t* __restrict__ data,
+template <int T2, bool DEC, int NBUF> struct Lds {
+    using L = RsWgLayout<T2>;
+    static constexpr int TBL = DEC ? L::TABLE_BYTES : L::OFF_SYN; // encode needs SL + MAP only
+    static constexpr int OFF_PAR = TBL;                              // 2 x 64 x 8 B remainder slots
+    static constexpr int OFF_BUF = OFF_PAR + 1024 + 64;             // + slack: par[b+1] over-read
+    static constexpr int BYTES = OFF_BUF + NBUF * BUF;
+    static_assert(OFF_BUF % 16 == 0 && TBL % 16 == 0, "aligned buffers");
+};
+
+template <int T2, bool DEC, int NBUF> constexpr int lds_bytes() { return Lds<T2, DEC, NBUF>::BYTES; }
+
+// LDS declared per workgroup: at least the layout, and more than 1/(WPC+1) of the CU's 160 KiB, so
+// exactly WPC workgroups are resident per CU -- a WPC x CUs persistent grid is then balanced
+// (a smaller footprint would let some CUs take WPC+1 workgroups and others fewer).
+template <int BYTES, int WPC> constexpr int lds_alloc()
+{
+    constexpr int floor_plus = (163840 / (WPC + 1) + 512) & ~511;
+    return BYTES > floor_plus ? BYTES : floor_plus;
+}
+
+// MODE (ablation builds only; the engine uses 3): bit 0 = remainder phase, bit 1 = codeword
+// emission (else a plain 16-byte copy out of the LDS tile, same bytes moved)
+template <int T2, int NBUF = 2, int WPC = 4, int MODE = 3, int NTST = 1>
+__global__ __launch_bounds__(256, WPC) void rs_wg_encode_kernel(const uint8_t* __restrict__ data,
     uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables)
 {
     using L = RsWgLayout<T2>;
-    using D = Lds<T2>;
+    using D = Lds<T2, false, NBUF>;
+    constexpr int LDS_ALLOC = lds_alloc<D::BYTES, WPC>();
+    static_assert(WPC * LDS_ALLOC <= 163840, "LDS for WPC workgroups per CU");
     constexpr int K = L::K;
     constexpr int IN_PIECES = TB * K / 16;   // 996 for 2t = 6
     constexpr int OUT_PIECES = TB * 255 / 16; // 1020
-    __shared__ __attribute__((aligned(16))) uint8_t lds[D::BYTES];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_ALLOC];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
-    for (uint32_t p = tid; p < (uint32_t)L::TABLE_BYTES / 16; p += NTHR)
+    const uint32_t row = lane_row(lane);
+    for (uint32_t p = tid; p < (uint32_t)D::TBL / 16; p += NTHR)
         *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
     if (tid < 128)
         *(uint64_t*)(lds + D::OFF_PAR + 8 * tid) = 0;
     const uint64_t nfull = nblocks / TB, ntiles = (nblocks + TB - 1) / TB;
     uint64_t t = blockIdx.x;
-    uint32_t cur = 0;
+    uint32_t cur = 0, pc = 0; // tile buffer, parity-slot set
     if (t < nfull)
         dma_tile<IN_PIECES>(lds + D::OFF_BUF + PAD, data + t * (TB * K), tid);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (; t < nfull; t += gridDim.x, cur ^= 1u) {
+    for (; t < nfull; t += gridDim.x) {
         barrier_lds(); // A: tile t in LDS (every wave's pieces), last tile's emission reads done
-        const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + cur * 512u;
+        const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + pc * 512u;
         const uint64_t nx = t + gridDim.x;
-        if (nx < nfull)
+        if (NBUF == 2 && nx < nfull)
             dma_tile<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, data + nx * (TB * K), tid);
         if (wave == 0)
-            *(uint64_t*)(lds + D::OFF_PAR + (cur ^ 1u) * 512u + 8u * lane) = 0;
-        phase_remainder<T2, K>(lds, buf, par, wave, lane);
+            *(uint64_t*)(lds + D::OFF_PAR + (pc ^ 1u) * 512u + 8u * lane) = 0;
+        if constexpr (MODE & 1)
+            phase_remainder<T2, K>(lds, buf, par, wave, row);
         barrier_lds(); // B: parity slots complete
         uint8_t* dst = raw + t * (TB * 255);
+        uint4 o[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t p = tid + 256u * k;
-            if (k < 3 || p < (uint32_t)OUT_PIECES)
-                st_nt(dst + 16u * p, enc_piece<T2>(lds, buf, par, p));
+            if constexpr (MODE & 2)
+                o[k] = enc_piece<T2>(lds, buf, par, p);
+            else
+                o[k] = *(const uint4*)(lds + buf + PAD + 16u * (p < 996u ? p : p - 64u));
+            if (NBUF == 2 && (k < 3 || p < (uint32_t)OUT_PIECES))
+                st_nt<NTST>(dst + 16u * p, o[k]); // store as soon as the piece is assembled
+        }
+        if (NBUF == 1) {
+            barrier_lds(); // every wave's emission reads done: the buffer is free
+            if (nx < nfull)
+                dma_tile<IN_PIECES>(lds + D::OFF_BUF + PAD, data + nx * (TB * K), tid);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t p = tid + 256u * k;
+                if (k < 3 || p < (uint32_t)OUT_PIECES)
+                    st_nt<NTST>(dst + 16u * p, o[k]);
+            }
         }
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); // next tile's DMA landed; stores may fly
+        cur ^= (NBUF == 2) ? 1u : 0u;
+        pc ^= 1u;
     }
     if (t == nfull && nfull < ntiles) {
         // the one partial tile (nblocks % 64 blocks)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         barrier_lds();
         const uint32_t nb = (uint32_t)(nblocks - t * TB);
-        const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + cur * 512u;
+        const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + pc * 512u;
         stage_bytes(lds + buf + PAD, data + t * (TB * K), nb * K, tid);
         barrier_lds();
-        phase_remainder<T2, K>(lds, buf, par, wave, lane);
+        phase_remainder<T2, K>(lds, buf, par, wave, row);
         barrier_lds();
         uint8_t* dst = raw + t * (TB * 255);
         const uint32_t nout = nb * 255u;
@@ -481,71 +530,98 @@ __global__ __launch_bounds__(256, 3) void rs_wg_encode_kernel(const uint8_t* __r
     }
 }
 
-template <int T2>
-__global__ __launch_bounds__(256, 3) void rs_wg_decode_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
+// MODE (ablation builds only; the engine uses 7): bit 0 = remainder phase, bit 1 = payload
+// emission (else a plain 16-byte copy), bit 2 = correction phase
+template <int T2, int NBUF = 2, int WPC = 3, int MODE = 7, int NTST = 1>
+__global__ __launch_bounds__(256, WPC) void rs_wg_decode_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
     uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables, int write_back)
 {
     using L = RsWgLayout<T2>;
-    using D = Lds<T2>;
+    using D = Lds<T2, true, NBUF>;
+    constexpr int LDS_ALLOC = lds_alloc<D::BYTES, WPC>();
+    static_assert(WPC * LDS_ALLOC <= 163840, "LDS for WPC workgroups per CU");
     constexpr int K = L::K;
     constexpr int IN_PIECES = TB * 255 / 16; // 1020
     constexpr int OUT_PIECES = TB * K / 16;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[D::BYTES];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_ALLOC];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
+    const uint32_t row = lane_row(lane);
     const bool wb = write_back != 0, want = data != nullptr;
-    for (uint32_t p = tid; p < (uint32_t)L::TABLE_BYTES / 16; p += NTHR)
+    for (uint32_t p = tid; p < (uint32_t)D::TBL / 16; p += NTHR)
         *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
     if (tid < 128)
         *(uint64_t*)(lds + D::OFF_PAR + 8 * tid) = 0;
     const uint64_t nfull = nblocks / TB, ntiles = (nblocks + TB - 1) / TB;
     uint64_t t = blockIdx.x;
-    uint32_t cur = 0;
+    uint32_t cur = 0, pc = 0;
     if (t < nfull)
         dma_tile<IN_PIECES>(lds + D::OFF_BUF + PAD, raw + t * (TB * 255), tid);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    for (; t < nfull; t += gridDim.x, cur ^= 1u) {
+    for (; t < nfull; t += gridDim.x) {
         barrier_lds(); // A
-        const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + cur * 512u;
+        const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + pc * 512u;
         const uint64_t nx = t + gridDim.x;
-        if (nx < nfull)
+        if (NBUF == 2 && nx < nfull)
             dma_tile<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, raw + nx * (TB * 255), tid);
         if (wave == 0)
-            *(uint64_t*)(lds + D::OFF_PAR + (cur ^ 1u) * 512u + 8u * lane) = 0;
-        phase_remainder<T2, 255>(lds, buf, par, wave, lane);
+            *(uint64_t*)(lds + D::OFF_PAR + (pc ^ 1u) * 512u + 8u * lane) = 0;
+        if constexpr (MODE & 1)
+            phase_remainder<T2, 255>(lds, buf, par, wave, row);
         barrier_lds(); // B: remainders complete
-        if (wave == 0) {
-            const uint32_t st = phase_correct<T2>(lds, buf, par, lane, true, raw, t * TB + lane, wb);
+        if ((MODE & 4) && wave == 0) {
+            const uint32_t st = phase_correct<T2>(lds, buf, par, row, true, raw, t * TB + row, wb);
             if (status)
-                status[t * TB + lane] = (uint8_t)st;
+                status[t * TB + row] = (uint8_t)st;
         }
         barrier_lds(); // C: corrections patched into the LDS rows
+        uint4 o[4];
+        uint8_t* dst = want ? data + t * (TB * K) : nullptr;
         if (want) {
-            uint8_t* dst = data + t * (TB * K);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const uint32_t p = tid + 256u * k;
-                if (k < 3 || p < (uint32_t)OUT_PIECES)
-                    st_nt(dst + 16u * p, dec_piece<T2>(lds, buf, p));
+                if constexpr (MODE & 2)
+                    o[k] = dec_piece<T2>(lds, buf, p);
+                else
+                    o[k] = *(const uint4*)(lds + buf + PAD + 16u * p);
+                if (NBUF == 2 && (k < 3 || p < (uint32_t)OUT_PIECES))
+                    st_nt<NTST>(dst + 16u * p, o[k]);
             }
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        if (NBUF == 1) {
+            barrier_lds();
+            if (nx < nfull)
+                dma_tile<IN_PIECES>(lds + D::OFF_BUF + PAD, raw + nx * (TB * 255), tid);
+            if (want) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t p = tid + 256u * k;
+                    if (k < 3 || p < (uint32_t)OUT_PIECES)
+                        st_nt<NTST>(dst + 16u * p, o[k]);
+                }
+            }
+        }
+        if (want)
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        cur ^= (NBUF == 2) ? 1u : 0u;
+        pc ^= 1u;
     }
     if (t == nfull && nfull < ntiles) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         barrier_lds();
         const uint32_t nb = (uint32_t)(nblocks - t * TB);
-        const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + cur * 512u;
+        const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + pc * 512u;
         stage_bytes(lds + buf + PAD, raw + t * (TB * 255), nb * 255u, tid);
         barrier_lds();
-        phase_remainder<T2, 255>(lds, buf, par, wave, lane);
+        phase_remainder<T2, 255>(lds, buf, par, wave, row);
         barrier_lds();
         if (wave == 0) {
-            const bool valid = lane < nb;
-            const uint32_t st = phase_correct<T2>(lds, buf, par, lane, valid, raw, t * TB + lane, wb);
+            const bool valid = row < nb;
+            const uint32_t st = phase_correct<T2>(lds, buf, par, row, valid, raw, t * TB + row, wb);
             if (status && valid)
-                status[t * TB + lane] = (uint8_t)st;
+                status[t * TB + row] = (uint8_t)st;
         }
         barrier_lds();
         if (want) {

@@ -20,13 +20,14 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH_ARGS = "bench.py --steps 50 --warmup 5 --prewarm-s 0.3 --no-cpu-baseline"
 
 
 def short(name):
     # "void ppfs::rs255_encode_kernel<6, 0, 1, 1, 0>(unsigned char const*, ...)" -> rs255_encode_kernel<6, 0, 1, 1, 0>
     n = name.replace("void ", "")
     n = n.split("(")[0]
-    return n.replace("ppfs::", "")
+    return n.replace("ppfs::", "").replace("wg::", "")
 
 
 def counters(path):
@@ -55,14 +56,13 @@ def main():
             for c, v in cs.items():
                 merged[k][c] = statistics.median(v)
     lines = [f"# rocprofv3 summary: {tag}", "",
-             "Command: `tools/profile_box.sh` (bench.py --steps 10 --warmup 3 --no-cpu-baseline, 2^20 blocks)", "",
+             "Command: `tools/profile_box.sh` (" + BENCH_ARGS + ", 2^20 blocks)", "",
              "| kernel | calls | avg us | min us | HBM read MB (2xFETCH) | HBM write MB | traffic MB/launch |",
              "|---|---|---|---|---|---|---|"]
     latest = {}
     for r in rows:
         k = short(r["Name"])
-        if not k.startswith("rs255") and not k.startswith("crc") and not k.startswith("ham") \
-                and not k.startswith("parity") and not k.startswith("rs_generic"):
+        if not k.startswith(("rs255", "rs_wg", "crc", "ham", "parity", "rs_generic")):
             continue
         c = merged.get(k, {})
         fetch = 2 * c.get("FETCH_SIZE", float("nan")) * 1024
