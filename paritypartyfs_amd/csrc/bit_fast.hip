@@ -1,0 +1,637 @@
+// bit_fast.hip -- Hamming SECDED and single-parity kernels for 1, 2 and 4 KiB blocks (gfx950).
+//
+// The BASELINE cfg4 shape (block_size 4096, 2^20 blocks: 4 GiB in, 4 GiB out per launch) is pure
+// streaming; these kernels keep every byte's work to a few VALU ops so they run at the HBM rate.
+// One wave per block, NP = block_size / 1024 pieces of 16 B per lane, coalesced: lane l of a wave
+// holds raw bytes [16 (64 k + l), +16) for k < NP, i.e. big-endian raw words w = 256 k + 4 l + u.
+// Waves are persistent (grid-stride over blocks) and prefetch the next block into VGPRs while the
+// current one is computed.  Smaller blocks use bit_kernels.hip.
+//
+// Reference semantics (lib/blockdevice/src/hamming_block_device.cpp, MSB-first bit numbering of
+// lib/common/include/ppfs/common/bit_helpers.hpp:8-52):
+//   - payload bit i sits at raw position r(i) = the i-th integer >= 3 that is not a power of two;
+//     for r in (2^j, 2^(j+1)) that is r = i + j + 2 (HammingDataBitsIterator :180-198), so raw
+//     word w >= 1 is one funnel of the payload bit stream at offset 32 w - j - 2, j = log2(32 w);
+//   - parity bit 2^j = bit j of the XOR of the positions of the set payload bits; bit 0 makes the
+//     total parity even (_encodeData :76-109); raw bits after the last payload bit L keep their
+//     old contents (the reference only writes payload and parity positions);
+//   - decode (_readAndFixBlock :21-65): over the used bits [0, L] (plus parity positions past L,
+//     none for block_size >= 1024): odd parity -> flip bit (XOR of set positions), write back
+//     that byte, status 1; even parity and a non-zero XOR -> BlockDevice_CorrectionError (5).
+// Parity (parity_block_device.cpp:31-97): even parity over the raw block, the fix bit is the LSB
+// of the last byte, whose other bits keep their old contents.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gf_common.hpp"
+
+namespace ppfs {
+namespace bf {
+
+constexpr int WAVES = 4;
+
+__device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+
+// XOR over the 64 lanes of a wave, returned wave-uniform: a DPP butterfly inside each row of 16
+// lanes, then row broadcasts 15 and 31 (lane 63 ends with the total).
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v)
+{
+    v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);        // quad_perm [1,0,3,2]
+    v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);        // quad_perm [2,3,0,1]
+    v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);       // row_half_mirror
+    v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);       // row_mirror
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false); // row_bcast:15
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false); // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// 32 bits of a big-endian bit stream in LDS starting at absolute bit position `bit` (the stream's
+// bit 0 is the MSB of byte 0 of `base`); reads two aligned dwords.
+__device__ __forceinline__ uint32_t be_fetch32(const uint8_t* base, uint32_t bit)
+{
+    const uint32_t* w = (const uint32_t*)(base + ((bit >> 5) << 2));
+    const uint64_t v = ((uint64_t)bswap(w[0]) << 32) | bswap(w[1]);
+    return (uint32_t)(v >> (32 - (bit & 31u)));
+}
+
+// top n bits (MSB side) of a word, n in [0, 32]
+__device__ __forceinline__ uint32_t top_bits(uint32_t n) { return n >= 32 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> n); }
+
+// syndrome contribution of the positions q (MSB-first) set in the XOR of a lane's words
+__device__ __forceinline__ uint32_t qbits(uint32_t x)
+{
+    return (__builtin_popcount(x & 0x55555555u) & 1u) | ((__builtin_popcount(x & 0x33333333u) & 1u) << 1)
+        | ((__builtin_popcount(x & 0x0F0F0F0Fu) & 1u) << 2) | ((__builtin_popcount(x & 0x00FF00FFu) & 1u) << 3)
+        | ((__builtin_popcount(x & 0x0000FFFFu) & 1u) << 4);
+}
+
+struct HamFast {
+    uint32_t bs, ds, L;
+    uint64_t data_bytes; // nblocks * ds: the payload buffer's end (no vector load may pass it)
+};
+
+// ------------------------------------------------------------------------------------
+// Hamming encode
+// ------------------------------------------------------------------------------------
+// The payload row (ds bytes at any alignment) is staged as the 16-byte pieces of the aligned
+// superset [a0, a0 + 16 npc) into the wave's LDS buffer; pieces past the buffer end (last block
+// only) are loaded byte by byte.  NPL = pieces per lane in the prefetch registers.
+template <int NP> struct HamEncStage {
+    static constexpr int NPL = NP + 1; // superset <= 64 NP + 1 pieces
+    uint4 v[NPL];
+};
+
+template <int NP>
+__device__ __forceinline__ void ham_stage_load(HamEncStage<NP>& s, const uint8_t* __restrict__ data, uint64_t blk,
+    const HamFast& a, uint32_t lane)
+{
+    const uint64_t start = blk * a.ds, a0 = start & ~15ull;
+    const uint32_t npc = (uint32_t)((start + a.ds - a0 + 15) >> 4);
+#pragma unroll
+    for (int k = 0; k < HamEncStage<NP>::NPL; ++k) {
+        const uint32_t p = 64u * k + lane;
+        const uint64_t g = a0 + 16ull * p;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (p < npc) {
+            if (g + 16 <= a.data_bytes) {
+                v = *(const uint4*)(data + g);
+            } else {
+                uint32_t w[4] = { 0, 0, 0, 0 };
+                for (uint32_t b = 0; b < 16 && g + b < a.data_bytes; ++b)
+                    w[b >> 2] |= (uint32_t)data[g + b] << (8 * (b & 3));
+                v = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+        s.v[k] = v;
+    }
+}
+
+template <int NP>
+__device__ __forceinline__ void ham_stage_write(uint8_t* buf, const HamEncStage<NP>& s, uint32_t lane)
+{
+#pragma unroll
+    for (int k = 0; k < HamEncStage<NP>::NPL; ++k)
+        *(uint4*)(buf + 16u * (64u * k + lane)) = s.v[k];
+}
+
+template <int NP>
+__global__ __launch_bounds__(256) void ham_fast_encode_kernel(const uint8_t* __restrict__ data, uint8_t* __restrict__ raw,
+    const uint8_t* __restrict__ skip, uint64_t nblocks, HamFast a)
+{
+    constexpr int BUF = (NP + 1) * 1024 + 32; // NP + 1 staged pieces per lane + read slack
+    __shared__ __attribute__((aligned(16))) uint8_t lds[WAVES * BUF];
+    const uint32_t lane = lane_id(), wave = wave_id();
+    uint8_t* buf = lds + wave * BUF;
+    const uint32_t nwords = a.bs / 4, lastw = nwords - 1;
+    const uint64_t stride = (uint64_t)gridDim.x * WAVES;
+    uint64_t blk = (uint64_t)blockIdx.x * WAVES + wave;
+    HamEncStage<NP> st;
+    if (blk < nblocks)
+        ham_stage_load<NP>(st, data, blk, a, lane);
+    for (; blk < nblocks; blk += stride) {
+        ham_stage_write<NP>(buf, st, lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const uint64_t nx = blk + stride;
+        if (nx < nblocks)
+            ham_stage_load<NP>(st, data, nx, a, lane); // lands while this block is computed
+        const uint32_t m = (uint32_t)((blk * a.ds) & 15u); // payload byte 0 sits at LDS byte m
+        uint8_t* rb = raw + blk * a.bs;
+        const bool skipped = skip && skip[blk] == 5;
+        // old raw tail word (bits past L keep their contents): the last word of the block
+        uint32_t old_tail = 0;
+        if (lane == 63)
+            old_tail = bswap(*(const uint32_t*)(rb + 4 * lastw));
+        uint32_t X[NP][4];
+        uint32_t ax = 0, aw = 0;
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            const uint32_t w0 = 256u * k + 4u * lane;
+            if (k == 0 && lane == 0) {
+                // words 0-3: positions 0..127 hold parity bits 0,1,2,4,8,16,32,64
+                const uint32_t D = be_fetch32(buf, 8 * m);
+                X[0][0] = (((D >> 31) & 1u) << 28) | (((D >> 28) & 7u) << 24) | (((D >> 21) & 0x7Fu) << 16)
+                    | ((D >> 6) & 0x7FFFu);
+                X[0][1] = be_fetch32(buf, 8 * m + 32 - 5 - 2) & 0x7FFFFFFFu;  // j = 5, parity at 32
+                X[0][2] = be_fetch32(buf, 8 * m + 64 - 6 - 2) & 0x7FFFFFFFu;  // j = 6, parity at 64
+                X[0][3] = be_fetch32(buf, 8 * m + 96 - 6 - 2);
+            } else {
+                const uint32_t j = 36u - (uint32_t)__builtin_clz(w0); // log2(32 w0)
+                const uint32_t o = 8 * m + 32 * w0 - j - 2;           // stream bit of word w0, position 0
+                const uint32_t* src = (const uint32_t*)(buf + ((o >> 5) << 2));
+                const uint32_t s = o & 31u;
+                uint32_t E[5];
+#pragma unroll
+                for (int i = 0; i < 5; ++i)
+                    E[i] = bswap(src[i]);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    X[k][u] = (uint32_t)((((uint64_t)E[u] << 32) | E[u + 1]) >> (32 - s));
+                if ((w0 & (w0 - 1)) == 0)
+                    X[k][0] &= 0x7FFFFFFFu; // position 32 w0 = 2^j is a parity bit
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t w = w0 + u;
+                if (32 * w + 31 > a.L) // bits past the last payload bit are not payload
+                    X[k][u] &= top_bits(a.L >= 32 * w ? a.L - 32 * w + 1 : 0);
+                ax ^= X[k][u];
+                aw ^= (__builtin_popcount(X[k][u]) & 1u) ? w : 0u;
+            }
+        }
+        // syndrome S = XOR of the positions of the set payload bits, and the payload parity
+        const uint32_t red = wave_xor(((aw << 5 | qbits(ax)) << 1) | (__builtin_popcount(ax) & 1u));
+        const uint32_t S = red >> 1;
+        const uint32_t bit0 = (red ^ (uint32_t)__builtin_popcount(S)) & 1u; // total parity even
+        if (!skipped) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                const uint32_t w0 = 256u * k + 4u * lane;
+                if (k == 0 && lane == 0) {
+                    X[0][0] |= (bit0 << 31) | ((S & 1u) << 30) | (((S >> 1) & 1u) << 29) | (((S >> 2) & 1u) << 27)
+                        | (((S >> 3) & 1u) << 23) | (((S >> 4) & 1u) << 15);
+                    X[0][1] |= ((S >> 5) & 1u) << 31;
+                    X[0][2] |= ((S >> 6) & 1u) << 31;
+                } else if ((w0 & (w0 - 1)) == 0 && 32 * w0 < 8 * a.bs) {
+                    const uint32_t j = 36u - (uint32_t)__builtin_clz(w0);
+                    X[k][0] |= ((S >> j) & 1u) << 31;
+                }
+                if (k == NP - 1 && lane == 63) {
+                    const uint32_t keep = ~top_bits(a.L - 32 * lastw + 1);
+                    X[k][3] = (X[k][3] & ~keep) | (old_tail & keep);
+                }
+                *(uint4*)(rb + 16u * (64u * k + lane)) =
+                    make_uint4(bswap(X[k][0]), bswap(X[k][1]), bswap(X[k][2]), bswap(X[k][3]));
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); // LDS reads done before the rewrite
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// bytes [lo, hi) of a 16-byte piece (the partial first / last piece of an unaligned row: the
+// other bytes belong to the neighbouring rows, written by other waves): whole dwords where the
+// range covers them, single bytes at the two ends
+__device__ __forceinline__ void store_piece_part(uint8_t* dst, const uint32_t (&o)[4], uint32_t lo, uint32_t hi)
+{
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint32_t d0 = 4 * u;
+        if (lo <= d0 && d0 + 4 <= hi) {
+            *(uint32_t*)(dst + d0) = o[u];
+        } else {
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (d0 + b >= lo && d0 + b < hi)
+                    dst[d0 + b] = (uint8_t)(o[u] >> (8 * b));
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Hamming decode
+// ------------------------------------------------------------------------------------
+// payload bits [i, i + 32) for 0 <= i < 64, from the corrected raw image in LDS (big-endian
+// stream).  Below raw bit 72 the parity positions 1,2,4,8,16,32,64 interleave with the payload,
+// so payload bits 0..63 are gathered with fixed masks from raw words 0-2; payload bits 64..
+// continue at raw bit 72 with no parity position before raw bit 128.
+__device__ __forceinline__ uint32_t ham_head32(const uint8_t* img, uint32_t i)
+{
+    const uint32_t* w = (const uint32_t*)img;
+    const uint32_t W0 = bswap(w[0]), W1 = bswap(w[1]), W2 = bswap(w[2]);
+    // payload 0 <- raw 3; 1-3 <- 5-7; 4-10 <- 9-15; 11-25 <- 17-31; 26-56 <- 33-63; 57-63 <- 65-71
+    const uint32_t hi = (((W0 >> 28) & 1u) << 31) | (((W0 >> 24) & 7u) << 28) | (((W0 >> 16) & 0x7Fu) << 21)
+        | ((W0 & 0x7FFFu) << 6) | ((W1 >> 25) & 0x3Fu);
+    const uint32_t lo = ((W1 & 0x1FFFFFFu) << 7) | ((W2 >> 24) & 0x7Fu);
+    const uint64_t P = ((uint64_t)hi << 32) | lo;                    // payload bits 0..63
+    const uint32_t head = (uint32_t)((P << i) >> 32);                    // payload bits [i, min(i + 32, 64))
+    const uint32_t tail = i > 32 ? be_fetch32(img, 72) >> (64 - i) : 0u; // payload bits 64.. from raw 72
+    return head | tail;
+}
+
+// payload bits [i, i + 32) for i >= 64: at most one parity position (the next power of two)
+// among their raw positions; bits before it from the raw stream at r(i), after it at r(i) + 1
+__device__ __forceinline__ uint32_t ham_mid32(const uint8_t* img, uint32_t i)
+{
+    uint32_t j = 31u - (uint32_t)__builtin_clz(i + 2);
+    if (i + j + 2 >= (2u << j))
+        j++;
+    const uint32_t r = i + j + 2, n = (2u << j) - r;
+    const uint32_t A = be_fetch32(img, r), B = be_fetch32(img, r + 1);
+    const uint32_t mk = top_bits(n);
+    return (A & mk) | (B & ~mk);
+}
+
+template <int NP>
+__global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
+    uint8_t* __restrict__ status, uint64_t nblocks, int write_back, HamFast a)
+{
+    constexpr int BUF = NP * 1024 + 16; // raw image + zero slack
+    __shared__ __attribute__((aligned(16))) uint8_t lds[WAVES * BUF];
+    const uint32_t lane = lane_id(), wave = wave_id();
+    uint8_t* img = lds + wave * BUF;
+    const uint32_t lastw = a.bs / 4 - 1;
+    const uint64_t stride = (uint64_t)gridDim.x * WAVES;
+    uint64_t blk = (uint64_t)blockIdx.x * WAVES + wave;
+    uint4 R[NP];
+    if (blk < nblocks) {
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            R[k] = *(const uint4*)(raw + blk * a.bs + 16u * (64u * k + lane));
+    }
+    for (; blk < nblocks; blk += stride) {
+        uint32_t X[NP][4];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            X[k][0] = R[k].x;
+            X[k][1] = R[k].y;
+            X[k][2] = R[k].z;
+            X[k][3] = R[k].w;
+        }
+        const uint64_t nx = blk + stride;
+        if (nx < nblocks) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                R[k] = *(const uint4*)(raw + nx * a.bs + 16u * (64u * k + lane));
+        }
+        uint32_t ax = 0, aw = 0;
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t w = 256u * k + 4u * lane + u;
+                uint32_t x = bswap(X[k][u]);
+                if (32 * w + 31 > a.L)
+                    x &= top_bits(a.L >= 32 * w ? a.L - 32 * w + 1 : 0); // used bits only
+                ax ^= x;
+                aw ^= (__builtin_popcount(x) & 1u) ? w : 0u;
+            }
+        }
+        const uint32_t red = wave_xor(((aw << 5 | qbits(ax)) << 1) | (__builtin_popcount(ax) & 1u));
+        const uint32_t S = red >> 1, par = red & 1u;
+        const uint32_t st = par ? 1u : (S ? 5u : 0u);
+        uint8_t* rb = raw + blk * a.bs;
+        if (par) {
+            // flip bit S in the owner lane's register copy; write back that byte
+            const uint32_t ws = S >> 5;
+            if (((ws >> 2) & 63u) == lane) {
+                const uint32_t flip = 0x80u << (8 * ((S >> 3) & 3u)) >> (S & 7u);
+#pragma unroll
+                for (int k = 0; k < NP; ++k)
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (256u * k + 4u * lane + u == ws)
+                            X[k][u] ^= flip;
+                if (write_back)
+                    rb[S >> 3] = (uint8_t)(rb[S >> 3] ^ (0x80u >> (S & 7u)));
+            }
+        }
+        if (status && lane == 0)
+            status[blk] = (uint8_t)st;
+        if (data && st != 5) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                *(uint4*)(img + 16u * (64u * k + lane)) = make_uint4(X[k][0], X[k][1], X[k][2], X[k][3]);
+            if (lane < 4)
+                *(uint32_t*)(img + NP * 1024 + 4 * lane) = 0;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            // payload row [blk ds, +ds) as 16-byte pieces of the global 16-byte grid
+            const uint64_t start = blk * a.ds, a0 = start & ~15ull;
+            const uint32_t m = (uint32_t)(start - a0);
+            const uint32_t npc = (m + a.ds + 15) >> 4;
+            // one rolled loop over this lane's pieces keeps the live state to one piece
+#pragma unroll 1
+            for (int k = 0; k <= NP; ++k) {
+                const uint32_t p = 64u * k + lane;
+                if (p >= npc)
+                    break;
+                const int32_t b0 = (int32_t)(16 * p) - (int32_t)m; // payload byte of piece byte 0
+                uint32_t o[4];
+                if (b0 >= 8) {
+                    // payload bits [i0, i0 + 128) sit at raw bits [r0, ...) with at most one parity
+                    // position inside (the next power of two pn): bits before it come from the raw
+                    // stream at r0 (A), bits after it from r0 + 1 (B)
+                    const uint32_t i0 = 8u * (uint32_t)b0;
+                    uint32_t j = 31u - (uint32_t)__builtin_clz(i0 + 2);
+                    if (i0 + j + 2 >= (2u << j))
+                        j++;
+                    const uint32_t r0 = i0 + j + 2;
+                    const uint32_t n = (2u << j) - r0; // payload bits before the parity position
+                    const uint32_t* src = (const uint32_t*)(img + ((r0 >> 5) << 2));
+                    const uint32_t sft = r0 & 31u;
+                    uint32_t E[5];
+#pragma unroll
+                    for (int i = 0; i < 5; ++i)
+                        E[i] = bswap(src[i]);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const uint64_t pair = ((uint64_t)E[u] << 32) | E[u + 1];
+                        const uint32_t A = (uint32_t)(pair >> (32 - sft));
+                        const uint32_t B = (uint32_t)(pair >> (31 - sft));
+                        const int32_t c = (int32_t)n - 32 * u;
+                        const uint32_t mk = top_bits(c <= 0 ? 0u : (uint32_t)c);
+                        o[u] = bswap((A & mk) | (B & ~mk));
+                    }
+                } else {
+                    // the row's first bytes: payload bits below 64 (several parity positions)
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int32_t i = 8 * (b0 + 4 * u);
+                        uint32_t v;
+                        if (i < 0)
+                            v = i <= -32 ? 0u : ham_head32(img, 0) >> (uint32_t)(-i);
+                        else if (i < 64)
+                            v = ham_head32(img, (uint32_t)i);
+                        else
+                            v = ham_mid32(img, (uint32_t)i);
+                        o[u] = bswap(v);
+                    }
+                }
+                uint8_t* dst = data + a0 + 16ull * p;
+                if (b0 >= 0 && b0 + 16 <= (int32_t)a.ds)
+                    *(uint4*)dst = make_uint4(o[0], o[1], o[2], o[3]);
+                else
+                    store_piece_part(dst, o, b0 < 0 ? (uint32_t)(-b0) : 0u,
+                        b0 + 16 > (int32_t)a.ds ? (uint32_t)((int32_t)a.ds - b0) : 16u);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        (void)lastw;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Parity
+// ------------------------------------------------------------------------------------
+// raw piece p (16 B) of the row from the payload superset pieces own = p and nxt = p + 1, with
+// the payload starting m bytes into piece 0 (m wave-uniform: a uniform branch per dword offset)
+__device__ __forceinline__ uint4 shift_pieces(uint4 own, uint4 nxt, uint32_t m)
+{
+    const uint32_t W[8] = { own.x, own.y, own.z, own.w, nxt.x, nxt.y, nxt.z, nxt.w };
+    const uint32_t sh = 8 * (m & 3u);
+    uint32_t o[4];
+    switch (m >> 2) {
+#define PPFS_SHIFT_CASE(D)                                                                                             \
+    case D:                                                                                                            \
+        for (int u = 0; u < 4; ++u)                                                                                    \
+            o[u] = __builtin_amdgcn_alignbit(W[u + D + 1], W[u + D], sh);                                              \
+        break;
+        PPFS_SHIFT_CASE(0)
+        PPFS_SHIFT_CASE(1)
+        PPFS_SHIFT_CASE(2)
+    default:
+        PPFS_SHIFT_CASE(3)
+#undef PPFS_SHIFT_CASE
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+__device__ __forceinline__ uint4 shfl_down1(uint4 v)
+{
+    return make_uint4(__shfl_down(v.x, 1, 64), __shfl_down(v.y, 1, 64), __shfl_down(v.z, 1, 64), __shfl_down(v.w, 1, 64));
+}
+
+__device__ __forceinline__ uint4 readlane0(uint4 v)
+{
+    return make_uint4(__builtin_amdgcn_readlane(v.x, 0), __builtin_amdgcn_readlane(v.y, 0),
+        __builtin_amdgcn_readlane(v.z, 0), __builtin_amdgcn_readlane(v.w, 0));
+}
+
+struct ParFast {
+    uint32_t bs;
+    uint64_t data_bytes;
+};
+
+template <int NP>
+__global__ __launch_bounds__(256) void parity_fast_encode_kernel(const uint8_t* __restrict__ data,
+    uint8_t* __restrict__ raw, const uint8_t* __restrict__ skip, uint64_t nblocks, ParFast a)
+{
+    const uint32_t lane = lane_id(), wave = wave_id();
+    const uint32_t ds = a.bs - 1;
+    const HamFast ha { a.bs, ds, 0, a.data_bytes };
+    const uint64_t stride = (uint64_t)gridDim.x * WAVES;
+    uint64_t blk = (uint64_t)blockIdx.x * WAVES + wave;
+    HamEncStage<NP> cur, nxt;
+    if (blk < nblocks)
+        ham_stage_load<NP>(cur, data, blk, ha, lane);
+    for (; blk < nblocks; blk += stride) {
+        const uint64_t nx = blk + stride;
+        if (nx < nblocks)
+            ham_stage_load<NP>(nxt, data, nx, ha, lane);
+        const uint32_t m = (uint32_t)((blk * ds) & 15u);
+        uint8_t* rb = raw + blk * a.bs;
+        const uint32_t old_last = (lane == 63) ? rb[a.bs - 1] : 0u;
+        uint4 O[NP];
+        uint32_t ones = 0;
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            // next piece: lane + 1 of this group, or lane 0 of the next group (or the extra piece)
+            uint4 nb = shfl_down1(cur.v[k]);
+            const uint4 first_next = readlane0(cur.v[k + 1]);
+            if (lane == 63)
+                nb = first_next;
+            uint4 o = shift_pieces(cur.v[k], nb, m);
+            if (k == NP - 1 && lane == 63)
+                o.w = (o.w & 0x00FFFFFFu) | (old_last << 24); // raw byte bs-1: old contents
+            ones += __builtin_popcount(o.x) + __builtin_popcount(o.y) + __builtin_popcount(o.z) + __builtin_popcount(o.w);
+            O[k] = o;
+        }
+        const uint32_t odd = wave_xor(ones & 1u);
+        if (!(skip && skip[blk] == 5)) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                uint4 o = O[k];
+                if (k == NP - 1 && lane == 63)
+                    o.w ^= odd << 24; // LSB of the last byte fixes the parity
+                *(uint4*)(rb + 16u * (64u * k + lane)) = o;
+            }
+        }
+        cur = nxt;
+    }
+}
+
+template <int NP>
+__global__ __launch_bounds__(256) void parity_fast_check_kernel(const uint8_t* __restrict__ raw,
+    uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks, ParFast a)
+{
+    const uint32_t lane = lane_id(), wave = wave_id();
+    const uint32_t ds = a.bs - 1;
+    const uint64_t stride = (uint64_t)gridDim.x * WAVES;
+    uint64_t blk = (uint64_t)blockIdx.x * WAVES + wave;
+    uint4 R[NP], N[NP];
+    if (blk < nblocks)
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            R[k] = *(const uint4*)(raw + blk * a.bs + 16u * (64u * k + lane));
+    for (; blk < nblocks; blk += stride) {
+        const uint64_t nx = blk + stride;
+        if (nx < nblocks)
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                N[k] = *(const uint4*)(raw + nx * a.bs + 16u * (64u * k + lane));
+        uint32_t ones = 0;
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            ones += __builtin_popcount(R[k].x) + __builtin_popcount(R[k].y) + __builtin_popcount(R[k].z)
+                + __builtin_popcount(R[k].w);
+        const uint32_t odd = wave_xor(ones & 1u);
+        if (status && lane == 0)
+            status[blk] = odd ? 5 : 0;
+        if (data) {
+            // payload byte x = raw byte x; output pieces on the payload's global 16-byte grid:
+            // piece p holds raw bytes [16 p - m, +16) = tail of raw piece p-1 + head of raw piece p
+            const uint64_t start = blk * ds, a0 = start & ~15ull;
+            const uint32_t m = (uint32_t)(start - a0);
+#pragma unroll
+            for (int k = 0; k <= NP; ++k) {
+                const uint32_t p = 64u * k + lane;
+                const uint4 own = k < NP ? R[k] : make_uint4(0, 0, 0, 0);
+                uint4 prev = make_uint4(__shfl_up(own.x, 1, 64), __shfl_up(own.y, 1, 64), __shfl_up(own.z, 1, 64),
+                    __shfl_up(own.w, 1, 64));
+                if (lane == 0) {
+                    const uint4 l63 = k > 0 ? make_uint4(__builtin_amdgcn_readlane(R[k > 0 ? k - 1 : 0].x, 63),
+                                                  __builtin_amdgcn_readlane(R[k > 0 ? k - 1 : 0].y, 63),
+                                                  __builtin_amdgcn_readlane(R[k > 0 ? k - 1 : 0].z, 63),
+                                                  __builtin_amdgcn_readlane(R[k > 0 ? k - 1 : 0].w, 63))
+                                            : make_uint4(0, 0, 0, 0);
+                    prev = l63;
+                }
+                // bytes [16 - m, 16) of prev then [0, 16 - m) of own
+                const uint4 o = shift_pieces(prev, own, (16u - m) & 15u);
+                const uint4 oo = m == 0 ? own : o;
+                const int32_t b0 = (int32_t)(16 * p) - (int32_t)m;
+                uint8_t* dst = data + a0 + 16ull * p;
+                if (b0 >= 0 && b0 + 16 <= (int32_t)ds) {
+                    *(uint4*)dst = oo;
+                } else if (b0 < (int32_t)ds && b0 + 16 > 0) {
+                    const uint32_t w[4] = { oo.x, oo.y, oo.z, oo.w };
+                    store_piece_part(dst, w, b0 < 0 ? (uint32_t)(-b0) : 0u,
+                        b0 + 16 > (int32_t)ds ? (uint32_t)((int32_t)ds - b0) : 16u);
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            R[k] = N[k];
+    }
+}
+
+} // namespace bf
+} // namespace ppfs
+
+using namespace ppfs;
+
+// Persistent grid = the kernel's resident workgroups per CU (occupancy query, i.e. what its
+// VGPR/LDS use allows) x CUs, capped by the work: a grid larger than what is resident would run
+// its last workgroups after the others finish.
+static int bf_cus()
+{
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0, c = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+            c = 256;
+        cus = c;
+    }
+    return cus;
+}
+
+template <typename K> static uint32_t bf_grid(K kernel, uint64_t nb)
+{
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0)
+        per_cu = 1;
+    const uint64_t want = (nb + bf::WAVES - 1) / bf::WAVES;
+    const uint64_t cap = (uint64_t)per_cu * (uint64_t)bf_cus();
+    return (uint32_t)(want < cap ? (want ? want : 1) : cap);
+}
+
+extern "C" int ppfs_bitfast_supported(uint32_t bs) { return bs == 1024 || bs == 2048 || bs == 4096; }
+
+#define PPFS_NP_DISPATCH(bs, KERNEL, nb, ...)                                                                         \
+    switch (bs) {                                                                                                      \
+    case 1024:                                                                                                         \
+        hipLaunchKernelGGL(KERNEL<1>, dim3(bf_grid(KERNEL<1>, nb)), dim3(256), 0, __VA_ARGS__);                        \
+        break;                                                                                                         \
+    case 2048:                                                                                                         \
+        hipLaunchKernelGGL(KERNEL<2>, dim3(bf_grid(KERNEL<2>, nb)), dim3(256), 0, __VA_ARGS__);                        \
+        break;                                                                                                         \
+    default:                                                                                                           \
+        hipLaunchKernelGGL(KERNEL<4>, dim3(bf_grid(KERNEL<4>, nb)), dim3(256), 0, __VA_ARGS__);                        \
+        break;                                                                                                         \
+    }
+
+extern "C" hipError_t ppfs_ham_fast_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs,
+    uint32_t ds, uint32_t L, hipStream_t s)
+{
+    const bf::HamFast a { bs, ds, L, nb * (uint64_t)ds };
+    PPFS_NP_DISPATCH(bs, bf::ham_fast_encode_kernel, nb, s, d, r, skip, nb, a)
+    return hipGetLastError();
+}
+
+extern "C" hipError_t ppfs_ham_fast_decode(uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, int wb, uint32_t bs,
+    uint32_t ds, uint32_t L, hipStream_t s)
+{
+    const bf::HamFast a { bs, ds, L, nb * (uint64_t)ds };
+    PPFS_NP_DISPATCH(bs, bf::ham_fast_decode_kernel, nb, s, r, d, st, nb, wb, a)
+    return hipGetLastError();
+}
+
+extern "C" hipError_t ppfs_parity_fast_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb,
+    uint32_t bs, hipStream_t s)
+{
+    const bf::ParFast a { bs, nb * (uint64_t)(bs - 1) };
+    PPFS_NP_DISPATCH(bs, bf::parity_fast_encode_kernel, nb, s, d, r, skip, nb, a)
+    return hipGetLastError();
+}
+
+extern "C" hipError_t ppfs_parity_fast_check(const uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, uint32_t bs,
+    hipStream_t s)
+{
+    const bf::ParFast a { bs, nb * (uint64_t)(bs - 1) };
+    PPFS_NP_DISPATCH(bs, bf::parity_fast_check_kernel, nb, s, r, d, st, nb, a)
+    return hipGetLastError();
+}

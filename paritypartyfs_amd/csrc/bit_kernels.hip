@@ -590,6 +590,15 @@ __global__ __launch_bounds__(256) void parity_check_kernel(const uint8_t* __rest
 
 using namespace ppfs;
 
+// 1, 2 and 4 KiB blocks: the streaming kernels of bit_fast.hip
+extern "C" int ppfs_bitfast_supported(uint32_t bs);
+extern "C" hipError_t ppfs_ham_fast_encode(const uint8_t*, uint8_t*, const uint8_t*, uint64_t, uint32_t, uint32_t,
+    uint32_t, hipStream_t);
+extern "C" hipError_t ppfs_ham_fast_decode(uint8_t*, uint8_t*, uint8_t*, uint64_t, int, uint32_t, uint32_t, uint32_t,
+    hipStream_t);
+extern "C" hipError_t ppfs_parity_fast_encode(const uint8_t*, uint8_t*, const uint8_t*, uint64_t, uint32_t, hipStream_t);
+extern "C" hipError_t ppfs_parity_fast_check(const uint8_t*, uint8_t*, uint8_t*, uint64_t, uint32_t, hipStream_t);
+
 static uint32_t bk_grid(uint64_t nb)
 {
     uint64_t g = (nb + BK_WAVES - 1) / BK_WAVES;
@@ -617,6 +626,8 @@ extern "C" hipError_t ppfs_crc_check(const uint8_t* r, uint8_t* d, uint8_t* st, 
 extern "C" hipError_t ppfs_ham_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs,
     uint32_t ds, uint32_t L, hipStream_t s)
 {
+    if (ppfs_bitfast_supported(bs))
+        return ppfs_ham_fast_encode(d, r, skip, nb, bs, ds, L, s);
     HamArgs a { bs, ds, 8 * bs, L };
     hipLaunchKernelGGL(ham_encode_kernel, dim3(bk_grid(nb)), dim3(256), 0, s, d, r, skip, nb, a);
     return hipGetLastError();
@@ -625,6 +636,8 @@ extern "C" hipError_t ppfs_ham_encode(const uint8_t* d, uint8_t* r, const uint8_
 extern "C" hipError_t ppfs_ham_decode(uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, int wb, uint32_t bs,
     uint32_t ds, uint32_t L, hipStream_t s)
 {
+    if (ppfs_bitfast_supported(bs))
+        return ppfs_ham_fast_decode(r, d, st, nb, wb, bs, ds, L, s);
     HamArgs a { bs, ds, 8 * bs, L };
     hipLaunchKernelGGL(ham_decode_kernel, dim3(bk_grid(nb)), dim3(256), 0, s, r, d, st, nb, wb, a);
     return hipGetLastError();
@@ -633,6 +646,8 @@ extern "C" hipError_t ppfs_ham_decode(uint8_t* r, uint8_t* d, uint8_t* st, uint6
 extern "C" hipError_t ppfs_parity_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs,
     hipStream_t s)
 {
+    if (ppfs_bitfast_supported(bs))
+        return ppfs_parity_fast_encode(d, r, skip, nb, bs, s);
     hipLaunchKernelGGL(parity_encode_kernel, dim3(bk_grid(nb)), dim3(256), 0, s, d, r, skip, nb, bs);
     return hipGetLastError();
 }
@@ -640,6 +655,8 @@ extern "C" hipError_t ppfs_parity_encode(const uint8_t* d, uint8_t* r, const uin
 extern "C" hipError_t ppfs_parity_check(const uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, uint32_t bs,
     hipStream_t s)
 {
+    if (ppfs_bitfast_supported(bs))
+        return ppfs_parity_fast_check(r, d, st, nb, bs, s);
     hipLaunchKernelGGL(parity_check_kernel, dim3(bk_grid(nb)), dim3(256), 0, s, r, d, st, nb, bs);
     return hipGetLastError();
 }

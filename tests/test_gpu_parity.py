@@ -245,13 +245,15 @@ def test_crc_encode_check_match_oracle(oracle, imp, bs):
 # ------------------------------------------------------------------------------------
 # Hamming
 # ------------------------------------------------------------------------------------
-@pytest.mark.parametrize("bs", [8, 16, 64, 256, 512, 4096])
-def test_hamming_matches_oracle(oracle, bs):
+@pytest.mark.parametrize("bs,nb", [(8, 1000), (16, 1000), (64, 1000), (256, 1000), (512, 1000), (1024, 1000),
+                                   (2048, 700), (4096, 300), (4096, 5003)])
+def test_hamming_matches_oracle(oracle, bs, nb):
+    """bs >= 1024 runs the streaming kernels of bit_fast.hip; 5003 blocks of 4 KiB make every
+    persistent wave walk several blocks (next-block prefetch) and end on a ragged last block."""
     eng = EccEngine(ECC_HAMMING, bs)
     ds = oracle.ham_data_size(bs)
     assert (eng.raw_block_size, eng.data_size) == (bs, ds)
-    nb = 300 if bs >= 4096 else 1000
-    rng = rng_for("ham", bs)
+    rng = rng_for("ham", bs, nb)
     data = rng.integers(0, 256, nb * ds, dtype=np.uint8)
     old = rng.integers(0, 256, nb * bs, dtype=np.uint8)
     exp = oracle.ham_encode(bs, data, raw_old=old)
@@ -280,11 +282,11 @@ def test_hamming_matches_oracle(oracle, bs):
 # ------------------------------------------------------------------------------------
 # Parity and raw
 # ------------------------------------------------------------------------------------
-@pytest.mark.parametrize("bs", [2, 16, 255, 256, 4096])
-def test_parity_matches_oracle(oracle, bs):
+@pytest.mark.parametrize("bs,nb", [(2, 999), (16, 999), (255, 999), (256, 999), (1024, 999), (2048, 999),
+                                   (4096, 999), (4096, 5003)])
+def test_parity_matches_oracle(oracle, bs, nb):
     eng = EccEngine(ECC_PARITY, bs)
-    nb = 999
-    rng = rng_for("par", bs)
+    rng = rng_for("par", bs, nb)
     data = rng.integers(0, 256, nb * (bs - 1), dtype=np.uint8)
     old = rng.integers(0, 256, nb * bs, dtype=np.uint8)
     exp = oracle.parity_encode(bs, data, raw_old=old)
