@@ -33,6 +33,8 @@ hipError_t ppfs_rs_generic_encode(const uint8_t* d, uint8_t* r, uint64_t nb, int
 hipError_t ppfs_rs_generic_decode(uint8_t* r, uint8_t* d, uint8_t* st, uint8_t* spill, uint64_t nb, int n, int t2,
     int wb, const uint8_t* tab, hipStream_t s);
 int ppfs_crc_tables_bytes(void);
+int ppfs_crc_fast_tables_bytes(void);
+int ppfs_crc_fast_supported(uint32_t bs, uint32_t n);
 hipError_t ppfs_crc_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs, uint32_t ds,
     uint32_t n, uint64_t mask, const uint8_t* tab, hipStream_t s);
 hipError_t ppfs_crc_check(const uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, uint32_t bs, uint32_t ds, uint32_t n,
@@ -305,6 +307,32 @@ std::vector<uint8_t> build_crc_tables(uint64_t P, int n, uint32_t ds)
     return out;
 }
 
+// Maps of the CRC fast path (bit_fast.hip, n <= 32): 8 nibble tables x 16 u32 entries each,
+// T[i][v] = (v << 4i) * C mod P for a constant C = x^e mod P.  Maps: x^0, x^32, x^64, x^96 (piece
+// dwords), x^8192 (one lane's pieces, 1 KiB apart), x^(128 2^j) j < 6 (lane tree), then the final
+// factor placing the zero-padded 16-byte grid: encode x^(8 (ds + m - 1024 (NP + 1)) + n - 1) for
+// each payload misalignment m < 16, check x^(8 (ds - bs) + n - 1).
+std::vector<uint8_t> build_crc_fast_tables(uint64_t P, int n, uint32_t ds, uint32_t bs)
+{
+    CrcHost c { P, n, n == 64 ? ~0ull : ((1ull << n) - 1) };
+    const long NP = bs / 1024;
+    std::vector<long> ex = { 0, 32, 64, 96, 8192 };
+    for (int j = 0; j < 6; ++j)
+        ex.push_back(128L << j);
+    for (long m = 0; m < 16; ++m)
+        ex.push_back(8L * ((long)ds + m - 1024L * (NP + 1)) + n - 1);
+    ex.push_back(8L * ((long)ds - (long)bs) + n - 1);
+    std::vector<uint8_t> out((size_t)ppfs_crc_fast_tables_bytes(), 0);
+    uint32_t* t = (uint32_t*)out.data();
+    for (size_t mi = 0; mi < ex.size(); ++mi) {
+        const uint64_t C = c.xpow(ex[mi]);
+        for (int i = 0; i < 8; ++i)
+            for (int v = 0; v < 16; ++v)
+                t[(mi * 8 + i) * 16 + v] = (uint32_t)c.mul(c.mod((uint64_t)v << (4 * i)), C);
+    }
+    return out;
+}
+
 int bitlen64(uint64_t v)
 {
     int c = 0;
@@ -402,6 +430,10 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
         c->raw = p.block_size;
         c->data = p.block_size - nbc;
         tables = build_crc_tables(p.crc_polynomial, n, c->data);
+        if (ppfs_crc_fast_supported(p.block_size, (uint32_t)n)) {
+            const std::vector<uint8_t> f = build_crc_fast_tables(p.crc_polynomial, n, c->data, p.block_size);
+            tables.insert(tables.end(), f.begin(), f.end());
+        }
         c->kname = "crc-nibble-shift";
         break;
     }

@@ -558,6 +558,252 @@ __global__ __launch_bounds__(256) void parity_fast_check_kernel(const uint8_t* _
     }
 }
 
+
+// ------------------------------------------------------------------------------------
+// CRC (n <= 32): V = D(x) x^(n-1) mod P over the payload D (MSB first), stored = (V << 1) & mask
+// written MSB first after the payload (crc_polynomial.cpp:56-76 stops one reduction step early;
+// closed form in DESIGN.md / SURVEY.md §0.4).  Everything is a linear map of 32-bit values mod P,
+// done with nibble tables ("cmap": 8 LDS lookups of u32, every lane reading the same table):
+//   piece (16 B = dwords D0..D3, big-endian) -> D0 x^96 + D1 x^64 + D2 x^32 + D3 mod P;
+//   a lane's pieces (1 KiB apart) by Horner with x^8192; the 64 lanes by a 6-level tree with
+//   x^(128 2^j); then one block-uniform factor x^e that places the zero-padded 16-byte grid at the
+//   payload's real position (e < 0 uses x^-1: P(0) = 1).
+// ------------------------------------------------------------------------------------
+constexpr int CF_MAP = 512;                      // 8 nibbles x 16 entries x u32
+constexpr int CF_M0 = 0, CF_K = 4, CF_L = 5, CF_FENC = 11, CF_FCHK = 27, CF_NMAPS = 28;
+constexpr int CF_BYTES = CF_NMAPS * CF_MAP;     // 14 KiB
+
+// (x >> 8k) & 0x3C (a nibble * 4, the entry's byte offset): one v_and_b32_sdwa for k > 0
+__device__ __forceinline__ uint32_t sel3c(uint32_t x, int k)
+{
+    uint32_t r;
+    switch (k & 3) {
+    case 0:
+        return x & 0x3Cu;
+    case 1:
+        asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+            : "=v"(r) : "v"(x), "s"(0x3Cu));
+        return r;
+    case 2:
+        asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD"
+            : "=v"(r) : "v"(x), "s"(0x3Cu));
+        return r;
+    default:
+        asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD"
+            : "=v"(r) : "v"(x), "s"(0x3Cu));
+        return r;
+    }
+}
+
+// v(x) * C mod P, C given by its map (tb: LDS byte address of 8 nibble tables)
+__device__ __forceinline__ uint32_t cmap(const uint8_t* tb, uint32_t v)
+{
+    const uint32_t lo = v << 2, hi = v >> 2; // low / high nibble of byte b at bits 8b+2..8b+5
+    uint32_t e[8];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        e[2 * b] = *(const uint32_t*)(tb + (2 * b) * 64 + sel3c(lo, b));
+        e[2 * b + 1] = *(const uint32_t*)(tb + (2 * b + 1) * 64 + sel3c(hi, b));
+    }
+    return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(e[0], e[1], e[2], 0x96),
+        __builtin_amdgcn_bitop3_b32(e[3], e[4], e[5], 0x96), e[6] ^ e[7], 0x96);
+}
+
+struct CrcFast {
+    uint32_t bs, ds, n, nbc, mask;
+    uint64_t data_bytes;
+};
+
+// 16 payload bytes (memory order) -> piece value mod P; bytes outside [lo, hi) count as zero
+__device__ __forceinline__ uint32_t crc_piece(const uint8_t* tbl, uint4 v, uint32_t lo, uint32_t hi, bool n32)
+{
+    uint32_t w[4] = { v.x, v.y, v.z, v.w };
+    if (lo > 0 || hi < 16) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            uint32_t keep = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                keep |= (4u * u + b >= lo && 4u * u + b < hi) ? (0xFFu << (8 * b)) : 0u;
+            w[u] &= keep;
+        }
+    }
+    const uint32_t d3 = bswap(w[3]);
+    return __builtin_amdgcn_bitop3_b32(cmap(tbl + 3 * CF_MAP, bswap(w[0])), cmap(tbl + 2 * CF_MAP, bswap(w[1])),
+               cmap(tbl + 1 * CF_MAP, bswap(w[2])), 0x96)
+        ^ (n32 ? d3 : cmap(tbl + CF_M0 * CF_MAP, d3));
+}
+
+// Sum over the wave of value_l * x^(128 (63 - l)) -> wave-uniform
+__device__ __forceinline__ uint32_t crc_lane_tree(const uint8_t* tbl, uint32_t acc)
+{
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const uint32_t other = __shfl_down(acc, 1 << j, 64);
+        acc = cmap(tbl + (CF_L + j) * CF_MAP, acc) ^ other;
+    }
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)acc);
+}
+
+template <int NP>
+__global__ __launch_bounds__(256) void crc_fast_encode_kernel(const uint8_t* __restrict__ data,
+    uint8_t* __restrict__ raw, const uint8_t* __restrict__ skip, uint64_t nblocks, CrcFast a,
+    const uint8_t* __restrict__ tables)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t tbl[CF_BYTES];
+    for (uint32_t p = threadIdx.x; p < CF_BYTES / 16; p += 256)
+        *(uint4*)(tbl + 16 * p) = *(const uint4*)(tables + 16 * p);
+    __syncthreads();
+    const uint32_t lane = lane_id(), wave = wave_id();
+    const HamFast ha { a.bs, a.ds, 0, a.data_bytes };
+    const bool n32 = a.n == 32;
+    const uint64_t stride = (uint64_t)gridDim.x * WAVES;
+    uint64_t blk = (uint64_t)blockIdx.x * WAVES + wave;
+    HamEncStage<NP> cur, nxt;
+    if (blk < nblocks)
+        ham_stage_load<NP>(cur, data, blk, ha, lane);
+    for (; blk < nblocks; blk += stride) {
+        const uint64_t nx = blk + stride;
+        if (nx < nblocks)
+            ham_stage_load<NP>(nxt, data, nx, ha, lane);
+        const uint32_t m = (uint32_t)((blk * a.ds) & 15u); // payload byte 0 = superset byte m
+        uint8_t* rb = raw + blk * a.bs;
+        // superset piece q = 64 k + lane holds superset bytes [16 q, +16); payload = [m, m + ds)
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k <= NP; ++k) {
+            const int32_t q16 = 16 * (64 * k + (int32_t)lane);
+            const int32_t lo = (int32_t)m - q16, hi = (int32_t)(m + a.ds) - q16;
+            const uint32_t lo_c = lo < 0 ? 0u : (lo > 16 ? 16u : (uint32_t)lo);
+            const uint32_t hi_c = hi < 0 ? 0u : (hi > 16 ? 16u : (uint32_t)hi);
+            const uint32_t pv = crc_piece(tbl, cur.v[k], lo_c, hi_c > lo_c ? hi_c : lo_c, n32);
+            acc = k == 0 ? pv : (cmap(tbl + CF_K * CF_MAP, acc) ^ pv);
+        }
+        const uint32_t Vs = crc_lane_tree(tbl, acc);
+        const uint32_t V = cmap(tbl + (CF_FENC + m) * CF_MAP, Vs);
+        const uint32_t st = (V << 1) & a.mask;
+        if (!(skip && skip[blk] == 5)) {
+            // raw bytes [ds, ds + nbc): the n CRC bits MSB first (a partial last byte keeps its old
+            // low bits); all in the row's last raw piece (lane 63, k = NP - 1)
+            uint32_t old_last = 0;
+            if (lane == 63 && (a.n & 7u))
+                old_last = rb[a.ds + a.nbc - 1];
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                uint4 nb = shfl_down1(cur.v[k]);
+                const uint4 first_next = readlane0(cur.v[k + 1]);
+                if (lane == 63)
+                    nb = first_next;
+                uint4 o = shift_pieces(cur.v[k], nb, m);
+                if (k == NP - 1 && lane == 63) {
+                    uint32_t w[4] = { o.x, o.y, o.z, o.w };
+                    const uint32_t base = a.ds - 16u * (64u * (NP - 1) + 63u); // field byte 0 in the piece
+#pragma unroll
+                    for (int b = 0; b < 16; ++b) {
+                        const int32_t u = b - (int32_t)base;
+                        if (u >= 0 && u < (int32_t)a.nbc) {
+                            uint32_t byte;
+                            if (8u * (uint32_t)(u + 1) <= a.n) {
+                                byte = (st >> (a.n - 8u * (uint32_t)(u + 1))) & 0xFFu;
+                            } else {
+                                const uint32_t rbits = a.n & 7u;
+                                byte = ((st & ((1u << rbits) - 1u)) << (8 - rbits)) | (old_last & ((1u << (8 - rbits)) - 1u));
+                            }
+                            w[b >> 2] = (w[b >> 2] & ~(0xFFu << (8 * (b & 3)))) | (byte << (8 * (b & 3)));
+                        }
+                    }
+                    o = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+                *(uint4*)(rb + 16u * (64u * k + lane)) = o;
+            }
+        }
+        cur = nxt;
+    }
+}
+
+template <int NP>
+__global__ __launch_bounds__(256) void crc_fast_check_kernel(const uint8_t* __restrict__ raw,
+    uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks, CrcFast a,
+    const uint8_t* __restrict__ tables)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t tbl[CF_BYTES];
+    for (uint32_t p = threadIdx.x; p < CF_BYTES / 16; p += 256)
+        *(uint4*)(tbl + 16 * p) = *(const uint4*)(tables + 16 * p);
+    __syncthreads();
+    const uint32_t lane = lane_id(), wave = wave_id();
+    const bool n32 = a.n == 32;
+    const uint32_t ds = a.ds;
+    const uint64_t stride = (uint64_t)gridDim.x * WAVES;
+    uint64_t blk = (uint64_t)blockIdx.x * WAVES + wave;
+    uint4 R[NP], N[NP];
+    if (blk < nblocks)
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            R[k] = *(const uint4*)(raw + blk * a.bs + 16u * (64u * k + lane));
+    for (; blk < nblocks; blk += stride) {
+        const uint64_t nx = blk + stride;
+        if (nx < nblocks)
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                N[k] = *(const uint4*)(raw + nx * a.bs + 16u * (64u * k + lane));
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            const int32_t q16 = 16 * (64 * k + (int32_t)lane);
+            const int32_t hi = (int32_t)ds - q16;
+            const uint32_t hi_c = hi < 0 ? 0u : (hi > 16 ? 16u : (uint32_t)hi);
+            const uint32_t pv = crc_piece(tbl, R[k], 0u, hi_c, n32);
+            acc = k == 0 ? pv : (cmap(tbl + CF_K * CF_MAP, acc) ^ pv);
+        }
+        const uint32_t Vs = crc_lane_tree(tbl, acc);
+        const uint32_t V = cmap(tbl + CF_FCHK * CF_MAP, Vs);
+        const uint32_t st = (V << 1) & a.mask;
+        // stored field: n bits MSB first from byte ds (in the last raw piece, lane 63)
+        const uint4 last = make_uint4(__builtin_amdgcn_readlane(R[NP - 1].x, 63), __builtin_amdgcn_readlane(R[NP - 1].y, 63),
+            __builtin_amdgcn_readlane(R[NP - 1].z, 63), __builtin_amdgcn_readlane(R[NP - 1].w, 63));
+        const uint32_t lw[4] = { last.x, last.y, last.z, last.w };
+        const uint32_t base = ds - 16u * (64u * (NP - 1) + 63u);
+        uint64_t f = 0;
+        for (uint32_t u = 0; u < a.nbc; ++u) {
+            const uint32_t b = base + u;
+            f = (f << 8) | ((lw[b >> 2] >> (8 * (b & 3))) & 0xFFu);
+        }
+        const uint32_t field = (uint32_t)(f >> (8 * a.nbc - a.n));
+        if (status && lane == 0)
+            status[blk] = (st == field) ? 0 : 5;
+        if (data) {
+            const uint64_t start = blk * ds, a0 = start & ~15ull;
+            const uint32_t m = (uint32_t)(start - a0);
+#pragma unroll
+            for (int k = 0; k <= NP; ++k) {
+                const uint32_t p = 64u * k + lane;
+                const uint4 own = k < NP ? R[k] : make_uint4(0, 0, 0, 0);
+                uint4 prev = make_uint4(__shfl_up(own.x, 1, 64), __shfl_up(own.y, 1, 64), __shfl_up(own.z, 1, 64),
+                    __shfl_up(own.w, 1, 64));
+                if (lane == 0)
+                    prev = k > 0 ? make_uint4(__builtin_amdgcn_readlane(R[k > 0 ? k - 1 : 0].x, 63),
+                                       __builtin_amdgcn_readlane(R[k > 0 ? k - 1 : 0].y, 63),
+                                       __builtin_amdgcn_readlane(R[k > 0 ? k - 1 : 0].z, 63),
+                                       __builtin_amdgcn_readlane(R[k > 0 ? k - 1 : 0].w, 63))
+                                 : make_uint4(0, 0, 0, 0);
+                const uint4 oo = m == 0 ? own : shift_pieces(prev, own, (16u - m) & 15u);
+                const int32_t b0 = (int32_t)(16 * p) - (int32_t)m;
+                uint8_t* dst = data + a0 + 16ull * p;
+                if (b0 >= 0 && b0 + 16 <= (int32_t)ds) {
+                    *(uint4*)dst = oo;
+                } else if (b0 < (int32_t)ds && b0 + 16 > 0) {
+                    const uint32_t w[4] = { oo.x, oo.y, oo.z, oo.w };
+                    store_piece_part(dst, w, b0 < 0 ? (uint32_t)(-b0) : 0u,
+                        b0 + 16 > (int32_t)ds ? (uint32_t)((int32_t)ds - b0) : 16u);
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            R[k] = N[k];
+    }
+}
+
 } // namespace bf
 } // namespace ppfs
 
@@ -617,6 +863,24 @@ extern "C" hipError_t ppfs_ham_fast_decode(uint8_t* r, uint8_t* d, uint8_t* st, 
 {
     const bf::HamFast a { bs, ds, L, nb * (uint64_t)ds };
     PPFS_NP_DISPATCH(bs, bf::ham_fast_decode_kernel, nb, s, r, d, st, nb, wb, a)
+    return hipGetLastError();
+}
+
+extern "C" int ppfs_crc_fast_tables_bytes(void) { return bf::CF_BYTES; }
+
+extern "C" hipError_t ppfs_crc_fast_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs,
+    uint32_t ds, uint32_t n, uint64_t mask, const uint8_t* tab, hipStream_t s)
+{
+    const bf::CrcFast a { bs, ds, n, bs - ds, (uint32_t)mask, nb * (uint64_t)ds };
+    PPFS_NP_DISPATCH(bs, bf::crc_fast_encode_kernel, nb, s, d, r, skip, nb, a, tab)
+    return hipGetLastError();
+}
+
+extern "C" hipError_t ppfs_crc_fast_check(const uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, uint32_t bs,
+    uint32_t ds, uint32_t n, uint64_t mask, const uint8_t* tab, hipStream_t s)
+{
+    const bf::CrcFast a { bs, ds, n, bs - ds, (uint32_t)mask, nb * (uint64_t)ds };
+    PPFS_NP_DISPATCH(bs, bf::crc_fast_check_kernel, nb, s, r, d, st, nb, a, tab)
     return hipGetLastError();
 }
 

@@ -598,6 +598,13 @@ extern "C" hipError_t ppfs_ham_fast_decode(uint8_t*, uint8_t*, uint8_t*, uint64_
     hipStream_t);
 extern "C" hipError_t ppfs_parity_fast_encode(const uint8_t*, uint8_t*, const uint8_t*, uint64_t, uint32_t, hipStream_t);
 extern "C" hipError_t ppfs_parity_fast_check(const uint8_t*, uint8_t*, uint8_t*, uint64_t, uint32_t, hipStream_t);
+extern "C" hipError_t ppfs_crc_fast_encode(const uint8_t*, uint8_t*, const uint8_t*, uint64_t, uint32_t, uint32_t,
+    uint32_t, uint64_t, const uint8_t*, hipStream_t);
+extern "C" hipError_t ppfs_crc_fast_check(const uint8_t*, uint8_t*, uint8_t*, uint64_t, uint32_t, uint32_t, uint32_t,
+    uint64_t, const uint8_t*, hipStream_t);
+
+// the CRC fast path (n <= 32, 1-4 KiB blocks) reads its tables after the generic ones
+extern "C" int ppfs_crc_fast_supported(uint32_t bs, uint32_t n) { return ppfs_bitfast_supported(bs) && n <= 32; }
 
 static uint32_t bk_grid(uint64_t nb)
 {
@@ -610,6 +617,8 @@ extern "C" int ppfs_crc_tables_bytes(void) { return CRC_TBL_BYTES; }
 extern "C" hipError_t ppfs_crc_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs,
     uint32_t ds, uint32_t n, uint64_t mask, const uint8_t* tab, hipStream_t s)
 {
+    if (ppfs_crc_fast_supported(bs, n))
+        return ppfs_crc_fast_encode(d, r, skip, nb, bs, ds, n, mask, tab + CRC_TBL_BYTES, s);
     CrcArgs a { bs, ds, n, (ds + 63) / 64, (n + 3) / 4, mask };
     hipLaunchKernelGGL(crc_encode_kernel, dim3(bk_grid(nb)), dim3(256), 0, s, d, r, skip, nb, a, tab);
     return hipGetLastError();
@@ -618,6 +627,8 @@ extern "C" hipError_t ppfs_crc_encode(const uint8_t* d, uint8_t* r, const uint8_
 extern "C" hipError_t ppfs_crc_check(const uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, uint32_t bs, uint32_t ds,
     uint32_t n, uint64_t mask, const uint8_t* tab, hipStream_t s)
 {
+    if (ppfs_crc_fast_supported(bs, n))
+        return ppfs_crc_fast_check(r, d, st, nb, bs, ds, n, mask, tab + CRC_TBL_BYTES, s);
     CrcArgs a { bs, ds, n, (ds + 63) / 64, (n + 3) / 4, mask };
     hipLaunchKernelGGL(crc_check_kernel, dim3(bk_grid(nb)), dim3(256), 0, s, r, d, st, nb, a, tab);
     return hipGetLastError();
