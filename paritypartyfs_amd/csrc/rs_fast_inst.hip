@@ -1,6 +1,7 @@
 // rs_fast_inst.hip -- one fast-path instantiation (2t = PPFS_T2), compiled once per 2t.
 #include "rs_fast.hpp"
 #include "rs_wg.hpp"
+#include "rs_col.hpp"
 
 #ifndef PPFS_T2
 #error "compile with -DPPFS_T2=<2t>"
@@ -31,33 +32,41 @@ static uint32_t rs_grid(uint64_t nb)
     return (uint32_t)(want < cap ? (want ? want : 1) : cap);
 }
 
-#if PPFS_T2 <= 8
-// workgroup path (2t <= 8): one 256-thread workgroup per 64-block tile, WPC resident per CU
-constexpr int ENC_NBUF = 2, ENC_WPC = (4 * wg::lds_bytes<PPFS_T2, false, 2>() <= 163840) ? 4 : 3;
-constexpr int DEC_NBUF = 2, DEC_WPC = 3;
-
-static uint32_t rs_wg_grid(uint64_t nb, int wpc)
+// persistent tile grid: WPC resident 256-thread workgroups per CU, capped by the 64-block tiles
+static uint32_t rs_tile_grid(uint64_t nb, int wpc)
 {
     int dev = 0;
     (void)hipGetDevice(&dev);
     int c = 0;
     if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
         c = 256;
-    const uint64_t tiles = (nb + wg::TB - 1) / wg::TB;
+    const uint64_t tiles = (nb + 63) / 64;
     const uint64_t cap = (uint64_t)wpc * (uint64_t)c;
     return (uint32_t)(tiles < cap ? (tiles ? tiles : 1) : cap);
 }
+
+#if PPFS_T2 <= 8
+// segment workgroup path (2t <= 8): one 256-thread workgroup per 64-block tile, WPC resident per CU
+constexpr int ENC_NBUF = 2, ENC_WPC = (4 * wg::lds_bytes<PPFS_T2, false, 2>() <= 163840) ? 4 : 3;
+constexpr int DEC_NBUF = 2, DEC_WPC = 3;
+#elif PPFS_T2 > 16
+// column-split workgroup path (16 < 2t <= 32): two workgroups per CU (LDS: byte tables + 2 tiles)
+constexpr int COL_WPC = 2;
 #endif
+// 8 < 2t <= 16: lane-per-block kernels (rs_fast.hpp); the column path leaves half of its lanes on
+// all-zero state columns there and measured slower on decode
 
 extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d, uint8_t* r, uint64_t nb,
     const uint8_t* tab, hipStream_t s)
 {
 #if PPFS_T2 <= 8
-    hipLaunchKernelGGL((wg::rs_wg_encode_kernel<PPFS_T2, ENC_NBUF, ENC_WPC>), dim3(rs_wg_grid(nb, ENC_WPC)), dim3(256), 0, s,
+    hipLaunchKernelGGL((wg::rs_wg_encode_kernel<PPFS_T2, ENC_NBUF, ENC_WPC>), dim3(rs_tile_grid(nb, ENC_WPC)), dim3(256),
+        0, s, d, r, nb, tab);
+#elif PPFS_T2 > 16
+    hipLaunchKernelGGL((col::rs_col_encode_kernel<PPFS_T2, COL_WPC>), dim3(rs_tile_grid(nb, COL_WPC)), dim3(256), 0, s,
         d, r, nb, tab);
 #else
-    const uint32_t grid = rs_grid(nb);
-    hipLaunchKernelGGL(rs255_encode_kernel<PPFS_T2>, dim3(grid), dim3(256), 0, s, d, r, nb, tab);
+    hipLaunchKernelGGL(rs255_encode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, d, r, nb, tab);
 #endif
     return hipGetLastError();
 }
@@ -66,11 +75,13 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
     const uint8_t* tab, int wb, hipStream_t s)
 {
 #if PPFS_T2 <= 8
-    hipLaunchKernelGGL((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC>), dim3(rs_wg_grid(nb, DEC_WPC)), dim3(256), 0,
-        s, r, d, st, nb, tab, wb);
+    hipLaunchKernelGGL((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC>), dim3(rs_tile_grid(nb, DEC_WPC)), dim3(256),
+        0, s, r, d, st, nb, tab, wb);
+#elif PPFS_T2 > 16
+    hipLaunchKernelGGL((col::rs_col_decode_kernel<PPFS_T2, COL_WPC>), dim3(rs_tile_grid(nb, COL_WPC)), dim3(256), 0, s,
+        r, d, st, nb, tab, wb);
 #else
-    const uint32_t grid = rs_grid(nb);
-    hipLaunchKernelGGL(rs255_decode_kernel<PPFS_T2>, dim3(grid), dim3(256), 0, s, r, d, st, nb, tab, wb);
+    hipLaunchKernelGGL(rs255_decode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, r, d, st, nb, tab, wb);
 #endif
     return hipGetLastError();
 }

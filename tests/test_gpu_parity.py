@@ -121,10 +121,12 @@ def inject_rs_fast(rng, cw, n, t, nblocks):
     return bad.reshape(-1)
 
 
-@pytest.mark.parametrize("bs,t", [(512, 3), (256, 4), (255, 1), (1024, 5)], ids=lambda x: str(x))
+@pytest.mark.parametrize("bs,t", [(512, 3), (256, 4), (255, 1), (1024, 5), (4096, 8), (4096, 16)],
+                         ids=lambda x: str(x))
 def test_rs_many_tiles_per_workgroup(oracle, bs, t):
-    """Batches past one resident grid (3 workgroups/CU x 256 CUs x 64 blocks): every workgroup walks
-    several tiles, so the double-buffered prefetch of the next tile and the ragged last tile run."""
+    """Batches past one resident grid (2-4 workgroups/CU x 256 CUs x 64 blocks): every workgroup
+    walks several tiles, so the double-buffered prefetch of the next tile and the ragged last tile
+    run (segment kernels for 2t <= 8, column kernels for 2t > 8)."""
     n, k, _ = oracle.rs_sizes(bs, t)
     nb = 3 * 768 * 64 + 37
     eng = EccEngine(ECC_REED_SOLOMON, bs, t)
