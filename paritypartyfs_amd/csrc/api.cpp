@@ -35,6 +35,7 @@ hipError_t ppfs_rs_generic_decode(uint8_t* r, uint8_t* d, uint8_t* st, uint8_t* 
 int ppfs_crc_tables_bytes(void);
 int ppfs_crc_fast_tables_bytes(void);
 int ppfs_crc_fast_supported(uint32_t bs, uint32_t n);
+int ppfs_bitfast_supported(uint32_t bs);
 hipError_t ppfs_crc_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs, uint32_t ds,
     uint32_t n, uint64_t mask, const uint8_t* tab, hipStream_t s);
 hipError_t ppfs_crc_check(const uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, uint32_t bs, uint32_t ds, uint32_t n,
@@ -460,7 +461,7 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
             const std::vector<uint8_t> f = build_crc_fast_tables(p.crc_polynomial, n, c->data, p.block_size);
             tables.insert(tables.end(), f.begin(), f.end());
         }
-        c->kname = "crc-nibble-shift";
+        c->kname = ppfs_crc_fast_supported(p.block_size, (uint32_t)n) ? "crc-piecemap-wave" : "crc-nibble-shift";
         break;
     }
     case PPFS_ECC_HAMMING: {
@@ -480,7 +481,7 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
                 idx++;
             c->ham_L = idx++;
         }
-        c->kname = "hamming-funnel";
+        c->kname = ppfs_bitfast_supported(c->raw) ? "hamming-stream-wave" : "hamming-funnel";
         break;
     }
     case PPFS_ECC_PARITY:
@@ -490,7 +491,7 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
         }
         c->raw = p.block_size;
         c->data = p.block_size - 1;
-        c->kname = "parity-popcount";
+        c->kname = ppfs_bitfast_supported(c->raw) ? "parity-stream-wave" : "parity-popcount";
         break;
     default:
         delete c;
