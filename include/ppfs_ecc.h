@@ -128,6 +128,38 @@ int ppfs_ecc_decode_host(ppfs_ecc_ctx* ctx, uint8_t* raw, uint8_t* data, uint8_t
 int ppfs_ecc_write_host(ppfs_ecc_ctx* ctx, const uint8_t* data, uint8_t* raw, uint8_t* status,
     size_t nblocks);
 
+/*
+ * Whole-image scrub: the disk-image effect of readBlock(i, 0, dataSize()) for
+ * i = 0 .. nblocks-1 in index order, without the payloads -- RS writes back the corrected
+ * codeword (rs_block_device.cpp:175-180), Hamming the flipped byte (hamming_block_device.cpp:41-51),
+ * CRC and parity only check (crc_block_device.cpp:12-35, parity_block_device.cpp:90-97).
+ *   image        packed raw blocks from block 0; image_bytes >= nblocks * rawBlockSize() is the
+ *                extent a write-back may touch (a shortened RS code, n < 255, can write up to
+ *                255 - n bytes past a block end: into the next blocks, which are then scrubbed as
+ *                modified, as the sequential reference reads them; a write-back that would pass
+ *                image_bytes is rejected whole, like HeapDisk::write, heap_disk.cpp:21-27).
+ *   status       (may be NULL) one status byte per block.
+ *   counts       (host form, may be NULL) [blocks ok, blocks corrected, blocks failed].
+ * The device form enqueues on `stream`; with n < 255 it synchronises between runs of blocks.
+ */
+int ppfs_ecc_scrub_host(ppfs_ecc_ctx* ctx, uint8_t* image, size_t image_bytes, size_t nblocks, uint8_t* status,
+    size_t* counts);
+int ppfs_ecc_scrub_device(ppfs_ecc_ctx* ctx, uint8_t* d_image, size_t image_bytes, size_t nblocks,
+    uint8_t* d_status, void* stream);
+
+/*
+ * 2-of-3 bitwise majority of nrec replicated records of rec_bytes each, replacing
+ * SuperBlockManager::_performBitVoting (lib/super_block_manager/src/super_block_manager.cpp:133-165):
+ *   out[i] = majority(a[i], b[i], c[i]) bit by bit;
+ *   damaged (may be NULL) per record: bit k set when copy k+1 differs from the majority
+ *   (the reference's damaged1/2/3).
+ * The host form runs on HIP device `device` and returns when the outputs are in host memory.
+ */
+int ppfs_vote3_device(const uint8_t* d_a, const uint8_t* d_b, const uint8_t* d_c, uint8_t* d_out, size_t rec_bytes,
+    size_t nrec, uint32_t* d_damaged, void* stream);
+int ppfs_vote3_host(int device, const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* out, size_t rec_bytes,
+    size_t nrec, uint32_t* damaged);
+
 /* Last HIP error string recorded by this thread (diagnostics). */
 const char* ppfs_ecc_last_error(void);
 

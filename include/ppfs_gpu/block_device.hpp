@@ -375,6 +375,28 @@ public:
     virtual expected<void> readBlocks(block_index_t first, size_t count, uint8_t* out, uint8_t* err) = 0;
     virtual expected<void> writeBlocks(block_index_t first, size_t count, const uint8_t* payloads, uint8_t* err)
         = 0;
+
+    // Whole-image scrub extension: the disk and log effect of
+    // readBlock({i, 0}, dataSize()) for i in [first, first + count), in order, without the
+    // payloads.  counts (may be null): blocks ok / corrected / failed; err as readBlocks.
+    virtual expected<void> scrub(block_index_t first, size_t count, size_t* counts, uint8_t* err)
+    {
+        std::vector<uint8_t> out(count * dataSize()), e(count);
+        auto r = readBlocks(first, count, out.data(), e.data());
+        if (!r)
+            return r;
+        size_t failed = 0;
+        for (uint8_t x : e)
+            failed += x != 0;
+        if (counts) {
+            counts[0] = count - failed;
+            counts[1] = 0;
+            counts[2] = failed;
+        }
+        if (err)
+            std::memcpy(err, e.data(), count);
+        return {};
+    }
 };
 
 namespace detail {
@@ -570,6 +592,44 @@ public:
         auto w = detail::disk_write(_disk, (size_t)first * _raw, raw.data(), count * _raw);
         if (!w)
             return unexpected(w.error());
+        return {};
+    }
+
+    // One engine call (ppfs_ecc_scrub_host) over the disk image from block `first` to the disk
+    // end: the write-back of every corrected block is applied in index order, including RS
+    // bytes a shortened code writes past a block end; corrected blocks are logged in order.
+    expected<void> scrub(block_index_t first, size_t count, size_t* counts, uint8_t* err) override
+    {
+        if (err)
+            std::memset(err, 0, count);
+        const size_t base = (size_t)first * _raw;
+        if (base + count * _raw > _disk.size())
+            return unexpected(FsError::Disk_OutOfBounds);
+        std::vector<uint8_t> image(_disk.size() - base), status(count);
+        auto rr = detail::disk_read(_disk, base, image.size(), image.data());
+        if (!rr)
+            return unexpected(rr.error());
+        const std::vector<uint8_t> before = image;
+        size_t c3[3] = { 0, 0, 0 };
+        EccEngine::check(ppfs_ecc_scrub_host(_eng.ctx(), image.data(), image.size(), count, status.data(), c3), "scrub");
+        for (size_t i = 0; i < count; ++i) {
+            if (status[i] == PPFS_ECC_CORRECTION_ERROR && err)
+                err[i] = (uint8_t)FsError::BlockDevice_CorrectionError;
+            else if (status[i] == PPFS_ECC_CORRECTED)
+                log(first + (block_index_t)i);
+        }
+        size_t lo = 0, hi = image.size();
+        while (lo < hi && image[lo] == before[lo])
+            ++lo;
+        while (hi > lo && image[hi - 1] == before[hi - 1])
+            --hi;
+        if (hi > lo) {
+            auto w = detail::disk_write(_disk, base + lo, image.data() + lo, hi - lo);
+            if (!w)
+                return unexpected(w.error());
+        }
+        if (counts)
+            std::memcpy(counts, c3, sizeof c3);
         return {};
     }
 

@@ -1097,3 +1097,28 @@ EXPORT int oracle_dev_write(void* h, int block, size_t offset, const uint8_t* da
     *written = to_write;
     return 0;
 }
+
+/* ------------------------------------------------------------------------------------------
+ * SuperBlockManager::_performBitVoting (lib/super_block_manager/src/super_block_manager.cpp:133-165):
+ * per bit b1 + b2 + b3 >= 2 -> 1; copy k damaged when any bit differs from the majority.
+ * Restated bit by bit with the BitHelpers numbering, per record of rec_bytes.
+ * damaged[r] bit k-1 = damaged<k>.
+ * ------------------------------------------------------------------------------------------ */
+EXPORT void oracle_vote3(const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* out, size_t rec_bytes,
+    size_t nrec, uint32_t* damaged)
+{
+    for (size_t r = 0; r < nrec; ++r) {
+        const size_t o = r * rec_bytes, nbits = rec_bytes * 8;
+        int d1 = 0, d2 = 0, d3 = 0;
+        memset(out + o, 0, rec_bytes);
+        for (size_t bit = 0; bit < nbits; ++bit) {
+            const int b1 = get_bit(a + o, bit), b2 = get_bit(b + o, bit), b3 = get_bit(c + o, bit);
+            const int majority = (b1 + b2 + b3) >= 2;
+            set_bit(out + o, bit, majority);
+            d1 |= b1 != majority;
+            d2 |= b2 != majority;
+            d3 |= b3 != majority;
+        }
+        damaged[r] = (uint32_t)(d1 | (d2 << 1) | (d3 << 2));
+    }
+}

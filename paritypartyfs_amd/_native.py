@@ -31,6 +31,10 @@ EXPORTED_SYMBOLS = (
     "ppfs_ecc_encode_host",
     "ppfs_ecc_decode_host",
     "ppfs_ecc_write_host",
+    "ppfs_ecc_scrub_host",
+    "ppfs_ecc_scrub_device",
+    "ppfs_vote3_device",
+    "ppfs_vote3_host",
     "ppfs_ecc_last_error",
 )
 
@@ -61,6 +65,14 @@ def lib() -> ctypes.CDLL:
         raise NativeLibraryMissing(
             f"{LIB_PATH} not found: build it with `make -C paritypartyfs_amd/csrc` "
             "(or __graft_entry__.build()); the HIP engine has no CPU fallback")
+    # torch bundles its own libamdhip64; with both runtimes in one process torch's has to
+    # initialise first (measured: the other order leaves torch with "No HIP GPUs are available")
+    try:
+        import torch
+
+        torch.cuda.is_available()
+    except Exception:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     u8p = POINTER(c_uint8)
     L.ppfs_ecc_crc_implicit_to_explicit.restype = c_uint64
@@ -88,6 +100,14 @@ def lib() -> ctypes.CDLL:
     L.ppfs_ecc_decode_host.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_void_p]
     L.ppfs_ecc_write_host.restype = c_int
     L.ppfs_ecc_write_host.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]
+    L.ppfs_ecc_scrub_host.restype = c_int
+    L.ppfs_ecc_scrub_host.argtypes = [c_void_p, c_void_p, c_size_t, c_size_t, c_void_p, POINTER(c_size_t)]
+    L.ppfs_ecc_scrub_device.restype = c_int
+    L.ppfs_ecc_scrub_device.argtypes = [c_void_p, c_void_p, c_size_t, c_size_t, c_void_p, c_void_p]
+    L.ppfs_vote3_device.restype = c_int
+    L.ppfs_vote3_device.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p, c_void_p]
+    L.ppfs_vote3_host.restype = c_int
+    L.ppfs_vote3_host.argtypes = [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p]
     L.ppfs_ecc_last_error.restype = c_char_p
     L.ppfs_ecc_last_error.argtypes = []
     _ = u8p

@@ -195,6 +195,15 @@ class IBlockDevice:
                 err[i] = int(r.error())
         return out, err
 
+    def scrub(self, first: int = 0, count: Optional[int] = None) -> Tuple[Tuple[int, int, int], np.ndarray]:
+        """Whole-image scrub: the disk and log effect of readBlock(DataLocation(i, 0),
+        dataSize()) for i in [first, first+count), in order, without the payloads.
+        Returns ((ok, corrected, failed) block counts, FsError-or-0 per block)."""
+        count = self.numOfBlocks() - first if count is None else count
+        _, err = self.readBlocks(first, count)
+        failed = int(np.count_nonzero(err))
+        return (count - failed, 0, failed), err
+
     def writeBlocks(self, first: int, payloads: np.ndarray) -> np.ndarray:
         err = np.zeros(len(payloads), dtype=np.uint8)
         for i, p in enumerate(payloads):
@@ -317,6 +326,40 @@ class _EngineDevice(IBlockDevice):
                 i += 1
             done += i
         return out, err
+
+    def scrub(self, first: int = 0, count: Optional[int] = None) -> Tuple[Tuple[int, int, int], np.ndarray]:
+        """Whole-image scrub in one engine call (EccEngine.scrub_host): the disk
+        image from block `first` to the disk end goes through ppfs_ecc_scrub_host, which applies
+        the reference's read-path write-back block by block in index order (RS codeword incl.
+        bytes past a shortened block, Hamming flipped byte); corrected blocks are logged in order.
+        Returns ((ok, corrected, failed) block counts, FsError-or-0 per block)."""
+        n_all = self.numOfBlocks()
+        count = n_all - first if count is None else count
+        base = first * self._raw
+        r = self._disk.read(base, self._disk.size() - base) if 0 <= first and first + count <= n_all else None
+        if not r:
+            log0 = self._log_count()
+            _, err = self.readBlocks(first, count)  # blocks off the disk: per-block semantics
+            failed = int(np.count_nonzero(err))
+            corrected = self._log_count() - log0
+            return (count - failed - corrected, corrected, failed), err
+        image = np.frombuffer(r.value(), dtype=np.uint8).copy()
+        before = image.copy()
+        status = np.zeros(count, dtype=np.uint8)
+        counts = self._engine.scrub_host(image, nblocks=count, status=status)
+        err = np.where(status == STATUS_CORRECTION_ERROR, int(FsError.BlockDevice_CorrectionError), 0).astype(np.uint8)
+        for i in np.nonzero(status == STATUS_CORRECTED)[0]:
+            self._log(first + int(i))
+        changed = np.nonzero(image != before)[0]
+        if changed.size:
+            lo, hi = int(changed[0]), int(changed[-1]) + 1
+            w = self._disk.write(base + lo, image[lo:hi].tobytes())
+            if not w:
+                err[:] = int(w.error())
+        return counts, err
+
+    def _log_count(self) -> int:
+        return len(self._logger.corrections) if self._logger is not None else 0
 
     def writeBlocks(self, first: int, payloads: np.ndarray) -> np.ndarray:
         """== writeBlock(payload_i, DataLocation(first+i, 0)) in order (full-block writes)."""

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -47,6 +48,8 @@ hipError_t ppfs_ham_decode(uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, int
 hipError_t ppfs_parity_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs,
     hipStream_t s);
 hipError_t ppfs_parity_check(const uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, uint32_t bs, hipStream_t s);
+hipError_t ppfs_vote3_launch(const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* out, uint64_t rec_bytes,
+    uint64_t nrec, uint32_t* damaged, hipStream_t s);
 }
 
 namespace {
@@ -844,4 +847,171 @@ extern "C" int ppfs_ecc_decode_host(ppfs_ecc_ctx* c, uint8_t* raw, uint8_t* data
 extern "C" int ppfs_ecc_write_host(ppfs_ecc_ctx* c, const uint8_t* data, uint8_t* raw, uint8_t* status, size_t nblocks)
 {
     return host_run(c, OP_WRITE, data, nullptr, raw, status, nullptr, nblocks, 0);
+}
+
+// ---------------------------------------------------------------------------------------
+// Whole-image scrub: the effect of readBlock(i) for i = 0..nblocks-1 in order on
+// a disk image of image_bytes bytes, without the payloads: RS writes back the corrected
+// codeword (rs_block_device.cpp:175-180), Hamming the flipped byte (hamming_block_device.cpp:
+// 41-51), CRC and parity only check.  Blocks are independent except in one case: a shortened RS
+// code (n < 255) whose miscorrection lands at a position >= n writes those bytes past the block
+// end -- into the next block(s), which the sequential reference then reads modified, or off
+// the image, in which case HeapDisk::write (heap_disk.cpp:21-27) rejects the whole write-back.
+// Scrub reproduces that: one batch pass without write-back finds the spilling blocks (their
+// spill record), and the image is then processed in runs between them.
+// ---------------------------------------------------------------------------------------
+namespace {
+struct ScrubOps { // decode a block range of the image; copy spill bytes into the image
+    std::function<int(size_t b0, size_t nb, int wb, uint8_t* st, uint8_t* spill)> decode;
+    std::function<int(size_t addr, const uint8_t* src, size_t n)> put;
+};
+
+int scrub_run(const ppfs_ecc_ctx* c, size_t image_bytes, size_t nblocks, uint8_t* st, const ScrubOps& ops)
+{
+    const bool wb = c->p.ecc_type == PPFS_ECC_REED_SOLOMON || c->p.ecc_type == PPFS_ECC_HAMMING;
+    if (!(c->p.ecc_type == PPFS_ECC_REED_SOLOMON && c->rs_n < 255))
+        return ops.decode(0, nblocks, wb ? 1 : 0, st, nullptr);
+    const size_t n = c->raw, sb = 256 - n;
+    std::vector<uint8_t> spill(nblocks * sb);
+    int r = ops.decode(0, nblocks, 0, st, spill.data()); // status + spill records, image untouched
+    if (r)
+        return r;
+    size_t start = 0;
+    for (size_t i = 0; i < nblocks; ++i) {
+        const size_t extra = spill[i * sb];
+        if (!extra)
+            continue;
+        if (i > start && (r = ops.decode(start, i - start, 1, st + start, nullptr)))
+            return r;
+        const size_t end = (i + 1) * n + extra; // the write-back covers [i n, end)
+        if (end <= image_bytes) {
+            if ((r = ops.decode(i, 1, 1, st + i, nullptr)) || (r = ops.put((i + 1) * n, &spill[i * sb + 1], extra)))
+                return r;
+            const size_t j = std::min(nblocks - 1, (end - 1) / n); // last block the spill touched
+            if (j > i && (r = ops.decode(i + 1, j - i, 0, st + i + 1, &spill[(i + 1) * sb])))
+                return r;
+        } // else the reference's disk write fails and nothing of block i is written back
+        start = i + 1;
+    }
+    return start < nblocks ? ops.decode(start, nblocks - start, 1, st + start, nullptr) : 0;
+}
+
+void scrub_counts(const uint8_t* st, size_t nblocks, size_t* counts)
+{
+    if (!counts)
+        return;
+    counts[0] = counts[1] = counts[2] = 0;
+    for (size_t i = 0; i < nblocks; ++i)
+        counts[st[i] == PPFS_ECC_OK ? 0 : (st[i] == PPFS_ECC_CORRECTED ? 1 : 2)]++;
+}
+} // namespace
+
+extern "C" int ppfs_ecc_scrub_host(ppfs_ecc_ctx* c, uint8_t* image, size_t image_bytes, size_t nblocks,
+    uint8_t* status, size_t* counts)
+{
+    if (!c || (nblocks && !image) || image_bytes < nblocks * (size_t)c->raw)
+        return fail(PPFS_ECC_EINVAL, "scrub: bad argument");
+    std::vector<uint8_t> st_local;
+    if (!status) {
+        st_local.resize(nblocks);
+        status = st_local.data();
+    }
+    const size_t n = c->raw;
+    ScrubOps ops;
+    ops.decode = [&](size_t b0, size_t nb, int wb, uint8_t* st, uint8_t* spill) {
+        return ppfs_ecc_decode_host(c, image + b0 * n, nullptr, st, nb, wb, spill);
+    };
+    ops.put = [&](size_t addr, const uint8_t* src, size_t len) {
+        std::memcpy(image + addr, src, len);
+        return 0;
+    };
+    const int r = scrub_run(c, image_bytes, nblocks, status, ops);
+    if (r)
+        return r;
+    scrub_counts(status, nblocks, counts);
+    return 0;
+}
+
+extern "C" int ppfs_ecc_scrub_device(ppfs_ecc_ctx* c, uint8_t* d_image, size_t image_bytes, size_t nblocks,
+    uint8_t* d_status, void* stream)
+{
+    if (!c || (nblocks && !d_image) || image_bytes < nblocks * (size_t)c->raw)
+        return fail(PPFS_ECC_EINVAL, "scrub: bad argument");
+    hipStream_t s = (hipStream_t)stream;
+    const size_t n = c->raw, sb = 256 - std::min<size_t>(n, 255);
+    const bool chain = c->p.ecc_type == PPFS_ECC_REED_SOLOMON && c->rs_n < 255;
+    uint8_t* d_spill = nullptr;
+    if (chain) {
+        HIP_TRY(hipMallocAsync((void**)&d_spill, nblocks * sb, s), "scrub spill alloc");
+    }
+    ScrubOps ops;
+    ops.decode = [&](size_t b0, size_t nb, int wb, uint8_t* st_host, uint8_t* spill_host) {
+        uint8_t* st = d_status ? d_status + b0 : nullptr;
+        (void)st_host;
+        int r = ppfs_ecc_decode_device(c, d_image + b0 * n, nullptr, st, nb, wb, spill_host ? d_spill + b0 * sb : nullptr,
+            stream);
+        if (r || !spill_host)
+            return r;
+        HIP_TRY(hipMemcpyAsync(spill_host, d_spill + b0 * sb, nb * sb, hipMemcpyDeviceToHost, s), "scrub spill D2H");
+        HIP_TRY(hipStreamSynchronize(s), "scrub sync");
+        return 0;
+    };
+    ops.put = [&](size_t addr, const uint8_t* src, size_t len) {
+        HIP_TRY(hipMemcpyAsync(d_image + addr, src, len, hipMemcpyHostToDevice, s), "scrub spill H2D");
+        HIP_TRY(hipStreamSynchronize(s), "scrub sync"); // src is a host vector that goes away
+        return 0;
+    };
+    // status bytes live on the device; scrub_run only indexes st (never reads it)
+    std::vector<uint8_t> dummy(chain ? nblocks : 0);
+    const int r = scrub_run(c, image_bytes, nblocks, dummy.data(), ops);
+    if (d_spill)
+        (void)hipFreeAsync(d_spill, s);
+    return r;
+}
+
+// ---------------------------------------------------------------------------------------
+// 2-of-3 bitwise voting of replicated records (vote.hip)
+// ---------------------------------------------------------------------------------------
+extern "C" int ppfs_vote3_device(const uint8_t* d_a, const uint8_t* d_b, const uint8_t* d_c, uint8_t* d_out,
+    size_t rec_bytes, size_t nrec, uint32_t* d_damaged, void* stream)
+{
+    if ((nrec && rec_bytes && (!d_a || !d_b || !d_c || !d_out)))
+        return fail(PPFS_ECC_EINVAL, "vote3: null argument");
+    if (nrec && !rec_bytes)
+        return fail(PPFS_ECC_EINVAL, "vote3: zero record size");
+    return check_hip(ppfs_vote3_launch(d_a, d_b, d_c, d_out, rec_bytes, nrec, d_damaged, (hipStream_t)stream), "vote3");
+}
+
+extern "C" int ppfs_vote3_host(int device, const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* out,
+    size_t rec_bytes, size_t nrec, uint32_t* damaged)
+{
+    if (nrec && (!rec_bytes || !a || !b || !c || !out))
+        return fail(PPFS_ECC_EINVAL, "vote3: bad argument");
+    const size_t nbytes = rec_bytes * nrec;
+    if (nbytes == 0) {
+        if (damaged)
+            std::memset(damaged, 0, nrec * sizeof(uint32_t));
+        return 0;
+    }
+    HIP_TRY(hipSetDevice(device), "set device");
+    uint8_t* d = nullptr;
+    const size_t dmg_off = (4 * nbytes + 255) & ~(size_t)255;
+    HIP_TRY(hipMalloc(&d, dmg_off + nrec * sizeof(uint32_t)), "vote3 alloc");
+    int r = 0;
+    hipError_t e = hipMemcpy(d, a, nbytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(d + nbytes, b, nbytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemcpy(d + 2 * nbytes, c, nbytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = ppfs_vote3_launch(d, d + nbytes, d + 2 * nbytes, d + 3 * nbytes, rec_bytes, nrec,
+            damaged ? (uint32_t*)(d + dmg_off) : nullptr, nullptr);
+    if (e == hipSuccess)
+        e = hipMemcpy(out, d + 3 * nbytes, nbytes, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && damaged)
+        e = hipMemcpy(damaged, d + dmg_off, nrec * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    if (e != hipSuccess)
+        r = fail(PPFS_ECC_EHIP, "vote3", e);
+    (void)hipFree(d);
+    return r;
 }

@@ -1,0 +1,46 @@
+// vote.hip -- 2-of-3 bitwise majority of replicated records.
+//
+// Reference: SuperBlockManager::_performBitVoting, lib/super_block_manager/src/
+// super_block_manager.cpp:133-165: for every bit of the record, majority = (b1 + b2 + b3 >= 2);
+// copy k is "damaged" when any of its bits differs from the majority.  PPFS votes over the three
+// SuperBlock copies at mount; the batched form here votes nrec records at once (any record size),
+// one thread per byte: out = (a & b) | (a & c) | (b & c) as one v_bitop3, and a record's damage
+// bits are set with one atomic OR only where a byte disagrees.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ppfs {
+
+__global__ __launch_bounds__(256) void vote3_kernel(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b,
+    const uint8_t* __restrict__ c, uint8_t* __restrict__ out, uint64_t rec_bytes, uint64_t nbytes,
+    uint32_t* __restrict__ damaged)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nbytes; i += stride) {
+        const uint32_t x = a[i], y = b[i], z = c[i];
+        const uint32_t m = __builtin_amdgcn_bitop3_b32(x, y, z, 0xE8); // majority
+        out[i] = (uint8_t)m;
+        const uint32_t bad = (x != m ? 1u : 0u) | (y != m ? 2u : 0u) | (z != m ? 4u : 0u);
+        if (bad && damaged)
+            atomicOr(&damaged[i / rec_bytes], bad);
+    }
+}
+
+} // namespace ppfs
+
+extern "C" hipError_t ppfs_vote3_launch(const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* out,
+    uint64_t rec_bytes, uint64_t nrec, uint32_t* damaged, hipStream_t s)
+{
+    const uint64_t nbytes = rec_bytes * nrec;
+    if (damaged) {
+        const hipError_t e = hipMemsetAsync(damaged, 0, nrec * sizeof(uint32_t), s);
+        if (e != hipSuccess)
+            return e;
+    }
+    if (nbytes == 0)
+        return hipSuccess;
+    const uint64_t want = (nbytes + 255) / 256;
+    const uint32_t grid = (uint32_t)(want < 4096 ? want : 4096);
+    hipLaunchKernelGGL(ppfs::vote3_kernel, dim3(grid), dim3(256), 0, s, a, b, c, out, rec_bytes, nbytes, damaged);
+    return hipGetLastError();
+}

@@ -101,10 +101,48 @@ class EccEngine:
     def spill_bytes_per_block(self) -> int:
         return 256 - min(self.raw_block_size, 255)
 
+    # ---------------- whole-image scrub ----------------
+    def scrub_host(self, image: np.ndarray, nblocks: Optional[int] = None, status: Optional[np.ndarray] = None):
+        """readBlock(i) for every block of a host image, in order, for its write-back effect only
+        (include/ppfs_ecc.h ppfs_ecc_scrub_host).  Returns (ok, corrected, failed) block counts."""
+        n = nblocks if nblocks is not None else image.size // self.raw_block_size
+        counts = (ctypes.c_size_t * 3)()
+        check(lib().ppfs_ecc_scrub_host(self._h, _ptr(image), image.size, n, _ptr(status), counts))
+        return int(counts[0]), int(counts[1]), int(counts[2])
+
+    def scrub(self, image, status=None, nblocks: Optional[int] = None, stream=None) -> None:
+        """Device-resident scrub of a torch uint8 image (ppfs_ecc_scrub_device)."""
+        n = nblocks if nblocks is not None else image.numel() // self.raw_block_size
+        check(lib().ppfs_ecc_scrub_device(self._h, _ptr(image), image.numel(), n, _ptr(status),
+                                          _stream_handle(stream)))
+
+
+def vote3_host(a: np.ndarray, b: np.ndarray, c: np.ndarray, rec_bytes: Optional[int] = None, device: int = 0):
+    """2-of-3 bitwise majority of replicated records (SuperBlockManager::_performBitVoting,
+    super_block_manager.cpp:133-165) on the GPU.  Returns (voted bytes, per-record damage bits:
+    bit k = copy k+1 differs from the majority)."""
+    a, b, c = (np.ascontiguousarray(x, dtype=np.uint8).reshape(-1) for x in (a, b, c))
+    if not (a.size == b.size == c.size):
+        raise ValueError("vote3: copies differ in size")
+    rb = int(rec_bytes) if rec_bytes is not None else a.size
+    nrec = a.size // rb if rb else 0
+    out = np.empty_like(a)
+    dmg = np.zeros(nrec, dtype=np.uint32)
+    check(lib().ppfs_vote3_host(int(device), _ptr(a), _ptr(b), _ptr(c), _ptr(out), rb, nrec, dmg.ctypes.data))
+    return out, dmg
+
+
+def vote3(a, b, c, out, rec_bytes: int, damaged=None, stream=None) -> None:
+    """Device-resident vote3 over torch uint8 tensors; damaged: int32 tensor of nrec (or None)."""
+    nrec = a.numel() // rec_bytes
+    dptr = None if damaged is None else damaged.data_ptr()
+    check(lib().ppfs_vote3_device(_ptr(a), _ptr(b), _ptr(c), _ptr(out), rec_bytes, nrec, dptr,
+                                  _stream_handle(stream)))
+
 
 def crc_implicit_to_explicit(p: int) -> int:
     """CrcPolynomial::MsgImplicit (crc_polynomial.cpp:41-54) -> explicit form."""
     return int(lib().ppfs_ecc_crc_implicit_to_explicit(ctypes.c_uint64(p)))
 
 
-__all__ = ["EccEngine", "crc_implicit_to_explicit", "_native"]
+__all__ = ["EccEngine", "crc_implicit_to_explicit", "vote3", "vote3_host", "_native"]

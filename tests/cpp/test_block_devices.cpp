@@ -4,7 +4,7 @@
 //   unit_tests/test_rs_block_device.cpp, test_crc_block_device.cpp (device tests),
 //   test_hamming_block_device.cpp, test_parity_block_device.cpp, test_stack_disk.cpp.
 // Part 2 is differential: random sequences of formatBlock / writeBlock (any offset and length)
-// / readBlock / readBlocks / writeBlocks / raw corruption applied to the adapter and to the
+// / readBlock / readBlocks / writeBlocks / scrub / raw corruption applied to the adapter and to the
 // oracle's device model (oracle/ppfs_oracle.c oracle_dev_*, the reference's per-block
 // semantics restated in C; TEST INFRASTRUCTURE ONLY), comparing every return value, every
 // payload, the correction log and the whole disk image after each operation.
@@ -370,7 +370,7 @@ static void differential(const Cfg& c, uint64_t seed, int nops)
     }
     std::vector<uint8_t> buf(NB * 4096), obuf(NB * 4096);
     for (int op = 0; op < nops; ++op) {
-        const int kind = (int)rnd(8);
+        const int kind = (int)rnd(9);
         const int b = (int)rnd(NB + 1); // NB: past the used range (still on the disk)
         if (kind == 0) { // formatBlock
             auto r = dev->formatBlock((unsigned)b);
@@ -429,6 +429,21 @@ static void differential(const Cfg& c, uint64_t seed, int nops)
                 if (orr == 0)
                     EXPECT_TRUE(std::memcmp(buf.data() + i * ds, obuf.data(), ds) == 0);
             }
+        } else if (kind == 8) { // scrub == per-block readBlock loop, payloads dropped
+            const size_t first = rnd(NB), cnt = 1 + rnd(NB - first);
+            std::vector<uint8_t> err(cnt);
+            size_t counts[3] = { 0, 0, 0 };
+            auto r = dev->scrub((block_index_t)first, cnt, counts, err.data());
+            EXPECT_TRUE(r.has_value());
+            size_t failed = 0;
+            for (size_t i = 0; i < cnt; ++i) {
+                size_t olen = 0;
+                int orr = oracle_dev_read(od, (int)(first + i), 0, ds, 4096, obuf.data(), &olen);
+                EXPECT_EQ((int)err[i], orr);
+                failed += orr != 0;
+            }
+            EXPECT_EQ(counts[0] + counts[1] + counts[2], cnt);
+            EXPECT_EQ(counts[2], failed);
         } else { // writeBlocks == per-block writeBlock loop
             const size_t first = rnd(NB), cnt = 1 + rnd(NB - first);
             for (size_t i = 0; i < cnt * ds; ++i)

@@ -54,6 +54,8 @@ class Oracle:
         L.oracle_hamming_decode.argtypes = [c_int, vp, vp, vp, vp, vp, c_size_t]
         L.oracle_parity_encode.argtypes = [c_int, vp, vp, c_size_t]
         L.oracle_parity_check.argtypes = [c_int, vp, vp, vp, c_size_t]
+        L.oracle_vote3.restype = None
+        L.oracle_vote3.argtypes = [vp, vp, vp, vp, c_size_t, c_size_t, vp]
         L.oracle_dev_create.restype = vp
         L.oracle_dev_create.argtypes = [c_int, c_int, c_int, c_uint64, vp, c_size_t, vp, c_size_t]
         L.oracle_dev_destroy.argtypes = [vp]
@@ -176,6 +178,18 @@ class Oracle:
         st = np.zeros(nb, np.uint8)
         self.L.oracle_parity_check(bs, _p(raw), _p(data), _p(st), nb)
         return data, st
+
+
+def _vote3(self, a, b, c, rec_bytes):
+    a, b, c = (np.ascontiguousarray(x, np.uint8).reshape(-1) for x in (a, b, c))
+    nrec = a.size // rec_bytes
+    out = np.zeros(a.size, np.uint8)
+    dmg = np.zeros(nrec, np.uint32)
+    self.L.oracle_vote3(_p(a), _p(b), _p(c), _p(out), rec_bytes, nrec, _p(dmg))
+    return out, dmg
+
+
+Oracle.vote3 = _vote3
 
 
 class OracleDevice:

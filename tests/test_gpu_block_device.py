@@ -4,7 +4,8 @@
    test_crc_block_device.cpp:73-200, test_hamming_block_device.cpp, test_parity_block_device.cpp).
 2. Differential sequences vs the oracle's device model (tests/oracle_lib.OracleDevice): random
    formatBlock / writeBlock (any offset, length) / readBlock (any capacity) / readBlocks /
-   writeBlocks / raw corruption; every return value, payload, the log and the disk image must match.
+   writeBlocks / scrub / raw corruption; every return value, payload, the log and the disk image
+   must match.
 """
 import zlib
 
@@ -117,7 +118,7 @@ def test_block_device_differential(oracle, name, typ, bs, t, poly):
         return np.array_equal(disk.buf, od.disk) and [x[1] for x in log.corrections] == od.log_entries()
 
     for op in range(70):
-        kind = int(rng.integers(0, 8))
+        kind = int(rng.integers(0, 9))
         b = int(rng.integers(0, NB + 1))
         if kind == 0:
             assert bool(dev.formatBlock(b)) == (od.format(b) == 0)
@@ -160,6 +161,13 @@ def test_block_device_differential(oracle, name, typ, bs, t, poly):
                 assert int(err[i]) == rc
                 if rc == 0:
                     assert out[i].tobytes() == o
+        elif kind == 8:
+            first = int(rng.integers(0, NB))
+            cnt = int(rng.integers(1, NB - first + 1))
+            _, err = dev.scrub(first, cnt)
+            for i in range(cnt):
+                rc, _ = od.read(first + i, 0, ds, 4096)
+                assert int(err[i]) == rc
         else:
             first = int(rng.integers(0, NB))
             cnt = int(rng.integers(1, NB - first + 1))
