@@ -223,7 +223,7 @@ template <int T2> std::vector<uint8_t> build_rs_wg_tables_t()
 }
 
 // tables of the column-split RS path, 8 < 2t <= 32 (layout: rs_layout.hpp RsColLayout)
-std::vector<uint8_t> build_rs_col_tables(int t2)
+[[maybe_unused]] std::vector<uint8_t> build_rs_col_tables(int t2)
 {
     const GfHost& G = gf();
     std::vector<uint8_t> out((size_t)ppfs::rs_col_table_bytes(), 0);
@@ -246,10 +246,39 @@ std::vector<uint8_t> build_rs_col_tables(int t2)
     return out;
 }
 
+// tables of the pair RS path, 16 < 2t <= 32 (layout: rs_layout.hpp RsPairLayout)
+std::vector<uint8_t> build_rs_pair_tables(int t2)
+{
+    const GfHost& G = gf();
+    std::vector<uint8_t> out((size_t)ppfs::rs_pair_table_bytes(), 0);
+    const std::vector<uint8_t> g = rs_generator(t2);
+    for (int i = 0; i < 8; ++i) {
+        const std::vector<uint8_t> xi = rs_xpow_mod(t2 + i, g, t2);
+        for (int h = 0; h < 2; ++h)
+            for (int v = 0; v < 16; ++v) {
+                uint8_t entry[32] = { 0 };
+                for (int q = 0; q < t2; ++q)
+                    entry[32 - t2 + q] = G.mul((uint8_t)(v << (4 * h)), xi[q]);
+                for (int c = 0; c < 2; ++c)
+                    std::memcpy(&out[(size_t)(2 * i + h) * 512 + (size_t)c * 256 + (size_t)v * 16], entry + 16 * c, 16);
+            }
+    }
+    build_gf_block(out.data() + 16 * 512);
+    uint8_t* xp = out.data() + 16 * 512 + 1024;
+    std::memset(xp, 0xFF, 255 * 32);
+    for (int p = 0; p < 255; ++p) {
+        const std::vector<uint8_t> xr = rs_xpow_mod(p + t2, g, t2);
+        for (int q = 0; q < t2; ++q)
+            if (xr[q])
+                xp[p * 32 + (32 - t2 + q)] = G.log[xr[q]];
+    }
+    return out;
+}
+
 std::vector<uint8_t> build_rs_fast_tables(int t2)
 {
     if (t2 > 16)
-        return build_rs_col_tables(t2);
+        return build_rs_pair_tables(t2);
     switch (t2) {
     case 2:
         return build_rs_wg_tables_t<2>();
@@ -434,7 +463,7 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
         tables.resize(4096 + 8192 + 1024, 0);
         if (c->rs_fast) {
             tables = build_rs_fast_tables(c->rs_t2);
-            c->kname = c->rs_t2 <= 8 ? "rs255-wg-seg4-lds" : (c->rs_t2 <= 16 ? "rs255-slice8-lds" : "rs255-col4-byte-lds");
+            c->kname = c->rs_t2 <= 8 ? "rs255-wg-seg4-lds" : (c->rs_t2 <= 16 ? "rs255-slice8-lds" : "rs255-pair-nibble-lds");
         } else {
             tables.assign(1024 + 256, 0);
             build_gf_block(tables.data());

@@ -112,18 +112,28 @@ __device__ __forceinline__ void col_remainder(uint32_t& lo_out, uint32_t& hi_out
     hi_out = hi;
 }
 
-// 16 bytes at any LDS byte address
+// 16 bytes at any LDS byte address, from the two aligned 16-byte pieces that cover them.
+// Emission lanes read consecutive 16-byte pieces: as ds_read_b128 a 16-lane group then covers
+// the 64 banks exactly, where five ds_read_b32 per lane (lane stride 4 dwords) hit each bank
+// 4 times per 32-lane group.  The per-lane dword offset is selected with two v_bfi levels.
 __device__ __forceinline__ void win16(uint32_t (&X)[4], const uint8_t* lds, uint32_t addr)
 {
-    const uint32_t* w = (const uint32_t*)(lds + (addr & ~3u));
+    const uint32_t a16 = addr & ~15u;
+    const uint4 A = *(const uint4*)(lds + a16), B = *(const uint4*)(lds + a16 + 16);
+    const uint32_t D[8] = { A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w };
     const uint32_t sh = (addr & 3u) * 8u;
-    uint32_t d[5];
+    // masks, not selects: LLVM folds a select between array elements into a dynamic index (scratch)
+    const uint32_t m2 = 0u - ((addr >> 3) & 1u), m1 = 0u - ((addr >> 2) & 1u);
+    uint32_t F[6], E[5];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+        F[i] = bfi(m2, D[i + 2], D[i]);
 #pragma unroll
     for (int i = 0; i < 5; ++i)
-        d[i] = w[i];
+        E[i] = bfi(m1, F[i + 1], F[i]);
 #pragma unroll
     for (int m = 0; m < 4; ++m)
-        X[m] = __builtin_amdgcn_alignbit(d[m + 1], d[m], sh);
+        X[m] = __builtin_amdgcn_alignbit(E[m + 1], E[m], sh);
 }
 
 __device__ __forceinline__ uint32_t mword(const M128& mk, int m)

@@ -2,6 +2,7 @@
 #include "rs_fast.hpp"
 #include "rs_wg.hpp"
 #include "rs_col.hpp"
+#include "rs_pair.hpp"
 
 #ifndef PPFS_T2
 #error "compile with -DPPFS_T2=<2t>"
@@ -50,8 +51,18 @@ static uint32_t rs_tile_grid(uint64_t nb, int wpc)
 constexpr int ENC_NBUF = 2, ENC_WPC = (4 * wg::lds_bytes<PPFS_T2, false, 2>() <= 163840) ? 4 : 3;
 constexpr int DEC_NBUF = 2, DEC_WPC = 3;
 #elif PPFS_T2 > 16
-// column-split workgroup path (16 < 2t <= 32): two workgroups per CU (LDS: byte tables + 2 tiles)
-constexpr int COL_WPC = 2;
+// pair workgroup path (16 < 2t <= 32, rs_pair.hpp): 128-thread workgroups, (WPC, NBUF) per CU.
+// Single-buffered tiles let 6 (encode) / 4 (decode) workgroups share a CU: the chains are
+// latency-bound, and more resident tiles beat the in-workgroup prefetch (measured at 2t = 32:
+// encode 270 -> 197 us, decode 241 -> 206 us vs 3 double-buffered workgroups).  The column
+// kernels of rs_col.hpp are kept for ablation.
+#ifndef PPFS_PAIR_ENC
+#define PPFS_PAIR_ENC 6, 1
+#endif
+#ifndef PPFS_PAIR_DEC
+#define PPFS_PAIR_DEC 4, 1
+#endif
+constexpr int PAIR_ENC_WPC = pair::wpc_of(PPFS_PAIR_ENC), PAIR_DEC_WPC = pair::wpc_of(PPFS_PAIR_DEC);
 #endif
 // 8 < 2t <= 16: lane-per-block kernels (rs_fast.hpp); the column path leaves half of its lanes on
 // all-zero state columns there and measured slower on decode
@@ -63,8 +74,8 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
     hipLaunchKernelGGL((wg::rs_wg_encode_kernel<PPFS_T2, ENC_NBUF, ENC_WPC>), dim3(rs_tile_grid(nb, ENC_WPC)), dim3(256),
         0, s, d, r, nb, tab);
 #elif PPFS_T2 > 16
-    hipLaunchKernelGGL((col::rs_col_encode_kernel<PPFS_T2, COL_WPC>), dim3(rs_tile_grid(nb, COL_WPC)), dim3(256), 0, s,
-        d, r, nb, tab);
+    hipLaunchKernelGGL((pair::rs_pair_encode_kernel<PPFS_T2, PPFS_PAIR_ENC>), dim3(rs_tile_grid(nb, PAIR_ENC_WPC)),
+        dim3(pair::NTHR), 0, s, d, r, nb, tab);
 #else
     hipLaunchKernelGGL(rs255_encode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, d, r, nb, tab);
 #endif
@@ -78,8 +89,8 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
     hipLaunchKernelGGL((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC>), dim3(rs_tile_grid(nb, DEC_WPC)), dim3(256),
         0, s, r, d, st, nb, tab, wb);
 #elif PPFS_T2 > 16
-    hipLaunchKernelGGL((col::rs_col_decode_kernel<PPFS_T2, COL_WPC>), dim3(rs_tile_grid(nb, COL_WPC)), dim3(256), 0, s,
-        r, d, st, nb, tab, wb);
+    hipLaunchKernelGGL((pair::rs_pair_decode_kernel<PPFS_T2, PPFS_PAIR_DEC>), dim3(rs_tile_grid(nb, PAIR_DEC_WPC)),
+        dim3(pair::NTHR), 0, s, r, d, st, nb, tab, wb);
 #else
     hipLaunchKernelGGL(rs255_decode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, r, d, st, nb, tab, wb);
 #endif

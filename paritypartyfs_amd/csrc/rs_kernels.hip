@@ -201,10 +201,10 @@ extern "C" int ppfs_rs_fast_supported(int n, int t2)
 
 // device table blob of the fast path (rs_layout.hpp): segment layout for 2t <= 8, lane-per-block
 // nibble slicing tables (4 KiB; the 1 KiB GF block is appended by the builder) for 8 < 2t <= 16,
-// column layout (byte-indexed 32-byte entries, GF block, XP rows) for 16 < 2t <= 32
+// pair layout (nibble planes of 16-byte columns, GF block, XP rows) for 16 < 2t <= 32
 extern "C" int ppfs_rs_fast_tables_bytes(int t2)
 {
-    return t2 <= 8 ? rs_wg_table_bytes(t2) : (t2 <= 16 ? 4096 : rs_col_table_bytes());
+    return t2 <= 8 ? rs_wg_table_bytes(t2) : (t2 <= 16 ? 4096 : rs_pair_table_bytes());
 }
 
 extern "C" hipError_t ppfs_rs_fast_encode(int t2, const uint8_t* d, uint8_t* r, uint64_t nb, const uint8_t* tab,

@@ -58,4 +58,22 @@ template <int T2> struct RsColLayout {
 
 constexpr int rs_col_table_bytes() { return 4 * 256 * 32 + GF_BYTES + 255 * 32; }
 
+// Pair RS path (rs_pair.hpp), 16 < 2t <= 32: the same 32-byte top-aligned state, two lanes per
+// block each holding a 16-byte column.
+//   SL   slicing-by-8, nibble-indexed: table t = 2i + h (byte i of the chunk, nibble h), column
+//        plane c: 16 entries x 16 B = bytes [16c, 16c+16) of (v << 4h) * x^(2t+i) mod g, at
+//        512 t + 256 c + 16 v (each plane is exactly the 64 LDS banks)
+//   GF   the 1 KiB EXP2 / LOG / QS block;  XP  as RsColLayout (decode only)
+template <int T2> struct RsPairLayout {
+    static_assert(T2 > 16 && T2 <= 32 && (T2 % 2) == 0, "pair RS path: 2t in (16, 32]");
+    static constexpr int N = 255, K = N - T2;
+    static constexpr int OFF_SL = 0;
+    static constexpr int OFF_GF = OFF_SL + 16 * 512;
+    static constexpr int OFF_XP = OFF_GF + GF_BYTES;
+    static constexpr int ENC_BYTES = OFF_GF;
+    static constexpr int TABLE_BYTES = OFF_XP + 255 * 32;
+};
+
+constexpr int rs_pair_table_bytes() { return 16 * 512 + GF_BYTES + 255 * 32; }
+
 } // namespace ppfs

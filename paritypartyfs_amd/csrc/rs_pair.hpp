@@ -1,0 +1,473 @@
+#pragma once
+// rs_pair.hpp -- workgroup RS(255, 255-2t) encode / decode for gfx950 with 16 < 2t <= 32
+// (cfg5: t = 16, RS(255, 223)), conflict-free LDS lookups.
+//
+// Reference semantics: lib/blockdevice/src/rs_block_device.cpp (encode :95-117, decode :119-183;
+// see rs_col.hpp / rs_wg.hpp for the line map).
+//
+// The column kernels of rs_col.hpp (four lanes per block, byte-indexed tables) are bound by LDS
+// bank conflicts: a 32-lane ds_read_b64 group holds 8 blocks whose random table entries collide
+// (PMC: 56 % of LDS cycles are conflict cycles).  This design makes every lookup conflict-free:
+//   - Two lanes per block; lane c holds the 16-byte column [16c, 16c+16) of the block's 32-byte
+//     top-aligned remainder (coefficient q at byte 32 - 2t + q).
+//   - Slicing-by-8 over NIBBLE tables whose column halves are 256-byte planes: 16 entries x 16 B
+//     = exactly the 64 LDS banks.  A ds_read_b128 is serviced in four 16-lane groups,
+//     {0-3,12-15,20-27}, {4-11,16-19,28-31} and the same +32 (MI355X_MICROARCH.md, LDS); lanes
+//     are assigned so that each group holds one column only, so all 16 lanes of a group read one
+//     plane -- distinct entries sit in distinct banks, equal entries broadcast.  Column of lane l
+//     = parity of bits 2-4 of l; the partner of lane l is lane l ^ 4 (DPP row_shl:4 / row_shr:4
+//     with bank masks).
+//   - Per 8 payload bytes: exchange the top dwords with the partner, fold the state's top 8 bytes
+//     into the chunk, shift the state 8 bytes up (column 1 takes column 0's top half), and XOR in
+//     16 table entries (one ds_read_b128 each, address = one SDWA add).
+//   - 64-block tiles, 128-thread workgroups (2 waves, 32 blocks each), 3 per CU; LDS-DMA double
+//     buffering and the emission of rs_col.hpp / rs_wg.hpp.
+//   - Decode correction per pair: S_1, S_2 and the XP-row check for a single error, else all 2t
+//     syndromes (16 per lane) and the reference's BM / roots / Forney in lane 0, out of line.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gf_common.hpp"
+#include "rs_col.hpp"
+#include "rs_fast.hpp"
+#include "rs_layout.hpp"
+#include "rs_wg.hpp"
+
+namespace ppfs {
+namespace pair {
+
+using col::col_dec_piece;
+using col::col_enc_piece;
+using col::col_fix;
+using wg::barrier_lds;
+using wg::dma16;
+using wg::lds_addr;
+using wg::st_bytes;
+using wg::st_nt;
+
+constexpr int TB = 64;    // blocks per tile
+constexpr int NTHR = 128; // threads per workgroup: 2 waves x 32 blocks x 2 lanes
+static_assert(col::PAD == 48 && col::BUF == 16464, "emission helpers assume rs_col.hpp's tile buffer");
+constexpr int PAD = col::PAD, BUF = col::BUF;
+constexpr int wpc_of(int wpc, int nbuf) { return (void)nbuf, wpc; }
+
+// value of the partner lane (lane ^ 4)
+__device__ __forceinline__ uint32_t pair_xchg(uint32_t v)
+{
+    // row_shl:4 writes banks 0 and 2 (lanes with bit 2 clear take lane + 4), row_shr:4 banks 1, 3
+    const int x = __builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xF, 0x5, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(x, (int)v, 0x114, 0xF, 0xA, false);
+}
+
+// column of a lane: one column per ds_read_b128 lane group
+__device__ __forceinline__ uint32_t lane_col(uint32_t lane) { return __builtin_popcount((lane >> 2) & 7u) & 1u; }
+// block (0..31) of a lane within its wave: lanes l and l ^ 4 share it
+__device__ __forceinline__ uint32_t lane_blk(uint32_t lane) { return ((lane >> 3) << 2) | (lane & 3u); }
+
+// base + byte K of x (one v_add_u32_sdwa)
+template <int K> __device__ __forceinline__ uint32_t add_byte(uint32_t x, uint32_t base)
+{
+    uint32_t r;
+    if constexpr (K == 0)
+        asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD"
+            : "=v"(r) : "v"(x), "v"(base));
+    else if constexpr (K == 1)
+        asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+            : "=v"(r) : "v"(x), "v"(base));
+    else if constexpr (K == 2)
+        asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD"
+            : "=v"(r) : "v"(x), "v"(base));
+    else
+        asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD"
+            : "=v"(r) : "v"(x), "v"(base));
+    return r;
+}
+
+__device__ __forceinline__ uint4 ld16(const uint8_t* lds, uint32_t addr) { return *(const uint4*)(lds + addr); }
+
+__device__ __forceinline__ void xor4(uint32_t (&a)[4], const uint4& e)
+{
+    a[0] ^= e.x;
+    a[1] ^= e.y;
+    a[2] ^= e.z;
+    a[3] ^= e.w;
+}
+
+// the 16 nibble lookups of one chunk (lo, hi): entries XORed into acc.  tb = lane's plane base
+// (SL + 256 c, offset into lds[]); table t = 2i + h sits at tb + 512 t.
+__device__ __forceinline__ void pair_lookups(uint32_t (&acc)[4], const uint8_t* lds, uint32_t tb, uint32_t lo, uint32_t hi)
+{
+    const uint32_t Ll = (lo << 4) & 0xF0F0F0F0u, Hl = lo & 0xF0F0F0F0u;
+    const uint32_t Lh = (hi << 4) & 0xF0F0F0F0u, Hh = hi & 0xF0F0F0F0u;
+    uint4 e[16];
+    e[0] = ld16(lds, add_byte<0>(Ll, tb) + 0 * 512);
+    e[1] = ld16(lds, add_byte<0>(Hl, tb) + 1 * 512);
+    e[2] = ld16(lds, add_byte<1>(Ll, tb) + 2 * 512);
+    e[3] = ld16(lds, add_byte<1>(Hl, tb) + 3 * 512);
+    e[4] = ld16(lds, add_byte<2>(Ll, tb) + 4 * 512);
+    e[5] = ld16(lds, add_byte<2>(Hl, tb) + 5 * 512);
+    e[6] = ld16(lds, add_byte<3>(Ll, tb) + 6 * 512);
+    e[7] = ld16(lds, add_byte<3>(Hl, tb) + 7 * 512);
+    e[8] = ld16(lds, add_byte<0>(Lh, tb) + 8 * 512);
+    e[9] = ld16(lds, add_byte<0>(Hh, tb) + 9 * 512);
+    e[10] = ld16(lds, add_byte<1>(Lh, tb) + 10 * 512);
+    e[11] = ld16(lds, add_byte<1>(Hh, tb) + 11 * 512);
+    e[12] = ld16(lds, add_byte<2>(Lh, tb) + 12 * 512);
+    e[13] = ld16(lds, add_byte<2>(Hh, tb) + 13 * 512);
+    e[14] = ld16(lds, add_byte<3>(Lh, tb) + 14 * 512);
+    e[15] = ld16(lds, add_byte<3>(Hh, tb) + 15 * 512);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        auto w = [&](int i) -> uint32_t { return q == 0 ? e[i].x : q == 1 ? e[i].y : q == 2 ? e[i].z : e[i].w; };
+        uint32_t a = xor3(acc[q], w(0), w(1));
+        a = xor3(a, w(2), w(3));
+        a = xor3(a, w(4), w(5));
+        a = xor3(a, w(6), w(7));
+        a = xor3(a, w(8), w(9));
+        a = xor3(a, w(10), w(11));
+        a = xor3(a, w(12), w(13));
+        acc[q] = xor3(a, w(14), w(15));
+    }
+}
+
+// Remainder column c of a LEN-byte row at LDS byte `row` (s = state bytes [16c, 16c+16)).
+template <int LEN>
+__device__ __forceinline__ void pair_remainder(uint32_t (&s)[4], const uint8_t* lds, uint32_t row, uint32_t tb, uint32_t c)
+{
+    constexpr int NC = (LEN + 7) / 8;
+    constexpr int TOPN = LEN - 8 * (NC - 1);
+    const uint32_t sh = (row & 3u) * 8u;
+    const uint32_t* w = (const uint32_t*)(lds + (row & ~3u));
+    const uint32_t cm = c ? ~0u : 0u;
+    uint32_t up = w[2 * NC];
+#pragma unroll
+    for (int j = NC - 1; j >= 0; --j) {
+        const uint32_t d1 = w[2 * j + 1], d0 = w[2 * j];
+        uint32_t hi = __builtin_amdgcn_alignbit(up, d1, sh); // payload bytes 8j+4 .. 8j+7
+        uint32_t lo = __builtin_amdgcn_alignbit(d1, d0, sh); // payload bytes 8j .. 8j+3
+        up = d0;
+        if (j == NC - 1) {
+            if constexpr (TOPN < 4) {
+                lo &= (1u << (8 * TOPN)) - 1u;
+                hi = 0;
+            } else if constexpr (TOPN == 4) {
+                hi = 0;
+            } else if constexpr (TOPN < 8) {
+                hi &= (1u << (8 * (TOPN - 4))) - 1u;
+            }
+            s[0] = s[1] = s[2] = s[3] = 0;
+            pair_lookups(s, lds, tb, lo, hi);
+        } else {
+            const uint32_t p2 = pair_xchg(s[2]), p3 = pair_xchg(s[3]);
+            lo ^= c ? s[2] : p2; // fold the top 8 coefficients (column 1's upper half)
+            hi ^= c ? s[3] : p3;
+            uint32_t n[4] = { p2 & cm, p3 & cm, s[0], s[1] }; // state * x^8
+            pair_lookups(n, lds, tb, lo, hi);
+            s[0] = n[0];
+            s[1] = n[1];
+            s[2] = n[2];
+            s[3] = n[3];
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t pair_or(uint32_t v) { return v | pair_xchg(v); }
+
+// General correction (2+ errors), out of line; both lanes of the pair: lane c computes S_i for
+// i = 16c+1 .. 16c+16 into the block's slot (over r', which both lanes have read), then lane 0
+// runs BM / roots / Forney (rs_fast.hpp).
+template <int T2>
+__device__ __noinline__ void pair_correct_general(uint8_t* lds, uint32_t goff, uint32_t row, uint32_t slot, uint32_t c,
+    uint8_t* __restrict__ raw_g, uint64_t gblk, bool wb)
+{
+    const Gf gf { lds + goff };
+    const uint4 r0 = *(const uint4*)(lds + slot), r1 = *(const uint4*)(lds + slot + 16);
+    const uint32_t rw[8] = { r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w };
+    wave_fence(); // both lanes hold r' before the slot is overwritten
+    uint32_t sw[4] = { 0u, 0u, 0u, 0u };
+#pragma unroll
+    for (int ii = 0; ii < 16; ++ii) {
+        const uint32_t i = 16u * c + 1u + (uint32_t)ii;
+        uint32_t e = (255u * 32u - i * (uint32_t)T2) % 255u; // i (q - 2t) mod 255 at q = 0
+        uint32_t sacc = 0;
+#pragma unroll
+        for (int q = 0; q < T2; ++q) {
+            constexpr int P0 = 32 - T2;
+            const uint32_t rv = (rw[(P0 + q) >> 2] >> (8 * ((P0 + q) & 3))) & 0xFFu;
+            const uint32_t v = gf.exp(gf.log(rv) + e);
+            sacc ^= rv ? v : 0u;
+            e += i;
+            e = e >= 255u ? e - 255u : e;
+        }
+        sw[ii >> 2] |= (i <= (uint32_t)T2 ? sacc : 0u) << (8 * (ii & 3));
+    }
+    *(uint4*)(lds + slot + 16u * c) = make_uint4(sw[0], sw[1], sw[2], sw[3]);
+    wave_fence();
+    if (c == 0) {
+        uint32_t S[T2];
+        const uint4 s0 = *(const uint4*)(lds + slot), s1 = *(const uint4*)(lds + slot + 16);
+        const uint32_t sw8[8] = { s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w };
+#pragma unroll
+        for (int i = 0; i < T2; ++i)
+            S[i] = (sw8[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+        rs_correct_general<T2>(S, gf, [&](uint32_t pos, uint32_t ev) { col_fix(lds, row, raw_g, gblk, wb, pos, ev); });
+    }
+}
+
+// Decode correction for the pair's block; s = the lane's column of r' = x^2t c(x) mod g.  Single
+// error: S_1, S_2 -> X = S_2/S_1, e = S_1/X, confirmed iff r' == e * XP row LOG X (rs_col.hpp).
+template <int T2>
+__device__ __forceinline__ uint32_t pair_correct(uint8_t* lds, uint32_t goff, uint32_t xoff, uint32_t row, uint32_t slot,
+    uint32_t c, const uint32_t (&s)[4], bool valid, uint8_t* __restrict__ raw_g, uint64_t gblk, bool wb)
+{
+    const bool err = valid && pair_or(s[0] | s[1] | s[2] | s[3]) != 0u;
+    if (!__builtin_amdgcn_ballot_w64(err))
+        return 0u;
+    const Gf gf { lds + goff };
+    // state byte 16c+k is coefficient q = 16c+k-POFF; exponent i (q - 2t) = i (16c + k - 32)
+    uint32_t s1 = 0, s2 = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t rb = (s[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+        const uint32_t lb = gf.log(rb), u = 16u * c + (uint32_t)k;
+        const uint32_t v1 = gf.exp(lb + u + 223u), v2 = gf.exp(lb + 2u * u + 191u);
+        s1 ^= rb ? v1 : 0u;
+        s2 ^= rb ? v2 : 0u;
+    }
+    s1 ^= pair_xchg(s1);
+    s2 ^= pair_xchg(s2);
+    const uint32_t l1 = gf.log(s1), l2 = gf.log(s2);
+    uint32_t lx = l2 + 255u - l1;
+    lx = lx >= 255u ? lx - 255u : lx;
+    uint32_t le = l1 + 255u - lx;
+    le = le >= 255u ? le - 255u : le;
+    const uint4 xr = *(const uint4*)(lds + xoff + 32u * lx + 16u * c);
+    const uint32_t xw[4] = { xr.x, xr.y, xr.z, xr.w };
+    uint32_t bad = (s1 == 0u || s2 == 0u) ? 1u : 0u;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t x = (xw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+        const uint32_t rb = (s[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+        const uint32_t ev = x == 0xFFu ? 0u : gf.exp(le + x);
+        bad |= ev != rb ? 1u : 0u;
+    }
+    const bool geo = err && pair_or(bad) == 0u;
+    if (geo && c == 0)
+        col_fix(lds, row, raw_g, gblk, wb, lx, gf.exp(le));
+    if (err && !geo)
+        pair_correct_general<T2>(lds, goff, row, slot, c, raw_g, gblk, wb);
+    return err ? 1u : 0u;
+}
+
+// LDS-DMA of a tile by 128 threads: piece p = tid + 128 k lands at dst + 16 p.
+template <int NPIECE>
+__device__ __forceinline__ void dma_tile128(uint8_t* dst, const uint8_t* __restrict__ src, uint32_t tid)
+{
+    constexpr int K = (NPIECE + NTHR - 1) / NTHR;
+    const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(dst) + (tid & ~63u) * 16u);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint32_t p = tid + (uint32_t)NTHR * k;
+        if ((k + 1) * NTHR <= NPIECE || p < (uint32_t)NPIECE)
+            dma16(src + (size_t)p * 16, base + 16u * NTHR * k);
+    }
+}
+
+__device__ __forceinline__ void stage_bytes128(uint8_t* dst, const uint8_t* __restrict__ src, uint32_t nbytes, uint32_t tid)
+{
+    for (uint32_t i = tid; i < nbytes; i += NTHR)
+        dst[i] = src[i];
+}
+
+// LDS plan (single __shared__ array at LDS address 0): tables | remainder / syndrome slots
+// (65 x 32 B + slack) | NBUF tile buffers.  NBUF = 2: the next tile's DMA is issued at the top of
+// an iteration; NBUF = 1: after this tile's emission reads (more workgroups per CU overlap it).
+template <int T2, bool DEC, int NBUF> struct Lds {
+    using L = RsPairLayout<T2>;
+    static constexpr int TBL = DEC ? L::TABLE_BYTES : L::ENC_BYTES;
+    static constexpr int OFF_PAR = TBL;
+    static constexpr int OFF_BUF = OFF_PAR + 2080;
+    static constexpr int BYTES = OFF_BUF + NBUF * BUF;
+    static_assert(OFF_BUF % 16 == 0 && TBL % 16 == 0, "aligned buffers");
+};
+
+template <int T2, int WPC = 3, int NBUF = 2, int NTST = 1>
+__global__ __launch_bounds__(NTHR, 2) void rs_pair_encode_kernel(const uint8_t* __restrict__ data,
+    uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables)
+{
+    using L = RsPairLayout<T2>;
+    using D = Lds<T2, false, NBUF>;
+    constexpr int LDS_ALLOC = wg::lds_alloc<D::BYTES, WPC>();
+    static_assert(WPC * LDS_ALLOC <= 163840, "LDS for WPC workgroups per CU");
+    constexpr int K = L::K;
+    constexpr int IN_PIECES = TB * K / 16;
+    constexpr int OUT_PIECES = TB * 255 / 16; // 1020
+    constexpr int KOUT = (OUT_PIECES + NTHR - 1) / NTHR;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_ALLOC];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
+    const uint32_t c = lane_col(lane), blk = 32u * wave + lane_blk(lane);
+    const uint32_t tb = L::OFF_SL + 256u * c; // offset in lds[]
+    for (uint32_t p = tid; p < (uint32_t)D::TBL / 16; p += NTHR)
+        *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
+    const uint64_t nfull = nblocks / TB, ntiles = (nblocks + TB - 1) / TB;
+    uint64_t t = blockIdx.x;
+    uint32_t cur = 0;
+    if (t < nfull)
+        dma_tile128<IN_PIECES>(lds + D::OFF_BUF + PAD, data + t * (TB * K), tid);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (; t < nfull; t += gridDim.x) {
+        barrier_lds(); // A: tile t in LDS, the last tile's emission reads done
+        const uint32_t buf = D::OFF_BUF + cur * BUF;
+        const uint64_t nx = t + gridDim.x;
+        if (NBUF == 2 && nx < nfull)
+            dma_tile128<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, data + nx * (TB * K), tid);
+        uint32_t s[4];
+        pair_remainder<K>(s, lds, buf + PAD + (uint32_t)K * blk, tb, c);
+        *(uint4*)(lds + D::OFF_PAR + 32u * blk + 16u * c) = make_uint4(s[0], s[1], s[2], s[3]);
+        barrier_lds(); // B: parity slots complete
+        uint8_t* dst = raw + t * (TB * 255);
+        // opaque per iteration: keeps the pieces' loop-invariant index maths (b, off, masks) from
+        // being hoisted out of the tile loop, where it held ~150 VGPRs and starved the lookups
+        uint32_t tid_o = tid;
+        asm volatile("" : "+v"(tid_o));
+#pragma unroll
+        for (int k = 0; k < KOUT; ++k) {
+            const uint32_t p = tid_o + (uint32_t)NTHR * k;
+            const uint4 o = col_enc_piece<T2>(lds, buf, D::OFF_PAR, p);
+            if ((k + 1) * NTHR <= OUT_PIECES || p < (uint32_t)OUT_PIECES)
+                st_nt<NTST>(dst + 16u * p, o);
+        }
+        if constexpr (NBUF == 1) {
+            barrier_lds(); // every wave's emission reads done: the buffer is free
+            if (nx < nfull)
+                dma_tile128<IN_PIECES>(lds + D::OFF_BUF + PAD, data + nx * (TB * K), tid);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // other workgroups overlap this wait
+        } else {
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); // next tile's DMA landed; stores may fly
+        }
+        cur ^= (NBUF == 2) ? 1u : 0u;
+    }
+    if (t == nfull && nfull < ntiles) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier_lds();
+        const uint32_t nb = (uint32_t)(nblocks - t * TB);
+        const uint32_t buf = D::OFF_BUF + cur * BUF;
+        stage_bytes128(lds + buf + PAD, data + t * (TB * K), nb * K, tid);
+        barrier_lds();
+        uint32_t s[4];
+        pair_remainder<K>(s, lds, buf + PAD + (uint32_t)K * blk, tb, c);
+        *(uint4*)(lds + D::OFF_PAR + 32u * blk + 16u * c) = make_uint4(s[0], s[1], s[2], s[3]);
+        barrier_lds();
+        uint8_t* dst = raw + t * (TB * 255);
+        const uint32_t nout = nb * 255u;
+        for (uint32_t p = tid; 16u * p < nout; p += NTHR) {
+            const uint4 v = col_enc_piece<T2>(lds, buf, D::OFF_PAR, p);
+            if (16u * p + 16u <= nout)
+                *(uint4*)(dst + 16u * p) = v;
+            else
+                st_bytes(dst + 16u * p, v, nout - 16u * p);
+        }
+    }
+}
+
+template <int T2, int WPC = 3, int NBUF = 2, int NTST = 1>
+__global__ __launch_bounds__(NTHR, 2) void rs_pair_decode_kernel(uint8_t* __restrict__ raw,
+    uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables,
+    int write_back)
+{
+    using L = RsPairLayout<T2>;
+    using D = Lds<T2, true, NBUF>;
+    constexpr int LDS_ALLOC = wg::lds_alloc<D::BYTES, WPC>();
+    static_assert(WPC * LDS_ALLOC <= 163840, "LDS for WPC workgroups per CU");
+    constexpr int K = L::K;
+    constexpr int IN_PIECES = TB * 255 / 16; // 1020
+    constexpr int OUT_PIECES = TB * K / 16;
+    constexpr int KOUT = (OUT_PIECES + NTHR - 1) / NTHR;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_ALLOC];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
+    const uint32_t c = lane_col(lane), blk = 32u * wave + lane_blk(lane);
+    const uint32_t tb = L::OFF_SL + 256u * c; // offset in lds[]
+    const bool wb = write_back != 0, want = data != nullptr;
+    const uint32_t slot = D::OFF_PAR + 32u * blk;
+    for (uint32_t p = tid; p < (uint32_t)D::TBL / 16; p += NTHR)
+        *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
+    const uint64_t nfull = nblocks / TB, ntiles = (nblocks + TB - 1) / TB;
+    uint64_t t = blockIdx.x;
+    uint32_t cur = 0;
+    if (t < nfull)
+        dma_tile128<IN_PIECES>(lds + D::OFF_BUF + PAD, raw + t * (TB * 255), tid);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (; t < nfull; t += gridDim.x) {
+        barrier_lds(); // A
+        const uint32_t buf = D::OFF_BUF + cur * BUF;
+        const uint64_t nx = t + gridDim.x;
+        if (NBUF == 2 && nx < nfull)
+            dma_tile128<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, raw + nx * (TB * 255), tid);
+        const uint32_t row = buf + PAD + 255u * blk;
+        uint32_t s[4];
+        pair_remainder<255>(s, lds, row, tb, c);
+        *(uint4*)(lds + slot + 16u * c) = make_uint4(s[0], s[1], s[2], s[3]); // read by the general path
+        wave_fence();
+        const uint32_t st =
+            pair_correct<T2>(lds, L::OFF_GF, L::OFF_XP, row, slot, c, s, true, raw, t * TB + blk, wb);
+        if (status && c == 0)
+            status[t * TB + blk] = (uint8_t)st;
+        barrier_lds(); // C: corrections patched into the LDS rows
+        uint8_t* dst = want ? data + t * (TB * K) : nullptr;
+        uint32_t tid_o = tid; // see the encode kernel
+        asm volatile("" : "+v"(tid_o));
+        if (want) {
+#pragma unroll
+            for (int k = 0; k < KOUT; ++k) {
+                const uint32_t p = tid_o + (uint32_t)NTHR * k;
+                const uint4 o = col_dec_piece<T2>(lds, buf, p);
+                if ((k + 1) * NTHR <= OUT_PIECES || p < (uint32_t)OUT_PIECES)
+                    st_nt<NTST>(dst + 16u * p, o);
+            }
+        }
+        if constexpr (NBUF == 1) {
+            barrier_lds(); // emission reads done: the buffer is free
+            if (nx < nfull)
+                dma_tile128<IN_PIECES>(lds + D::OFF_BUF + PAD, raw + nx * (TB * 255), tid);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // other workgroups overlap this wait
+        } else if (want) {
+            asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        cur ^= (NBUF == 2) ? 1u : 0u;
+    }
+    if (t == nfull && nfull < ntiles) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier_lds();
+        const uint32_t nb = (uint32_t)(nblocks - t * TB);
+        const uint32_t buf = D::OFF_BUF + cur * BUF;
+        stage_bytes128(lds + buf + PAD, raw + t * (TB * 255), nb * 255u, tid);
+        barrier_lds();
+        const uint32_t row = buf + PAD + 255u * blk;
+        uint32_t s[4];
+        pair_remainder<255>(s, lds, row, tb, c);
+        *(uint4*)(lds + slot + 16u * c) = make_uint4(s[0], s[1], s[2], s[3]);
+        wave_fence();
+        const bool valid = blk < nb;
+        const uint32_t st =
+            pair_correct<T2>(lds, L::OFF_GF, L::OFF_XP, row, slot, c, s, valid, raw, t * TB + blk, wb);
+        if (status && valid && c == 0)
+            status[t * TB + blk] = (uint8_t)st;
+        barrier_lds();
+        if (want) {
+            uint8_t* dst = data + t * (TB * K);
+            const uint32_t nout = nb * (uint32_t)K;
+            for (uint32_t p = tid; 16u * p < nout; p += NTHR) {
+                const uint4 v = col_dec_piece<T2>(lds, buf, p);
+                if (16u * p + 16u <= nout)
+                    *(uint4*)(dst + 16u * p) = v;
+                else
+                    st_bytes(dst + 16u * p, v, nout - 16u * p);
+            }
+        }
+    }
+}
+
+} // namespace pair
+} // namespace ppfs
