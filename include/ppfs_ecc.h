@@ -121,7 +121,10 @@ int ppfs_ecc_decode_device(ppfs_ecc_ctx* ctx, uint8_t* d_raw, uint8_t* d_data, u
 int ppfs_ecc_write_device(ppfs_ecc_ctx* ctx, const uint8_t* d_data, uint8_t* d_raw, uint8_t* d_status,
     size_t nblocks, void* stream);
 
-/* Host-memory variants (pinned staging, chunked, H2D/kernel/D2H overlapped). */
+/* Host-memory variants (chunked, H2D/kernel/D2H overlapped on two streams).  Pageable caller
+ * buffers go through the context's pinned staging buffers (one CPU copy each way); when every
+ * caller buffer of the call is page-locked (hipHostMalloc, or ppfs_ecc_host_register below) the
+ * chunks are DMA'd straight between the caller's memory and the device. */
 int ppfs_ecc_encode_host(ppfs_ecc_ctx* ctx, const uint8_t* data, uint8_t* raw, size_t nblocks);
 int ppfs_ecc_decode_host(ppfs_ecc_ctx* ctx, uint8_t* raw, uint8_t* data, uint8_t* status, size_t nblocks,
     int write_back, uint8_t* spill);
@@ -159,6 +162,14 @@ int ppfs_vote3_device(const uint8_t* d_a, const uint8_t* d_b, const uint8_t* d_c
     size_t nrec, uint32_t* d_damaged, void* stream);
 int ppfs_vote3_host(int device, const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* out, size_t rec_bytes,
     size_t nrec, uint32_t* damaged);
+
+/*
+ * Page-lock / release a caller buffer (hipHostRegister), e.g. the host mirror of a disk image
+ * (replacing FileDisk's seekp + fstream I/O, lib/disk/src/file_disk.cpp:56-101,
+ * by an mmap'd or resident image the *_host calls then DMA directly).
+ */
+int ppfs_ecc_host_register(void* ptr, size_t bytes);
+int ppfs_ecc_host_unregister(void* ptr);
 
 /* Last HIP error string recorded by this thread (diagnostics). */
 const char* ppfs_ecc_last_error(void);

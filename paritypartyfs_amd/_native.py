@@ -35,6 +35,8 @@ EXPORTED_SYMBOLS = (
     "ppfs_ecc_scrub_device",
     "ppfs_vote3_device",
     "ppfs_vote3_host",
+    "ppfs_ecc_host_register",
+    "ppfs_ecc_host_unregister",
     "ppfs_ecc_last_error",
 )
 
@@ -108,6 +110,10 @@ def lib() -> ctypes.CDLL:
     L.ppfs_vote3_device.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p, c_void_p]
     L.ppfs_vote3_host.restype = c_int
     L.ppfs_vote3_host.argtypes = [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p]
+    L.ppfs_ecc_host_register.restype = c_int
+    L.ppfs_ecc_host_register.argtypes = [c_void_p, c_size_t]
+    L.ppfs_ecc_host_unregister.restype = c_int
+    L.ppfs_ecc_host_unregister.argtypes = [c_void_p]
     L.ppfs_ecc_last_error.restype = c_char_p
     L.ppfs_ecc_last_error.argtypes = []
     _ = u8p

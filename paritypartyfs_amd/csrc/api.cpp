@@ -777,6 +777,20 @@ static bool raw_is_rmw(const ppfs_ecc_ctx* c)
         || (c->p.ecc_type == PPFS_ECC_CRC && (c->crc_n % 8) != 0);
 }
 
+// page-locked host memory (hipHostMalloc / hipHostRegister, e.g. ppfs_ecc_host_register): the
+// DMA engines can reach it directly, so the host paths skip the CPU copy through staging
+static bool host_pinned(const void* p)
+{
+    if (!p)
+        return true;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
 static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t* data_out, uint8_t* raw,
     uint8_t* status, uint8_t* spill, size_t nblocks, int write_back)
 {
@@ -793,11 +807,18 @@ static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t*
     const size_t spill_b = 256 - std::min<size_t>(c->raw, 255);
     size_t pending_first[2] = { 0, 0 }, pending_n[2] = { 0, 0 };
     bool busy[2] = { false, false };
+    // every caller buffer page-locked: DMA straight between it and the device staging buffers
+    const bool direct = host_pinned(data_in) && host_pinned(data_out) && host_pinned(raw) && host_pinned(status)
+        && host_pinned(spill);
 
     auto drain = [&](int i) -> int {
         if (!busy[i])
             return 0;
         HIP_TRY(hipStreamSynchronize(c->hs[i]), "sync");
+        if (direct) {
+            busy[i] = false;
+            return 0;
+        }
         const size_t b0 = pending_first[i], nb = pending_n[i];
         uint8_t* h = c->h_pin[i];
         if (op == OP_ENCODE || op == OP_WRITE || write_back)
@@ -823,13 +844,21 @@ static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t*
         // inputs host -> pinned -> device (data and raw regions are adjacent in the layout)
         const bool need_data = op == OP_ENCODE || op == OP_WRITE;
         const bool need_raw = op != OP_ENCODE || raw_is_rmw(c);
-        if (need_data)
-            std::memcpy(h + L.data, data_in + b0 * c->data, nb * c->data);
-        if (need_raw)
-            std::memcpy(h + L.raw, raw + b0 * c->raw, nb * c->raw);
-        const size_t in_lo = need_data ? L.data : L.raw;
-        const size_t in_hi = need_raw ? L.raw + nb * c->raw : L.data + nb * c->data;
-        HIP_TRY(hipMemcpyAsync(d + in_lo, h + in_lo, in_hi - in_lo, hipMemcpyHostToDevice, s), "H2D");
+        if (direct) {
+            if (need_data)
+                HIP_TRY(hipMemcpyAsync(d + L.data, data_in + b0 * c->data, nb * c->data, hipMemcpyHostToDevice, s),
+                    "H2D data");
+            if (need_raw)
+                HIP_TRY(hipMemcpyAsync(d + L.raw, raw + b0 * c->raw, nb * c->raw, hipMemcpyHostToDevice, s), "H2D raw");
+        } else {
+            if (need_data)
+                std::memcpy(h + L.data, data_in + b0 * c->data, nb * c->data);
+            if (need_raw)
+                std::memcpy(h + L.raw, raw + b0 * c->raw, nb * c->raw);
+            const size_t in_lo = need_data ? L.data : L.raw;
+            const size_t in_hi = need_raw ? L.raw + nb * c->raw : L.data + nb * c->data;
+            HIP_TRY(hipMemcpyAsync(d + in_lo, h + in_lo, in_hi - in_lo, hipMemcpyHostToDevice, s), "H2D");
+        }
         switch (op) {
         case OP_ENCODE:
             r = ppfs_ecc_encode_device(c, d + L.data, d + L.raw, nb, s);
@@ -844,15 +873,19 @@ static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t*
         }
         if (r)
             return r;
-        // outputs device -> pinned
+        // outputs device -> pinned staging (or straight to page-locked caller buffers)
+        uint8_t* o_raw = direct ? raw + b0 * c->raw : h + L.raw;
+        uint8_t* o_data = direct ? (data_out ? data_out + b0 * c->data : nullptr) : h + L.data;
+        uint8_t* o_st = direct ? (status ? status + b0 : nullptr) : h + L.status;
+        uint8_t* o_sp = direct ? (spill ? spill + b0 * spill_b : nullptr) : h + L.spill;
         if (op == OP_ENCODE || op == OP_WRITE || write_back)
-            HIP_TRY(hipMemcpyAsync(h + L.raw, d + L.raw, nb * c->raw, hipMemcpyDeviceToHost, s), "D2H raw");
+            HIP_TRY(hipMemcpyAsync(o_raw, d + L.raw, nb * c->raw, hipMemcpyDeviceToHost, s), "D2H raw");
         if (op == OP_DECODE && data_out)
-            HIP_TRY(hipMemcpyAsync(h + L.data, d + L.data, nb * c->data, hipMemcpyDeviceToHost, s), "D2H data");
+            HIP_TRY(hipMemcpyAsync(o_data, d + L.data, nb * c->data, hipMemcpyDeviceToHost, s), "D2H data");
         if (status && (op != OP_ENCODE))
-            HIP_TRY(hipMemcpyAsync(h + L.status, d + L.status, nb, hipMemcpyDeviceToHost, s), "D2H status");
+            HIP_TRY(hipMemcpyAsync(o_st, d + L.status, nb, hipMemcpyDeviceToHost, s), "D2H status");
         if (spill)
-            HIP_TRY(hipMemcpyAsync(h + L.spill, d + L.spill, nb * spill_b, hipMemcpyDeviceToHost, s), "D2H spill");
+            HIP_TRY(hipMemcpyAsync(o_sp, d + L.spill, nb * spill_b, hipMemcpyDeviceToHost, s), "D2H spill");
         pending_first[slot] = b0;
         pending_n[slot] = nb;
         busy[slot] = true;
@@ -1043,4 +1076,23 @@ extern "C" int ppfs_vote3_host(int device, const uint8_t* a, const uint8_t* b, c
         r = fail(PPFS_ECC_EHIP, "vote3", e);
     (void)hipFree(d);
     return r;
+}
+
+// ---------------------------------------------------------------------------------------
+// Page-locking of caller memory (a pinned host mirror of the disk image)
+// ---------------------------------------------------------------------------------------
+extern "C" int ppfs_ecc_host_register(void* ptr, size_t bytes)
+{
+    if (!ptr || !bytes)
+        return fail(PPFS_ECC_EINVAL, "host_register: bad argument");
+    HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault), "hipHostRegister");
+    return 0;
+}
+
+extern "C" int ppfs_ecc_host_unregister(void* ptr)
+{
+    if (!ptr)
+        return fail(PPFS_ECC_EINVAL, "host_unregister: null pointer");
+    HIP_TRY(hipHostUnregister(ptr), "hipHostUnregister");
+    return 0;
 }

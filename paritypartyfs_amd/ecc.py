@@ -117,6 +117,31 @@ class EccEngine:
                                           _stream_handle(stream)))
 
 
+class pinned:
+    """Page-lock numpy arrays for the duration of a `with` block (ppfs_ecc_host_register): the
+    *_host calls then DMA them directly instead of copying through staging buffers."""
+
+    def __init__(self, *arrays: np.ndarray):
+        self._arrays = [a for a in arrays if a is not None and a.nbytes]
+
+    def __enter__(self):
+        done = []
+        try:
+            for a in self._arrays:
+                check(lib().ppfs_ecc_host_register(_ptr(a), a.nbytes))
+                done.append(a)
+        except Exception:
+            for a in done:
+                lib().ppfs_ecc_host_unregister(_ptr(a))
+            raise
+        return self
+
+    def __exit__(self, *exc):
+        for a in self._arrays:
+            check(lib().ppfs_ecc_host_unregister(_ptr(a)))
+        return False
+
+
 def vote3_host(a: np.ndarray, b: np.ndarray, c: np.ndarray, rec_bytes: Optional[int] = None, device: int = 0):
     """2-of-3 bitwise majority of replicated records (SuperBlockManager::_performBitVoting,
     super_block_manager.cpp:133-165) on the GPU.  Returns (voted bytes, per-record damage bits:
@@ -145,4 +170,4 @@ def crc_implicit_to_explicit(p: int) -> int:
     return int(lib().ppfs_ecc_crc_implicit_to_explicit(ctypes.c_uint64(p)))
 
 
-__all__ = ["EccEngine", "crc_implicit_to_explicit", "vote3", "vote3_host", "_native"]
+__all__ = ["EccEngine", "crc_implicit_to_explicit", "pinned", "vote3", "vote3_host", "_native"]

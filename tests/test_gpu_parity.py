@@ -126,7 +126,7 @@ def inject_rs_fast(rng, cw, n, t, nblocks):
 def test_rs_many_tiles_per_workgroup(oracle, bs, t):
     """Batches past one resident grid (2-4 workgroups/CU x 256 CUs x 64 blocks): every workgroup
     walks several tiles, so the double-buffered prefetch of the next tile and the ragged last tile
-    run (segment kernels for 2t <= 8, column kernels for 2t > 8)."""
+    run (segment kernels for 2t <= 8, lane-per-block for 8 < 2t <= 16, pair kernels above)."""
     n, k, _ = oracle.rs_sizes(bs, t)
     nb = 3 * 768 * 64 + 37
     eng = EccEngine(ECC_REED_SOLOMON, bs, t)
@@ -401,3 +401,40 @@ def test_host_path_multichunk(oracle):
     assert (st == 1).all()
     assert np.array_equal(out, data)
     assert np.array_equal(bad, raw)
+
+
+@pytest.mark.parametrize("typ,bs,t,poly", [(ECC_REED_SOLOMON, 512, 3, 0), (ECC_REED_SOLOMON, 64, 3, 0),
+                                           (ECC_HAMMING, 4096, 0, 0), (ECC_CRC, 4096, 0, (0x9960034C << 1) + 1)],
+                         ids=["rs512", "rs64", "ham4096", "crc4096"])
+def test_host_path_pinned_equals_pageable(typ, bs, t, poly):
+    """Page-locked caller buffers (ppfs_ecc_host_register) take the direct-DMA path of the host
+    calls; results must be byte-identical to the staged (pageable) path, across chunks."""
+    from paritypartyfs_amd import pinned
+
+    eng = EccEngine(typ, bs, t, crc_polynomial_explicit=poly)
+    n, k = eng.raw_block_size, eng.data_size
+    nb = 70001 if bs <= 512 else 3001
+    rng = rng_for("pin", bs)
+    data = rng.integers(0, 256, nb * k, dtype=np.uint8)
+    outs = []
+    for kind in ("pageable", "pinned"):
+        raw = np.zeros(nb * n, np.uint8)
+        d = data.copy()
+        out = np.zeros(nb * k, np.uint8)
+        st = np.full(nb, 77, np.uint8)
+        sp = np.zeros(nb * eng.spill_bytes_per_block(), np.uint8)
+        ctx = pinned(d, raw, out, st, sp) if kind == "pinned" else None
+        if ctx:
+            ctx.__enter__()
+        try:
+            eng.encode_host(d, raw)
+            r2 = np.random.default_rng(5)
+            pos = r2.integers(0, n, nb) + np.arange(nb) * n
+            raw[pos] ^= r2.integers(1, 256, nb, dtype=np.uint8)
+            eng.decode_host(raw, out, st, write_back=True, spill=sp if bs < 255 else None)
+        finally:
+            if ctx:
+                ctx.__exit__(None, None, None)
+        outs.append((raw, out, st))
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
