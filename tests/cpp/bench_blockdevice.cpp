@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstdio>
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -40,11 +41,15 @@ int main(int argc, char** argv)
 {
     const double min_s = argc > 1 ? std::atof(argv[1]) : 0.2;
     const size_t block_size = 256;
-    StackDisk<> disk;
-    RawBlockDevice raw(block_size, disk);
-    ReedSolomonBlockDevice rs(disk, block_size, 16);
-    HammingBlockDevice hamming((int)std::log2(block_size), disk);
-    CrcBlockDevice crc(CrcPolynomial::MsgImplicit(0xea), disk, block_size);
+    // one disk per device (the reference's fixtures each build their own), so a device's blocks
+    // 0 and 1 are its own formatted codewords
+    std::vector<std::unique_ptr<StackDisk<>>> disks;
+    for (int i = 0; i < 4; ++i)
+        disks.push_back(std::make_unique<StackDisk<>>());
+    RawBlockDevice raw(block_size, *disks[0]);
+    ReedSolomonBlockDevice rs(*disks[1], block_size, 16);
+    HammingBlockDevice hamming((int)std::log2(block_size), *disks[2]);
+    CrcBlockDevice crc(CrcPolynomial::MsgImplicit(0xea), *disks[3], block_size);
     std::map<std::string, IBlockDevice*> devs = { { "raw", &raw }, { "crc", &crc }, { "hamming", &hamming },
         { "rs", &rs } };
     for (auto& kv : devs) // blocks 0 and 1 valid for every codec
