@@ -60,7 +60,7 @@ constexpr int DEC_NBUF = 2, DEC_WPC = 3;
 #define PPFS_PAIR_ENC 6, 1
 #endif
 #ifndef PPFS_PAIR_DEC
-#define PPFS_PAIR_DEC 4, 1
+#define PPFS_PAIR_DEC 5, 1
 #endif
 constexpr int PAIR_ENC_WPC = pair::wpc_of(PPFS_PAIR_ENC), PAIR_DEC_WPC = pair::wpc_of(PPFS_PAIR_DEC);
 #endif

@@ -217,7 +217,8 @@ __device__ __noinline__ void pair_correct_general(uint8_t* lds, uint32_t goff, u
 // Decode correction for the pair's block; s = the lane's column of r' = x^2t c(x) mod g.  Single
 // error: S_1, S_2 -> X = S_2/S_1, e = S_1/X, confirmed iff r' == e * XP row LOG X (rs_col.hpp).
 template <int T2>
-__device__ __forceinline__ uint32_t pair_correct(uint8_t* lds, uint32_t goff, uint32_t xoff, uint32_t row, uint32_t slot,
+__device__ __forceinline__ uint32_t pair_correct(uint8_t* lds, uint32_t goff, const uint8_t* __restrict__ xp, uint32_t row,
+    uint32_t slot,
     uint32_t c, const uint32_t (&s)[4], bool valid, uint8_t* __restrict__ raw_g, uint64_t gblk, bool wb)
 {
     const bool err = valid && pair_or(s[0] | s[1] | s[2] | s[3]) != 0u;
@@ -241,7 +242,7 @@ __device__ __forceinline__ uint32_t pair_correct(uint8_t* lds, uint32_t goff, ui
     lx = lx >= 255u ? lx - 255u : lx;
     uint32_t le = l1 + 255u - lx;
     le = le >= 255u ? le - 255u : le;
-    const uint4 xr = *(const uint4*)(lds + xoff + 32u * lx + 16u * c);
+    const uint4 xr = *(const uint4*)(xp + 32u * lx + 16u * c); // XP rows stay in global memory (L2)
     const uint32_t xw[4] = { xr.x, xr.y, xr.z, xr.w };
     uint32_t bad = (s1 == 0u || s2 == 0u) ? 1u : 0u;
 #pragma unroll
@@ -284,7 +285,9 @@ __device__ __forceinline__ void stage_bytes128(uint8_t* dst, const uint8_t* __re
 // an iteration; NBUF = 1: after this tile's emission reads (more workgroups per CU overlap it).
 template <int T2, bool DEC, int NBUF> struct Lds {
     using L = RsPairLayout<T2>;
-    static constexpr int TBL = DEC ? L::TABLE_BYTES : L::ENC_BYTES;
+    // decode copies SL + GF; the XP rows (8 KiB, read once per single-error block) stay in
+    // global memory so that one more workgroup fits a CU
+    static constexpr int TBL = DEC ? L::OFF_XP : L::ENC_BYTES;
     static constexpr int OFF_PAR = TBL;
     static constexpr int OFF_BUF = OFF_PAR + 2080;
     static constexpr int BYTES = OFF_BUF + NBUF * BUF;
@@ -371,7 +374,7 @@ __global__ __launch_bounds__(NTHR, 2) void rs_pair_encode_kernel(const uint8_t* 
 }
 
 template <int T2, int WPC = 3, int NBUF = 2, int NTST = 1>
-__global__ __launch_bounds__(NTHR, 2) void rs_pair_decode_kernel(uint8_t* __restrict__ raw,
+__global__ __launch_bounds__(NTHR, (WPC >= 5 ? 3 : 2)) void rs_pair_decode_kernel(uint8_t* __restrict__ raw,
     uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables,
     int write_back)
 {
@@ -409,7 +412,7 @@ __global__ __launch_bounds__(NTHR, 2) void rs_pair_decode_kernel(uint8_t* __rest
         *(uint4*)(lds + slot + 16u * c) = make_uint4(s[0], s[1], s[2], s[3]); // read by the general path
         wave_fence();
         const uint32_t st =
-            pair_correct<T2>(lds, L::OFF_GF, L::OFF_XP, row, slot, c, s, true, raw, t * TB + blk, wb);
+            pair_correct<T2>(lds, L::OFF_GF, tables + L::OFF_XP, row, slot, c, s, true, raw, t * TB + blk, wb);
         if (status && c == 0)
             status[t * TB + blk] = (uint8_t)st;
         barrier_lds(); // C: corrections patched into the LDS rows
@@ -451,7 +454,7 @@ __global__ __launch_bounds__(NTHR, 2) void rs_pair_decode_kernel(uint8_t* __rest
         wave_fence();
         const bool valid = blk < nb;
         const uint32_t st =
-            pair_correct<T2>(lds, L::OFF_GF, L::OFF_XP, row, slot, c, s, valid, raw, t * TB + blk, wb);
+            pair_correct<T2>(lds, L::OFF_GF, tables + L::OFF_XP, row, slot, c, s, valid, raw, t * TB + blk, wb);
         if (status && valid && c == 0)
             status[t * TB + blk] = (uint8_t)st;
         barrier_lds();
