@@ -428,6 +428,11 @@ struct ppfs_ecc_ctx {
     uint8_t* h_pin[2] = { nullptr, nullptr };
     uint8_t* d_stage[2] = { nullptr, nullptr };
     size_t stage_bytes = 0;
+    // zero-copy staging for small host batches (the per-block IBlockDevice calls): coherent
+    // host memory the kernels read and write in place, no H2D / D2H
+    uint8_t* h_zc = nullptr;
+    uint8_t* d_zc = nullptr;
+    size_t zc_bytes = 0;
 };
 
 extern "C" uint64_t ppfs_ecc_crc_implicit_to_explicit(uint64_t implicit_poly) { return (implicit_poly << 1) + 1; }
@@ -564,6 +569,8 @@ extern "C" void ppfs_ecc_destroy(ppfs_ecc_ctx* c)
         (void)hipFree(c->d_tables);
     if (c->d_scratch)
         (void)hipFree(c->d_scratch);
+    if (c->h_zc)
+        (void)hipHostFree(c->h_zc);
     delete c;
 }
 
@@ -791,6 +798,62 @@ static bool host_pinned(const void* p)
     return a.type == hipMemoryTypeHost;
 }
 
+static int device_op(ppfs_ecc_ctx* c, HostOp op, uint8_t* d, const Layout& L, size_t nb, int write_back, bool want_data,
+    bool want_spill, hipStream_t s)
+{
+    switch (op) {
+    case OP_ENCODE:
+        return ppfs_ecc_encode_device(c, d + L.data, d + L.raw, nb, s);
+    case OP_WRITE:
+        return ppfs_ecc_write_device(c, d + L.data, d + L.raw, d + L.status, nb, s);
+    case OP_DECODE:
+        return ppfs_ecc_decode_device(c, d + L.raw, want_data ? d + L.data : nullptr, d + L.status, nb, write_back,
+            want_spill ? d + L.spill : nullptr, s);
+    }
+    return fail(PPFS_ECC_EINVAL, "bad op");
+}
+
+constexpr size_t kSmallBlocks = 64; // one tile: the per-block IBlockDevice calls
+
+// Small batches run the kernels on coherent host memory in place: no H2D / D2H copies on the
+// critical path of a per-block readBlock / writeBlock (each async copy costs microseconds).
+static int host_run_small(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t* data_out, uint8_t* raw,
+    uint8_t* status, uint8_t* spill, size_t nb, int write_back)
+{
+    const Layout L = layout_for(c, nb);
+    if (c->zc_bytes < L.total) {
+        if (c->h_zc)
+            (void)hipHostFree(c->h_zc);
+        c->h_zc = c->d_zc = nullptr;
+        c->zc_bytes = 0;
+        const size_t bytes = std::max(L.total, layout_for(c, kSmallBlocks).total);
+        HIP_TRY(hipHostMalloc((void**)&c->h_zc, bytes, hipHostMallocMapped | hipHostMallocCoherent), "zero-copy alloc");
+        HIP_TRY(hipHostGetDevicePointer((void**)&c->d_zc, c->h_zc, 0), "zero-copy map");
+        c->zc_bytes = bytes;
+    }
+    if (!c->hs[0])
+        HIP_TRY(hipStreamCreateWithFlags(&c->hs[0], hipStreamNonBlocking), "stream");
+    uint8_t* h = c->h_zc;
+    const size_t spill_b = 256 - std::min<size_t>(c->raw, 255);
+    if (op == OP_ENCODE || op == OP_WRITE)
+        std::memcpy(h + L.data, data_in, nb * c->data);
+    if (op != OP_ENCODE || raw_is_rmw(c))
+        std::memcpy(h + L.raw, raw, nb * c->raw);
+    int r = device_op(c, op, c->d_zc, L, nb, write_back, data_out != nullptr, spill != nullptr, c->hs[0]);
+    if (r)
+        return r;
+    HIP_TRY(hipStreamSynchronize(c->hs[0]), "sync");
+    if (op == OP_ENCODE || op == OP_WRITE || write_back)
+        std::memcpy(raw, h + L.raw, nb * c->raw);
+    if (op == OP_DECODE && data_out)
+        std::memcpy(data_out, h + L.data, nb * c->data);
+    if (status && op != OP_ENCODE)
+        std::memcpy(status, h + L.status, nb);
+    if (spill)
+        std::memcpy(spill, h + L.spill, nb * spill_b);
+    return 0;
+}
+
 static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t* data_out, uint8_t* raw,
     uint8_t* status, uint8_t* spill, size_t nblocks, int write_back)
 {
@@ -798,6 +861,10 @@ static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t*
         return fail(PPFS_ECC_EINVAL, "null ctx");
     if (nblocks == 0)
         return 0;
+    if (nblocks <= kSmallBlocks) {
+        HIP_TRY(hipSetDevice(c->device), "set device");
+        return host_run_small(c, op, data_in, data_out, raw, status, spill, nblocks, write_back);
+    }
     const size_t chunk = std::min(nblocks, kChunkBlocks);
     const Layout L = layout_for(c, chunk);
     int r = ensure_staging(c, L.total);
@@ -874,18 +941,29 @@ static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t*
         if (r)
             return r;
         // outputs device -> pinned staging (or straight to page-locked caller buffers)
-        uint8_t* o_raw = direct ? raw + b0 * c->raw : h + L.raw;
-        uint8_t* o_data = direct ? (data_out ? data_out + b0 * c->data : nullptr) : h + L.data;
-        uint8_t* o_st = direct ? (status ? status + b0 : nullptr) : h + L.status;
-        uint8_t* o_sp = direct ? (spill ? spill + b0 * spill_b : nullptr) : h + L.spill;
-        if (op == OP_ENCODE || op == OP_WRITE || write_back)
-            HIP_TRY(hipMemcpyAsync(o_raw, d + L.raw, nb * c->raw, hipMemcpyDeviceToHost, s), "D2H raw");
-        if (op == OP_DECODE && data_out)
-            HIP_TRY(hipMemcpyAsync(o_data, d + L.data, nb * c->data, hipMemcpyDeviceToHost, s), "D2H data");
-        if (status && (op != OP_ENCODE))
-            HIP_TRY(hipMemcpyAsync(o_st, d + L.status, nb, hipMemcpyDeviceToHost, s), "D2H status");
-        if (spill)
-            HIP_TRY(hipMemcpyAsync(o_sp, d + L.spill, nb * spill_b, hipMemcpyDeviceToHost, s), "D2H spill");
+        const bool want_raw = op == OP_ENCODE || op == OP_WRITE || write_back;
+        const bool want_data = op == OP_DECODE && data_out;
+        const bool want_st = status && op != OP_ENCODE;
+        if (!direct && nb * (c->raw + c->data) <= (64u << 10)) {
+            // small batches (the per-block IBlockDevice calls): one D2H of the staging span
+            // instead of up to four -- each copy is a few us of latency on the critical path
+            const size_t lo = want_data ? L.data : L.raw;
+            const size_t hi = spill ? L.spill + nb * spill_b : (want_st ? L.status + nb : L.raw + nb * c->raw);
+            HIP_TRY(hipMemcpyAsync(h + lo, d + lo, hi - lo, hipMemcpyDeviceToHost, s), "D2H");
+        } else {
+            uint8_t* o_raw = direct ? raw + b0 * c->raw : h + L.raw;
+            uint8_t* o_data = direct ? (data_out ? data_out + b0 * c->data : nullptr) : h + L.data;
+            uint8_t* o_st = direct ? (status ? status + b0 : nullptr) : h + L.status;
+            uint8_t* o_sp = direct ? (spill ? spill + b0 * spill_b : nullptr) : h + L.spill;
+            if (want_raw)
+                HIP_TRY(hipMemcpyAsync(o_raw, d + L.raw, nb * c->raw, hipMemcpyDeviceToHost, s), "D2H raw");
+            if (want_data)
+                HIP_TRY(hipMemcpyAsync(o_data, d + L.data, nb * c->data, hipMemcpyDeviceToHost, s), "D2H data");
+            if (want_st)
+                HIP_TRY(hipMemcpyAsync(o_st, d + L.status, nb, hipMemcpyDeviceToHost, s), "D2H status");
+            if (spill)
+                HIP_TRY(hipMemcpyAsync(o_sp, d + L.spill, nb * spill_b, hipMemcpyDeviceToHost, s), "D2H spill");
+        }
         pending_first[slot] = b0;
         pending_n[slot] = nb;
         busy[slot] = true;

@@ -112,6 +112,8 @@ int main(int argc, char** argv)
         }
         auto t2 = clk::now();
         ok = ok && out == pay;
+        (void)dev.writeBlocks(0, NB, pay.data(), err.data()); // warm: staging buffers allocated
+        (void)dev.readBlocks(0, NB, out.data(), err.data());
         auto t3 = clk::now();
         (void)dev.writeBlocks(0, NB, pay.data(), err.data());
         auto t4 = clk::now();
