@@ -203,23 +203,6 @@ __device__ __forceinline__ void slice_lookups(Ent<W> (&e)[2 * NL], uint32_t lo, 
     }
 }
 
-// W = 8 variant of slice_lookups: byte P's two 32-byte entries XORed straight into acc
-template <int NL, int P>
-__device__ __forceinline__ void slice_accum(uint32_t (&acc)[8], uint32_t lo, uint32_t hi, uint32_t lo4, uint32_t hi4,
-    const uint8_t* lds)
-{
-    if constexpr (P < NL) {
-        const uint32_t x = P < 4 ? lo : hi, x4 = P < 4 ? lo4 : hi4;
-        Ent<8> e[2];
-        e[0] = tbl_ld<8>(lds, nib16<P & 3>(x4) + (2 * P) * 256);
-        e[1] = tbl_ld<8>(lds, nib16<P & 3>(x) + (2 * P + 1) * 256);
-        xor_into<8, 2>(acc, e);
-        if constexpr (P & 1)
-            __builtin_amdgcn_sched_barrier(0); // keep the machine scheduler from re-hoisting every load
-        slice_accum<NL, P + 1>(acc, lo, hi, lo4, hi4, lds);
-    }
-}
-
 // st <- (st * x^8 + sum_i chunk_i x^(2t+i)) mod g, top-aligned state.
 // NB = number of chunk bytes that may be non-zero when FIRST (state still zero).
 template <int W, bool FIRST, int NB>
@@ -236,16 +219,6 @@ __device__ __forceinline__ void slice8(uint32_t (&st)[W], uint32_t lo, uint32_t 
     for (int w = 2; w < W; ++w)
         acc[w] = FIRST ? 0u : st[w - 2];
     constexpr int NL = FIRST ? (NB < 8 ? NB : 8) : 8;
-    if constexpr (W == 8) {
-        // 32-byte entries: XOR each byte's two lookups in as they arrive so that at most a
-        // few entries (8 VGPRs each) are live -- all 16 at once spill the 256-VGPR budget
-        const uint32_t lo4 = lo << 4, hi4 = hi << 4;
-        slice_accum<NL, 0>(acc, lo, hi, lo4, hi4, lds);
-#pragma unroll
-        for (int w = 0; w < W; ++w)
-            st[w] = acc[w];
-        return;
-    }
     Ent<W> e[2 * NL];
 #if PPFS_SDWA_ADDR
     // slot address of a nibble = nibble * 16: the high nibble of byte k is (x >> 8k) & 0xF0,
