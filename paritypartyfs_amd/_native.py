@@ -10,7 +10,8 @@ import os
 from ctypes import POINTER, c_char_p, c_int, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libppfs_ecc.so")
+# PPFS_ECC_LIB: an alternative build of the same library (ablation runs, tools/)
+LIB_PATH = os.environ.get("PPFS_ECC_LIB") or os.path.join(_HERE, "_lib", "libppfs_ecc.so")
 
 # ECCType (lib/blockdevice/include/ppfs/blockdevice/ecc_type.hpp:8-14)
 ECC_NONE, ECC_CRC, ECC_HAMMING, ECC_PARITY, ECC_REED_SOLOMON = 0, 1, 2, 3, 4

@@ -50,6 +50,12 @@ static uint32_t rs_tile_grid(uint64_t nb, int wpc)
 // segment workgroup path (2t <= 8): one 256-thread workgroup per 64-block tile, WPC resident per CU
 constexpr int ENC_NBUF = 2, ENC_WPC = (4 * wg::lds_bytes<PPFS_T2, false, 2>() <= 163840) ? 4 : 3;
 constexpr int DEC_NBUF = 2, DEC_WPC = 3;
+#ifndef PPFS_ENC_NTST
+#define PPFS_ENC_NTST 1
+#endif
+#ifndef PPFS_DEC_NTST
+#define PPFS_DEC_NTST 1
+#endif
 #elif PPFS_T2 > 16
 // pair workgroup path (16 < 2t <= 32, rs_pair.hpp): 128-thread workgroups, (WPC, NBUF) per CU.
 // Single-buffered tiles let 6 (encode) / 4 (decode) workgroups share a CU: the chains are
@@ -71,7 +77,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
     const uint8_t* tab, hipStream_t s)
 {
 #if PPFS_T2 <= 8
-    hipLaunchKernelGGL((wg::rs_wg_encode_kernel<PPFS_T2, ENC_NBUF, ENC_WPC>), dim3(rs_tile_grid(nb, ENC_WPC)), dim3(256),
+    hipLaunchKernelGGL((wg::rs_wg_encode_kernel<PPFS_T2, ENC_NBUF, ENC_WPC, 3, PPFS_ENC_NTST>), dim3(rs_tile_grid(nb, ENC_WPC)), dim3(256),
         0, s, d, r, nb, tab);
 #elif PPFS_T2 > 16
     hipLaunchKernelGGL((pair::rs_pair_encode_kernel<PPFS_T2, PPFS_PAIR_ENC>), dim3(rs_tile_grid(nb, PAIR_ENC_WPC)),
@@ -86,7 +92,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
     const uint8_t* tab, int wb, hipStream_t s)
 {
 #if PPFS_T2 <= 8
-    hipLaunchKernelGGL((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC>), dim3(rs_tile_grid(nb, DEC_WPC)), dim3(256),
+    hipLaunchKernelGGL((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC, 7, PPFS_DEC_NTST>), dim3(rs_tile_grid(nb, DEC_WPC)), dim3(256),
         0, s, r, d, st, nb, tab, wb);
 #elif PPFS_T2 > 16
     hipLaunchKernelGGL((pair::rs_pair_decode_kernel<PPFS_T2, PPFS_PAIR_DEC>), dim3(rs_tile_grid(nb, PAIR_DEC_WPC)),
