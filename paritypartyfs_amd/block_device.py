@@ -307,6 +307,21 @@ class _EngineDevice(IBlockDevice):
             status = np.zeros(nb, dtype=np.uint8)
             spill = np.zeros(nb * e.spill_bytes_per_block(), dtype=np.uint8) if self._has_spill() else None
             e.decode_host(fixed, out[done:].reshape(-1), status, write_back=wb, spill=spill)
+            if spill is None:
+                # no write-back leaves its block: the per-block write-backs together are the
+                # changed bytes of the range, written once; the log keeps block order
+                bad = np.nonzero(status == STATUS_CORRECTION_ERROR)[0]
+                err[done + bad] = int(FsError.BlockDevice_CorrectionError)
+                out[done + bad] = 0
+                if wb:
+                    for i in np.nonzero(status == STATUS_CORRECTED)[0]:
+                        self._log(first + done + int(i))
+                    changed = np.nonzero(fixed != raw)[0]
+                    if changed.size:
+                        lo, hi = int(changed[0]), int(changed[-1]) + 1
+                        self._disk.write((first + done) * self._raw + lo, fixed[lo:hi].tobytes())
+                done += nb
+                continue
             i = 0
             while i < nb:
                 st = int(status[i])
