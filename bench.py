@@ -367,6 +367,10 @@ def main():
             "encode_GBps": round(alg_per_block * nb / (enc_avg * 1e-3) / 1e9, 1),
             "decode_GBps": round(alg_per_block * nb / (dec_avg * 1e-3) / 1e9, 1),
             "device_copy_GBps": round(copy_gbs, 1),
+            # payload rate beside the algorithmic one, and the dominant kernel
+            # against the device-to-device copy measured above
+            "payload_GiBps": round(value * k / alg_per_block, 3),
+            "roofline_frac_of_device_copy": round(achieved / copy_gbs, 4) if copy_gbs else None,
             "host_inclusive": host_incl,
             "kernel_path": eng.kernel_name,
             "launch": f"hipGraph of {group} steps" if graph is not None else "eager",
