@@ -66,6 +66,25 @@ int fail(int code, const char* what, hipError_t e = hipSuccess)
     return code;
 }
 
+// Runs a scope on a context's device and restores the caller's current device afterwards
+// (the HIP runtime may be shared with the caller's framework, e.g. torch's current device).
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess)
+            prev = -1;
+        if (prev != dev)
+            err = hipSetDevice(dev);
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0)
+            (void)hipSetDevice(prev);
+    }
+};
+
 #define HIP_TRY(expr, what)                                                                                            \
     do {                                                                                                               \
         hipError_t _e = (expr);                                                                                        \
@@ -534,7 +553,8 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
         delete c;
         return fail(PPFS_ECC_EINVAL, "unknown ecc_type");
     }
-    hipError_t e = hipSetDevice(device);
+    DeviceGuard guard(device);
+    hipError_t e = guard.err;
     if (e != hipSuccess) {
         delete c;
         return fail(PPFS_ECC_EHIP, "hipSetDevice", e);
@@ -556,7 +576,7 @@ extern "C" void ppfs_ecc_destroy(ppfs_ecc_ctx* c)
 {
     if (!c)
         return;
-    (void)hipSetDevice(c->device);
+    DeviceGuard guard(c->device);
     for (int i = 0; i < 2; ++i) {
         if (c->hs[i])
             (void)hipStreamDestroy(c->hs[i]);
@@ -738,7 +758,6 @@ static int ensure_staging(ppfs_ecc_ctx* c, size_t bytes)
 {
     if (c->stage_bytes >= bytes)
         return 0;
-    HIP_TRY(hipSetDevice(c->device), "set device");
     for (int i = 0; i < 2; ++i) {
         if (c->h_pin[i])
             (void)hipHostFree(c->h_pin[i]);
@@ -861,16 +880,15 @@ static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t*
         return fail(PPFS_ECC_EINVAL, "null ctx");
     if (nblocks == 0)
         return 0;
-    if (nblocks <= kSmallBlocks) {
-        HIP_TRY(hipSetDevice(c->device), "set device");
+    DeviceGuard guard(c->device);
+    HIP_TRY(guard.err, "set device");
+    if (nblocks <= kSmallBlocks)
         return host_run_small(c, op, data_in, data_out, raw, status, spill, nblocks, write_back);
-    }
     const size_t chunk = std::min(nblocks, kChunkBlocks);
     const Layout L = layout_for(c, chunk);
     int r = ensure_staging(c, L.total);
     if (r)
         return r;
-    HIP_TRY(hipSetDevice(c->device), "set device");
     const size_t spill_b = 256 - std::min<size_t>(c->raw, 255);
     size_t pending_first[2] = { 0, 0 }, pending_n[2] = { 0, 0 };
     bool busy[2] = { false, false };
@@ -1133,7 +1151,8 @@ extern "C" int ppfs_vote3_host(int device, const uint8_t* a, const uint8_t* b, c
             std::memset(damaged, 0, nrec * sizeof(uint32_t));
         return 0;
     }
-    HIP_TRY(hipSetDevice(device), "set device");
+    DeviceGuard guard(device);
+    HIP_TRY(guard.err, "set device");
     uint8_t* d = nullptr;
     const size_t dmg_off = (4 * nbytes + 255) & ~(size_t)255;
     HIP_TRY(hipMalloc(&d, dmg_off + nrec * sizeof(uint32_t)), "vote3 alloc");
