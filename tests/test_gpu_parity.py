@@ -175,6 +175,57 @@ def test_rs_full_batch_roundtrip_properties():
     assert bool((st == 0).all()) and torch.equal(out, data) and torch.equal(raw, clean)
 
 
+FULL_CFGS = [  # BASELINE configs at their per-GPU sizes (2^20 blocks)
+    ("cfg5_rs_t16", ECC_REED_SOLOMON, 4096, 16, 0),
+    ("cfg4_hamming", ECC_HAMMING, 4096, 0, 0),
+    ("cfg4_crc32", ECC_CRC, 4096, 0, (0x9960034C << 1) + 1),
+    ("parity4096", ECC_PARITY, 4096, 0, 0),
+]
+
+
+@pytest.mark.parametrize("name,typ,bs,t,poly", FULL_CFGS, ids=[c[0] for c in FULL_CFGS])
+def test_full_size_roundtrip_properties(name, typ, bs, t, poly):
+    """2^20 blocks on the device, one fault per block, size-independent properties:
+    RS t=16 -- one byte error: every block corrected, payloads and codewords restored, a clean
+    re-decode reports nothing; Hamming -- one bit flip in the used bits: corrected, the single
+    byte written back; CRC -- one flipped payload bit (not the undetectable last one): every block
+    fails its check (status 5); parity -- one flipped bit: every block fails.  Bit-exactness vs
+    the oracle is covered at smaller sizes by the tests above."""
+    nb = 1 << 20
+    eng = EccEngine(typ, bs, t, crc_polynomial_explicit=poly)
+    n, k = eng.raw_block_size, eng.data_size
+    g = torch.Generator(device="cuda").manual_seed(11)
+    data = torch.randint(0, 256, (nb * k,), dtype=torch.uint8, device="cuda", generator=g)
+    raw = torch.zeros(nb * n, dtype=torch.uint8, device="cuda")
+    eng.encode(data, raw, nblocks=nb)
+    clean = raw.clone()
+    base = torch.arange(nb, device="cuda", dtype=torch.int64) * n
+    if typ == ECC_REED_SOLOMON:
+        pos = base + torch.randint(0, n, (nb,), device="cuda", generator=g)
+        raw[pos] ^= torch.randint(1, 256, (nb,), dtype=torch.uint8, device="cuda", generator=g)
+    else:
+        # a bit inside the payload bytes [0, k - 1) (CRC: not the undetectable last payload bit)
+        byte = torch.randint(0, k - 1, (nb,), device="cuda", generator=g)
+        bit = torch.randint(0, 8, (nb,), device="cuda", generator=g).to(torch.uint8)
+        raw[base + byte] ^= torch.bitwise_left_shift(torch.ones_like(bit), bit)
+    out = torch.empty(nb * k, dtype=torch.uint8, device="cuda")
+    st = torch.full((nb,), 77, dtype=torch.uint8, device="cuda")
+    eng.decode(raw, out, st, write_back=True, nblocks=nb)
+    torch.cuda.synchronize()
+    if typ in (ECC_REED_SOLOMON, ECC_HAMMING):
+        assert bool((st == 1).all())
+        assert torch.equal(out, data)
+        assert torch.equal(raw, clean)
+        eng.decode(raw, out, st, write_back=True, nblocks=nb)
+        torch.cuda.synchronize()
+        assert bool((st == 0).all()) and torch.equal(out, data)
+    else:
+        assert bool((st == 5).all())
+        eng.decode(clean, out, st, write_back=False, nblocks=nb)
+        torch.cuda.synchronize()
+        assert bool((st == 0).all()) and torch.equal(out, data)
+
+
 def test_rs_generic_spill_matches_oracle(oracle):
     """Shortened code (n = 64): miscorrections past the block are reported in the spill."""
     bs, t, nb = 64, 3, 600
