@@ -33,15 +33,15 @@ static uint32_t rs_grid(uint64_t nb)
     return (uint32_t)(want < cap ? (want ? want : 1) : cap);
 }
 
-// persistent tile grid: WPC resident 256-thread workgroups per CU, capped by the 64-block tiles
-static uint32_t rs_tile_grid(uint64_t nb, int wpc)
+// persistent tile grid: WPC resident workgroups per CU, capped by the tiles (tb blocks each)
+static uint32_t rs_tile_grid(uint64_t nb, int wpc, int tb = 64)
 {
     int dev = 0;
     (void)hipGetDevice(&dev);
     int c = 0;
     if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
         c = 256;
-    const uint64_t tiles = (nb + 63) / 64;
+    const uint64_t tiles = (nb + (uint64_t)tb - 1) / (uint64_t)tb;
     const uint64_t cap = (uint64_t)wpc * (uint64_t)c;
     return (uint32_t)(tiles < cap ? (tiles ? tiles : 1) : cap);
 }
@@ -68,7 +68,18 @@ constexpr int DEC_NBUF = 2, DEC_WPC = 3;
 #ifndef PPFS_PAIR_DEC
 #define PPFS_PAIR_DEC 5, 1
 #endif
-constexpr int PAIR_ENC_WPC = pair::wpc_of(PPFS_PAIR_ENC), PAIR_DEC_WPC = pair::wpc_of(PPFS_PAIR_DEC);
+// encode into a codeword image (rs_pair_encode_img_kernel) where 16 | 2t; 0 = the window emission
+#ifndef PPFS_PAIR_IMG
+#define PPFS_PAIR_IMG 1
+#endif
+#ifndef PPFS_PAIR_IMG_NW
+#define PPFS_PAIR_IMG_NW 2 // waves per workgroup (32 blocks each)
+#endif
+#ifndef PPFS_PAIR_IMG_WPC
+#define PPFS_PAIR_IMG_WPC (PPFS_PAIR_IMG_NW == 4 ? 4 : 6)
+#endif
+constexpr bool PAIR_IMG = PPFS_PAIR_IMG && (PPFS_T2 % 16 == 0);
+constexpr int PAIR_ENC_WPC = PAIR_IMG ? PPFS_PAIR_IMG_WPC : pair::wpc_of(PPFS_PAIR_ENC), PAIR_DEC_WPC = pair::wpc_of(PPFS_PAIR_DEC);
 #endif
 // 8 < 2t <= 16: lane-per-block kernels (rs_fast.hpp); the column path leaves half of its lanes on
 // all-zero state columns there and measured slower on decode
@@ -80,8 +91,12 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
     hipLaunchKernelGGL((wg::rs_wg_encode_kernel<PPFS_T2, ENC_NBUF, ENC_WPC, 3, PPFS_ENC_NTST>), dim3(rs_tile_grid(nb, ENC_WPC)), dim3(256),
         0, s, d, r, nb, tab);
 #elif PPFS_T2 > 16
-    hipLaunchKernelGGL((pair::rs_pair_encode_kernel<PPFS_T2, PPFS_PAIR_ENC>), dim3(rs_tile_grid(nb, PAIR_ENC_WPC)),
-        dim3(pair::NTHR), 0, s, d, r, nb, tab);
+    if constexpr (PAIR_IMG)
+        hipLaunchKernelGGL((pair::rs_pair_encode_img_kernel<PPFS_T2, PPFS_PAIR_IMG_WPC, PPFS_PAIR_IMG_NW>),
+            dim3(rs_tile_grid(nb, PAIR_ENC_WPC, 32 * PPFS_PAIR_IMG_NW)), dim3(64 * PPFS_PAIR_IMG_NW), 0, s, d, r, nb, tab);
+    else
+        hipLaunchKernelGGL((pair::rs_pair_encode_kernel<PPFS_T2, PPFS_PAIR_ENC>), dim3(rs_tile_grid(nb, PAIR_ENC_WPC)),
+            dim3(pair::NTHR), 0, s, d, r, nb, tab);
 #else
     hipLaunchKernelGGL(rs255_encode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, d, r, nb, tab);
 #endif

@@ -260,6 +260,35 @@ __device__ __forceinline__ uint32_t pair_correct(uint8_t* lds, uint32_t goff, co
     return err ? 1u : 0u;
 }
 
+// Decode emission for 2t a multiple of 16: payload piece p starts at codeword byte
+// 16 p + 2t (b + 1) of the tile, a 16-byte aligned LDS address, and the bytes past block b's end
+// (from kb on) come from 2t further on.  Two aligned ds_read_b128 and one byte mask, where
+// col_dec_piece's windows (any alignment) cost four reads and the funnel shifts.
+template <int T2> __device__ __forceinline__ uint4 pair_dec_piece(const uint8_t* lds, uint32_t buf, uint32_t p)
+{
+    static_assert(T2 % 16 == 0, "aligned payload pieces need 16 | 2t");
+    constexpr uint32_t K = 255 - T2;
+    const uint32_t j0 = p * 16u, b = j0 / K, off = j0 - K * b;
+    const uint32_t S = buf + PAD + j0 + (uint32_t)T2 * (b + 1u);
+    const uint32_t kb = off > K - 16u ? K - off : 16u;
+    const uint4 X = ld16(lds, S), Z = ld16(lds, S + (uint32_t)T2);
+    const wg::M128 mZ = wg::range_mask(kb, 16);
+    const uint32_t x[4] = { X.x, X.y, X.z, X.w }, z[4] = { Z.x, Z.y, Z.z, Z.w };
+    uint32_t o[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+        o[m] = wg::bfi(col::mword(mZ, m), z[m], x[m]);
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+template <int T2> __device__ __forceinline__ uint4 dec_piece(const uint8_t* lds, uint32_t buf, uint32_t p)
+{
+    if constexpr (T2 % 16 == 0)
+        return pair_dec_piece<T2>(lds, buf, p);
+    else
+        return col_dec_piece<T2>(lds, buf, p);
+}
+
 // LDS-DMA of a tile by 128 threads: piece p = tid + 128 k lands at dst + 16 p.
 template <int NPIECE>
 __device__ __forceinline__ void dma_tile128(uint8_t* dst, const uint8_t* __restrict__ src, uint32_t tid)
@@ -373,6 +402,118 @@ __global__ __launch_bounds__(NTHR, 2) void rs_pair_encode_kernel(const uint8_t* 
     }
 }
 
+// ---- Encode into a codeword image (2t a multiple of 16) ----
+// The tile is DMA'd straight into the OUTPUT layout: codeword j of the tile at LDS IMG + 255 j,
+// payload at IMG + 255 j + 2t.  Output piece i (bytes [16 i, 16 i + 16) of the tile's codewords)
+// takes its payload bytes from tile payload offset 16 i - 2t (b + 1), b = the block of those bytes:
+// a 16-byte aligned source, so every piece is one LDS-DMA lane.  The parity bytes (registers after
+// the remainder) are then written into the gaps [255 j, 255 j + 2t) and the emission is a plain
+// aligned copy of the image: no per-piece windows, masks or parity merges (those were 42 % of the
+// VALU instructions of rs_pair_encode_kernel's tile loop).
+// image bytes of a TBK-block tile, + slack: the rows' last word reads run past the image
+template <int TBK> constexpr int img_bytes() { return TBK * 255 + 64; }
+
+// tile payload offset of output piece i, or -1 when the piece holds parity bytes only
+template <int T2> __device__ __forceinline__ int img_src(uint32_t i)
+{
+    const uint32_t e = 16u * i + 15u, b = e / 255u, off = e - 255u * b;
+    if (off >= (uint32_t)T2)
+        return (int)(16u * i) - T2 * (int)(b + 1u); // payload of block b (from 255 b + 2t on)
+    if (16u * i >= 255u * b)
+        return -1; // inside block b's parity
+    return (int)(16u * i) - T2 * (int)b; // ends block b-1's payload, then block b's parity
+}
+
+// NW waves per workgroup (32 blocks each), tiles of TBK = 32 NW blocks; the tables are shared by
+// the NW waves, so larger workgroups fit more waves per CU (NW = 4: 4 x 40.9 KB, 16 waves).
+template <int T2, int WPC = 6, int NW = 2, int NTST = 1>
+__global__ __launch_bounds__(64 * NW, 2) void rs_pair_encode_img_kernel(const uint8_t* __restrict__ data,
+    uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables)
+{
+    static_assert(T2 % 16 == 0, "aligned image pieces need 16 | 2t");
+    using L = RsPairLayout<T2>;
+    constexpr int TBL = L::ENC_BYTES;
+    constexpr int IMG = TBL;
+    constexpr int TBK = 32 * NW, NT = 64 * NW;
+    constexpr int BYTES = IMG + img_bytes<TBK>();
+    constexpr int LDS_ALLOC = wg::lds_alloc<BYTES, WPC>();
+    static_assert(WPC * LDS_ALLOC <= 163840, "LDS for WPC workgroups per CU");
+    static_assert(IMG % 16 == 0, "aligned image");
+    constexpr int K = L::K;
+    constexpr int PIECES = TBK * 255 / 16; // in and out (1020 at 64 blocks)
+    constexpr int KP = (PIECES + NT - 1) / NT;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_ALLOC];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
+    const uint32_t c = lane_col(lane), blk = 32u * wave + lane_blk(lane);
+    const uint32_t tb = L::OFF_SL + 256u * c;
+    for (uint32_t p = tid; p < (uint32_t)TBL / 16; p += NT)
+        *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
+    const uint32_t img_base = __builtin_amdgcn_readfirstlane(lds_addr(lds + IMG) + (tid & ~63u) * 16u);
+    auto dma_img = [&](const uint8_t* __restrict__ src) {
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+            const uint32_t i = tid + (uint32_t)NT * k;
+            const int so = img_src<T2>(i);
+            if (((k + 1) * NT <= PIECES || i < (uint32_t)PIECES) && so >= 0)
+                dma16(src + so, img_base + 16u * NT * k);
+        }
+    };
+    const uint64_t nfull = nblocks / TBK, ntiles = (nblocks + TBK - 1) / TBK;
+    uint64_t t = blockIdx.x;
+    if (t < nfull)
+        dma_img(data + t * (TBK * K));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t row = IMG + 255u * blk + (uint32_t)T2;
+    uint8_t* const gap = lds + IMG + 255u * blk + 16u * c; // this lane's 16 parity bytes
+    for (; t < nfull; t += gridDim.x) {
+        barrier_lds(); // A: tile t in the image, the last tile's emission reads done
+        uint32_t s[4];
+        pair_remainder<K>(s, lds, row, tb, c);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            gap[k] = (uint8_t)(s[k >> 2] >> (8 * (k & 3)));
+        barrier_lds(); // B: parity in the image
+        uint8_t* dst = raw + t * (TBK * 255);
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+            const uint32_t i = tid + (uint32_t)NT * k;
+            if ((k + 1) * NT <= PIECES || i < (uint32_t)PIECES)
+                st_nt<NTST>(dst + 16u * i, ld16(lds, IMG + 16u * i));
+        }
+        barrier_lds(); // C: the image is free
+        const uint64_t nx = t + gridDim.x;
+        if (nx < nfull)
+            dma_img(data + nx * (TBK * K));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // other workgroups overlap this wait
+    }
+    if (t == nfull && nfull < ntiles) {
+        // the one partial tile (nblocks % TBK blocks), staged byte by byte into the image
+        barrier_lds();
+        const uint32_t nb = (uint32_t)(nblocks - t * TBK);
+        const uint8_t* src = data + t * (TBK * K);
+        for (uint32_t j = tid; j < nb * (uint32_t)K; j += NT) {
+            const uint32_t b = j / (uint32_t)K;
+            lds[row - 255u * blk + 255u * b + (j - (uint32_t)K * b)] = src[j];
+        }
+        barrier_lds();
+        uint32_t s[4];
+        pair_remainder<K>(s, lds, row, tb, c);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            gap[k] = (uint8_t)(s[k >> 2] >> (8 * (k & 3)));
+        barrier_lds();
+        uint8_t* dst = raw + t * (TBK * 255);
+        const uint32_t nout = nb * 255u;
+        for (uint32_t i = tid; 16u * i < nout; i += NT) {
+            const uint4 v = ld16(lds, IMG + 16u * i);
+            if (16u * i + 16u <= nout)
+                *(uint4*)(dst + 16u * i) = v;
+            else
+                st_bytes(dst + 16u * i, v, nout - 16u * i);
+        }
+    }
+}
+
 template <int T2, int WPC = 3, int NBUF = 2, int NTST = 1>
 __global__ __launch_bounds__(NTHR, (WPC >= 5 ? 3 : 2)) void rs_pair_decode_kernel(uint8_t* __restrict__ raw,
     uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables,
@@ -423,7 +564,7 @@ __global__ __launch_bounds__(NTHR, (WPC >= 5 ? 3 : 2)) void rs_pair_decode_kerne
 #pragma unroll
             for (int k = 0; k < KOUT; ++k) {
                 const uint32_t p = tid_o + (uint32_t)NTHR * k;
-                const uint4 o = col_dec_piece<T2>(lds, buf, p);
+                const uint4 o = dec_piece<T2>(lds, buf, p);
                 if ((k + 1) * NTHR <= OUT_PIECES || p < (uint32_t)OUT_PIECES)
                     st_nt<NTST>(dst + 16u * p, o);
             }
@@ -462,7 +603,7 @@ __global__ __launch_bounds__(NTHR, (WPC >= 5 ? 3 : 2)) void rs_pair_decode_kerne
             uint8_t* dst = data + t * (TB * K);
             const uint32_t nout = nb * (uint32_t)K;
             for (uint32_t p = tid; 16u * p < nout; p += NTHR) {
-                const uint4 v = col_dec_piece<T2>(lds, buf, p);
+                const uint4 v = dec_piece<T2>(lds, buf, p);
                 if (16u * p + 16u <= nout)
                     *(uint4*)(dst + 16u * p) = v;
                 else
