@@ -262,6 +262,15 @@ template <int T2> std::vector<uint8_t> build_rs_wg_tables_t()
             if (xr[q])
                 xp[p * 32 + (32 - t2 + q)] = G.log[xr[q]];
     }
+    // the same rows for x^p mod g: the single-error check on c mod g (rs_pair.hpp, RM decode)
+    uint8_t* xpm = xp + 255 * 32;
+    std::memset(xpm, 0xFF, 255 * 32);
+    for (int p = 0; p < 255; ++p) {
+        const std::vector<uint8_t> xr = rs_xpow_mod(p, g, t2);
+        for (int q = 0; q < t2; ++q)
+            if (xr[q])
+                xpm[p * 32 + (32 - t2 + q)] = G.log[xr[q]];
+    }
     return out;
 }
 
@@ -290,6 +299,15 @@ std::vector<uint8_t> build_rs_pair_tables(int t2)
         for (int q = 0; q < t2; ++q)
             if (xr[q])
                 xp[p * 32 + (32 - t2 + q)] = G.log[xr[q]];
+    }
+    // the same rows for x^p mod g: the single-error check on c mod g (rs_pair.hpp, RM decode)
+    uint8_t* xpm = xp + 255 * 32;
+    std::memset(xpm, 0xFF, 255 * 32);
+    for (int p = 0; p < 255; ++p) {
+        const std::vector<uint8_t> xr = rs_xpow_mod(p, g, t2);
+        for (int q = 0; q < t2; ++q)
+            if (xr[q])
+                xpm[p * 32 + (32 - t2 + q)] = G.log[xr[q]];
     }
     return out;
 }

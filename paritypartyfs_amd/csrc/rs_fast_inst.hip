@@ -65,8 +65,11 @@ constexpr int DEC_NBUF = 2, DEC_WPC = 3;
 #ifndef PPFS_PAIR_ENC
 #define PPFS_PAIR_ENC 6, 1
 #endif
+#ifndef PPFS_PAIR_DEC_RM
+#define PPFS_PAIR_DEC_RM 1 // decode from c mod g (payload remainder ^ parity) where 2t = 32
+#endif
 #ifndef PPFS_PAIR_DEC
-#define PPFS_PAIR_DEC 5, 1
+#define PPFS_PAIR_DEC 5, 1, 1, (PPFS_T2 == 32 && PPFS_PAIR_DEC_RM)
 #endif
 // encode into a codeword image (rs_pair_encode_img_kernel) where 16 | 2t; 0 = the window emission
 #ifndef PPFS_PAIR_IMG

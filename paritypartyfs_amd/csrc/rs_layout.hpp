@@ -71,9 +71,10 @@ template <int T2> struct RsPairLayout {
     static constexpr int OFF_GF = OFF_SL + 16 * 512;
     static constexpr int OFF_XP = OFF_GF + GF_BYTES;
     static constexpr int ENC_BYTES = OFF_GF;
-    static constexpr int TABLE_BYTES = OFF_XP + 255 * 32;
+    static constexpr int OFF_XPM = OFF_XP + 255 * 32; // rows x^p mod g (decode from c mod g)
+    static constexpr int TABLE_BYTES = OFF_XPM + 255 * 32;
 };
 
-constexpr int rs_pair_table_bytes() { return 16 * 512 + GF_BYTES + 255 * 32; }
+constexpr int rs_pair_table_bytes() { return 16 * 512 + GF_BYTES + 2 * 255 * 32; }
 
 } // namespace ppfs

@@ -49,7 +49,7 @@ constexpr int TB = 64;    // blocks per tile
 constexpr int NTHR = 128; // threads per workgroup: 2 waves x 32 blocks x 2 lanes
 static_assert(col::PAD == 48 && col::BUF == 16464, "emission helpers assume rs_col.hpp's tile buffer");
 constexpr int PAD = col::PAD, BUF = col::BUF;
-constexpr int wpc_of(int wpc, int nbuf) { return (void)nbuf, wpc; }
+constexpr int wpc_of(int wpc, int nbuf, int = 1, int = 0) { return (void)nbuf, wpc; }
 
 // value of the partner lane (lane ^ 4)
 __device__ __forceinline__ uint32_t pair_xchg(uint32_t v)
@@ -176,7 +176,8 @@ __device__ __forceinline__ uint32_t pair_or(uint32_t v) { return v | pair_xchg(v
 // General correction (2+ errors), out of line; both lanes of the pair: lane c computes S_i for
 // i = 16c+1 .. 16c+16 into the block's slot (over r', which both lanes have read), then lane 0
 // runs BM / roots / Forney (rs_fast.hpp).
-template <int T2>
+// RM: the state is c mod g (coefficient q has exponent i q in S_i) instead of x^2t c mod g
+template <int T2, bool RM = false>
 __device__ __noinline__ void pair_correct_general(uint8_t* lds, uint32_t goff, uint32_t row, uint32_t slot, uint32_t c,
     uint8_t* __restrict__ raw_g, uint64_t gblk, bool wb)
 {
@@ -188,7 +189,7 @@ __device__ __noinline__ void pair_correct_general(uint8_t* lds, uint32_t goff, u
 #pragma unroll
     for (int ii = 0; ii < 16; ++ii) {
         const uint32_t i = 16u * c + 1u + (uint32_t)ii;
-        uint32_t e = (255u * 32u - i * (uint32_t)T2) % 255u; // i (q - 2t) mod 255 at q = 0
+        uint32_t e = RM ? 0u : (255u * 32u - i * (uint32_t)T2) % 255u; // i (q - 2t) (RM: i q) mod 255 at q = 0
         uint32_t sacc = 0;
 #pragma unroll
         for (int q = 0; q < T2; ++q) {
@@ -216,7 +217,7 @@ __device__ __noinline__ void pair_correct_general(uint8_t* lds, uint32_t goff, u
 
 // Decode correction for the pair's block; s = the lane's column of r' = x^2t c(x) mod g.  Single
 // error: S_1, S_2 -> X = S_2/S_1, e = S_1/X, confirmed iff r' == e * XP row LOG X (rs_col.hpp).
-template <int T2>
+template <int T2, bool RM = false>
 __device__ __forceinline__ uint32_t pair_correct(uint8_t* lds, uint32_t goff, const uint8_t* __restrict__ xp, uint32_t row,
     uint32_t slot,
     uint32_t c, const uint32_t (&s)[4], bool valid, uint8_t* __restrict__ raw_g, uint64_t gblk, bool wb)
@@ -231,7 +232,8 @@ __device__ __forceinline__ uint32_t pair_correct(uint8_t* lds, uint32_t goff, co
     for (int k = 0; k < 16; ++k) {
         const uint32_t rb = (s[k >> 2] >> (8 * (k & 3))) & 0xFFu;
         const uint32_t lb = gf.log(rb), u = 16u * c + (uint32_t)k;
-        const uint32_t v1 = gf.exp(lb + u + 223u), v2 = gf.exp(lb + 2u * u + 191u);
+        // exponent i (q - 2t) for i = 1, 2 (q = u, 2t = 32); RM: i q
+        const uint32_t v1 = gf.exp(lb + u + (RM ? 0u : 223u)), v2 = gf.exp(lb + 2u * u + (RM ? 0u : 191u));
         s1 ^= rb ? v1 : 0u;
         s2 ^= rb ? v2 : 0u;
     }
@@ -256,7 +258,7 @@ __device__ __forceinline__ uint32_t pair_correct(uint8_t* lds, uint32_t goff, co
     if (geo && c == 0)
         col_fix(lds, row, raw_g, gblk, wb, lx, gf.exp(le));
     if (err && !geo)
-        pair_correct_general<T2>(lds, goff, row, slot, c, raw_g, gblk, wb);
+        pair_correct_general<T2, RM>(lds, goff, row, slot, c, raw_g, gblk, wb);
     return err ? 1u : 0u;
 }
 
@@ -514,7 +516,26 @@ __global__ __launch_bounds__(64 * NW, 2) void rs_pair_encode_img_kernel(const ui
     }
 }
 
-template <int T2, int WPC = 3, int NBUF = 2, int NTST = 1>
+// c mod g of the LDS codeword row: the remainder of the payload (as encode) XOR the stored parity
+// -- K bytes through the lookups instead of all 255 for x^2t c mod g (28 chunks, not 32)
+template <int T2>
+__device__ __forceinline__ void pair_cmodg(uint32_t (&s)[4], const uint8_t* lds, uint32_t row, uint32_t tb, uint32_t c)
+{
+    static_assert(T2 == 32, "state byte q = coefficient q");
+    pair_remainder<255 - T2>(s, lds, row + (uint32_t)T2, tb, c);
+    const uint32_t a = row + 16u * c, sh = (a & 3u) * 8u;
+    const uint32_t* w = (const uint32_t*)(lds + (a & ~3u));
+    uint32_t d[5];
+#pragma unroll
+    for (int m = 0; m < 5; ++m)
+        d[m] = w[m];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+        s[m] ^= __builtin_amdgcn_alignbit(d[m + 1], d[m], sh);
+}
+
+// RM: decode from c mod g (pair_cmodg) and the x^p mod g rows; else from x^2t c mod g
+template <int T2, int WPC = 3, int NBUF = 2, int NTST = 1, bool RM = (T2 == 32)>
 __global__ __launch_bounds__(NTHR, (WPC >= 5 ? 3 : 2)) void rs_pair_decode_kernel(uint8_t* __restrict__ raw,
     uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables,
     int write_back)
@@ -549,11 +570,14 @@ __global__ __launch_bounds__(NTHR, (WPC >= 5 ? 3 : 2)) void rs_pair_decode_kerne
             dma_tile128<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, raw + nx * (TB * 255), tid);
         const uint32_t row = buf + PAD + 255u * blk;
         uint32_t s[4];
-        pair_remainder<255>(s, lds, row, tb, c);
+        if constexpr (RM)
+            pair_cmodg<T2>(s, lds, row, tb, c);
+        else
+            pair_remainder<255>(s, lds, row, tb, c);
         *(uint4*)(lds + slot + 16u * c) = make_uint4(s[0], s[1], s[2], s[3]); // read by the general path
         wave_fence();
-        const uint32_t st =
-            pair_correct<T2>(lds, L::OFF_GF, tables + L::OFF_XP, row, slot, c, s, true, raw, t * TB + blk, wb);
+        const uint32_t st = pair_correct<T2, RM>(
+            lds, L::OFF_GF, tables + (RM ? L::OFF_XPM : L::OFF_XP), row, slot, c, s, true, raw, t * TB + blk, wb);
         if (status && c == 0)
             status[t * TB + blk] = (uint8_t)st;
         barrier_lds(); // C: corrections patched into the LDS rows
@@ -590,12 +614,15 @@ __global__ __launch_bounds__(NTHR, (WPC >= 5 ? 3 : 2)) void rs_pair_decode_kerne
         barrier_lds();
         const uint32_t row = buf + PAD + 255u * blk;
         uint32_t s[4];
-        pair_remainder<255>(s, lds, row, tb, c);
+        if constexpr (RM)
+            pair_cmodg<T2>(s, lds, row, tb, c);
+        else
+            pair_remainder<255>(s, lds, row, tb, c);
         *(uint4*)(lds + slot + 16u * c) = make_uint4(s[0], s[1], s[2], s[3]);
         wave_fence();
         const bool valid = blk < nb;
-        const uint32_t st =
-            pair_correct<T2>(lds, L::OFF_GF, tables + L::OFF_XP, row, slot, c, s, valid, raw, t * TB + blk, wb);
+        const uint32_t st = pair_correct<T2, RM>(
+            lds, L::OFF_GF, tables + (RM ? L::OFF_XPM : L::OFF_XP), row, slot, c, s, valid, raw, t * TB + blk, wb);
         if (status && valid && c == 0)
             status[t * TB + blk] = (uint8_t)st;
         barrier_lds();
