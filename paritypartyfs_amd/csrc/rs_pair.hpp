@@ -64,6 +64,15 @@ __device__ __forceinline__ uint32_t lane_col(uint32_t lane) { return __builtin_p
 // block (0..31) of a lane within its wave: lanes l and l ^ 4 share it
 __device__ __forceinline__ uint32_t lane_blk(uint32_t lane) { return ((lane >> 3) << 2) | (lane & 3u); }
 
+// Block of a lane for tiles whose rows sit at a 255-byte stride (codewords, the encode image):
+// half-wave h (32 lanes, 16 blocks) takes blocks h, h + NH, h + 2 NH, ... (NH = halves per
+// workgroup), so the 16 rows a ds_read_b32 group reads start 255 NH / 4 dwords apart -- distinct
+// banks -- where 16 consecutive blocks (63.75 dwords apart) pile onto ~4 banks.
+template <int NH> __device__ __forceinline__ uint32_t spread_blk(uint32_t wave, uint32_t lane)
+{
+    return (uint32_t)NH * lane_blk(lane & 31u) + 2u * wave + (lane >> 5);
+}
+
 // base + byte K of x (one v_add_u32_sdwa)
 template <int K> __device__ __forceinline__ uint32_t add_byte(uint32_t x, uint32_t base)
 {
@@ -446,7 +455,7 @@ __global__ __launch_bounds__(64 * NW, 2) void rs_pair_encode_img_kernel(const ui
     constexpr int KP = (PIECES + NT - 1) / NT;
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_ALLOC];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
-    const uint32_t c = lane_col(lane), blk = 32u * wave + lane_blk(lane);
+    const uint32_t c = lane_col(lane), blk = spread_blk<2 * NW>(wave, lane);
     const uint32_t tb = L::OFF_SL + 256u * c;
     for (uint32_t p = tid; p < (uint32_t)TBL / 16; p += NT)
         *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
@@ -550,7 +559,7 @@ __global__ __launch_bounds__(NTHR, (WPC >= 5 ? 3 : 2)) void rs_pair_decode_kerne
     constexpr int KOUT = (OUT_PIECES + NTHR - 1) / NTHR;
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_ALLOC];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
-    const uint32_t c = lane_col(lane), blk = 32u * wave + lane_blk(lane);
+    const uint32_t c = lane_col(lane), blk = spread_blk<NTHR / 32>(wave, lane);
     const uint32_t tb = L::OFF_SL + 256u * c; // offset in lds[]
     const bool wb = write_back != 0, want = data != nullptr;
     const uint32_t slot = D::OFF_PAR + 32u * blk;
