@@ -76,7 +76,7 @@ constexpr int DEC_NBUF = 2, DEC_WPC = 3;
 #define PPFS_PAIR_IMG 1
 #endif
 #ifndef PPFS_PAIR_IMG_NW
-#define PPFS_PAIR_IMG_NW 2 // waves per workgroup (32 blocks each)
+#define PPFS_PAIR_IMG_NW 4 // waves per workgroup (32 blocks each): 4 x 4 = 16 waves per CU, +1-2 % over 2
 #endif
 #ifndef PPFS_PAIR_IMG_WPC
 #define PPFS_PAIR_IMG_WPC (PPFS_PAIR_IMG_NW == 4 ? 4 : 6)
