@@ -291,6 +291,41 @@ __device__ __forceinline__ uint32_t ham_mid32(const uint8_t* img, uint32_t i)
     return (A & mk) | (B & ~mk);
 }
 
+// payload bytes [b0, b0 + 16) (b0 >= 8) of the corrected raw image: payload bits [i0, i0 + 128)
+// sit at raw bits [r0, ...) with at most one parity position inside (the next power of two): bits
+// before it come from the raw stream at r0 (A), bits after it from r0 + 1 (B).  Most pieces hold
+// no parity position (n >= 128): A only.
+__device__ __forceinline__ void ham_mid_piece(const uint8_t* img, uint32_t b0, uint32_t (&o)[4])
+{
+    const uint32_t i0 = 8u * b0;
+    uint32_t j = 31u - (uint32_t)__builtin_clz(i0 + 2);
+    if (i0 + j + 2 >= (2u << j))
+        j++;
+    const uint32_t r0 = i0 + j + 2;
+    const uint32_t n = (2u << j) - r0; // payload bits before the parity position
+    const uint32_t* src = (const uint32_t*)(img + ((r0 >> 5) << 2));
+    const uint32_t sft = r0 & 31u;
+    uint32_t E[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+        E[i] = bswap(src[i]);
+    if (n >= 128) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            o[u] = bswap((uint32_t)((((uint64_t)E[u] << 32) | E[u + 1]) >> (32 - sft)));
+    } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint64_t pair = ((uint64_t)E[u] << 32) | E[u + 1];
+            const uint32_t A = (uint32_t)(pair >> (32 - sft));
+            const uint32_t B = (uint32_t)(pair >> (31 - sft));
+            const int32_t c = (int32_t)n - 32 * u;
+            const uint32_t mk = top_bits(c <= 0 ? 0u : (uint32_t)c);
+            o[u] = bswap((A & mk) | (B & ~mk));
+        }
+    }
+}
+
 template <int NP>
 __global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
     uint8_t* __restrict__ status, uint64_t nblocks, int write_back, HamFast a)
@@ -369,41 +404,22 @@ __global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restric
             const uint64_t start = blk * a.ds, a0 = start & ~15ull;
             const uint32_t m = (uint32_t)(start - a0);
             const uint32_t npc = (m + a.ds + 15) >> 4;
-            // one rolled loop over this lane's pieces keeps the live state to one piece
-#pragma unroll 1
-            for (int k = 0; k <= NP; ++k) {
-                const uint32_t p = 64u * k + lane;
-                if (p >= npc)
-                    break;
-                const int32_t b0 = (int32_t)(16 * p) - (int32_t)m; // payload byte of piece byte 0
+            auto store = [&](uint32_t p, int32_t b0, const uint32_t (&o)[4]) {
+                uint8_t* dst = data + a0 + 16ull * p;
+                if (b0 >= 0 && b0 + 16 <= (int32_t)a.ds)
+                    gst16(dst, make_uint4(o[0], o[1], o[2], o[3]));
+                else
+                    store_piece_part(dst, o, b0 < 0 ? (uint32_t)(-b0) : 0u,
+                        b0 + 16 > (int32_t)a.ds ? (uint32_t)((int32_t)a.ds - b0) : 16u);
+            };
+            // piece k = 0: the row's first bytes (payload bits below 64, several parity
+            // positions) sit in the pieces of lanes 0 and 1 only
+            {
+                const int32_t b0 = (int32_t)(16 * lane) - (int32_t)m;
                 uint32_t o[4];
                 if (b0 >= 8) {
-                    // payload bits [i0, i0 + 128) sit at raw bits [r0, ...) with at most one parity
-                    // position inside (the next power of two pn): bits before it come from the raw
-                    // stream at r0 (A), bits after it from r0 + 1 (B)
-                    const uint32_t i0 = 8u * (uint32_t)b0;
-                    uint32_t j = 31u - (uint32_t)__builtin_clz(i0 + 2);
-                    if (i0 + j + 2 >= (2u << j))
-                        j++;
-                    const uint32_t r0 = i0 + j + 2;
-                    const uint32_t n = (2u << j) - r0; // payload bits before the parity position
-                    const uint32_t* src = (const uint32_t*)(img + ((r0 >> 5) << 2));
-                    const uint32_t sft = r0 & 31u;
-                    uint32_t E[5];
-#pragma unroll
-                    for (int i = 0; i < 5; ++i)
-                        E[i] = bswap(src[i]);
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const uint64_t pair = ((uint64_t)E[u] << 32) | E[u + 1];
-                        const uint32_t A = (uint32_t)(pair >> (32 - sft));
-                        const uint32_t B = (uint32_t)(pair >> (31 - sft));
-                        const int32_t c = (int32_t)n - 32 * u;
-                        const uint32_t mk = top_bits(c <= 0 ? 0u : (uint32_t)c);
-                        o[u] = bswap((A & mk) | (B & ~mk));
-                    }
+                    ham_mid_piece(img, (uint32_t)b0, o);
                 } else {
-                    // the row's first bytes: payload bits below 64 (several parity positions)
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         const int32_t i = 8 * (b0 + 4 * u);
@@ -417,12 +433,18 @@ __global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restric
                         o[u] = bswap(v);
                     }
                 }
-                uint8_t* dst = data + a0 + 16ull * p;
-                if (b0 >= 0 && b0 + 16 <= (int32_t)a.ds)
-                    gst16(dst, make_uint4(o[0], o[1], o[2], o[3]));
-                else
-                    store_piece_part(dst, o, b0 < 0 ? (uint32_t)(-b0) : 0u,
-                        b0 + 16 > (int32_t)a.ds ? (uint32_t)((int32_t)a.ds - b0) : 16u);
+                store(lane, b0, o);
+            }
+            // pieces k >= 1: no head path; one rolled loop keeps the live state to one piece
+#pragma unroll 1
+            for (int k = 1; k <= NP; ++k) {
+                const uint32_t p = 64u * k + lane;
+                if (p >= npc)
+                    break;
+                const int32_t b0 = (int32_t)(16 * p) - (int32_t)m;
+                uint32_t o[4];
+                ham_mid_piece(img, (uint32_t)b0, o);
+                store(p, b0, o);
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
