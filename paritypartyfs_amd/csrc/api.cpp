@@ -48,6 +48,8 @@ hipError_t ppfs_ham_decode(uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, int
 hipError_t ppfs_parity_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs,
     hipStream_t s);
 hipError_t ppfs_parity_check(const uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, uint32_t bs, hipStream_t s);
+hipError_t ppfs_gather_rows_launch(const uint8_t* src, uint8_t* dst, const uint32_t* idx, uint32_t nrows,
+    uint32_t row_bytes, hipStream_t s);
 hipError_t ppfs_vote3_launch(const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* out, uint64_t rec_bytes,
     uint64_t nrec, uint32_t* damaged, hipStream_t s);
 }
@@ -796,8 +798,12 @@ namespace {
 constexpr size_t kChunkBlocks = 1u << 15; // 32 Ki blocks per chunk (~8 MiB of RS codewords)
 
 struct Layout { // offsets inside one staging buffer
-    size_t data, raw, status, spill, total;
+    size_t data, raw, status, spill, idx, gat, total;
 };
+
+// a decode with write-back returns only the codewords it changed (status 1): as a packed gather
+// when at most nb / kGatherDiv blocks changed, else the chunk's whole codeword range
+constexpr size_t kGatherDiv = 8;
 
 Layout layout_for(const ppfs_ecc_ctx* c, size_t nb)
 {
@@ -807,7 +813,9 @@ Layout layout_for(const ppfs_ecc_ctx* c, size_t nb)
     L.raw = al(L.data + nb * c->data);
     L.status = al(L.raw + nb * c->raw);
     L.spill = al(L.status + nb);
-    L.total = al(L.spill + nb * (256 - std::min<size_t>(c->raw, 255)));
+    L.idx = al(L.spill + nb * (256 - std::min<size_t>(c->raw, 255)));
+    L.gat = al(L.idx + (nb / kGatherDiv + 1) * sizeof(uint32_t));
+    L.total = al(L.gat + (nb / kGatherDiv + 1) * c->raw);
     return L;
 }
 } // namespace
@@ -880,8 +888,12 @@ static int host_run_small(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, ui
     if (r)
         return r;
     HIP_TRY(hipStreamSynchronize(c->hs[0]), "sync");
-    if (op == OP_ENCODE || op == OP_WRITE || write_back)
+    if (op == OP_ENCODE || op == OP_WRITE)
         std::memcpy(raw, h + L.raw, nb * c->raw);
+    else if (write_back) // only the codewords the decode changed (status 1)
+        for (size_t b = 0; b < nb; ++b)
+            if (h[L.status + b] == 1)
+                std::memcpy(raw + b * c->raw, h + L.raw + b * c->raw, c->raw);
     if (op == OP_DECODE && data_out)
         std::memcpy(data_out, h + L.data, nb * c->data);
     if (status && op != OP_ENCODE)
@@ -909,22 +921,79 @@ static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t*
         return r;
     const size_t spill_b = 256 - std::min<size_t>(c->raw, 255);
     size_t pending_first[2] = { 0, 0 }, pending_n[2] = { 0, 0 };
-    bool busy[2] = { false, false };
+    // fetched: the chunk's codewords already came back (staging, or the caller's page-locked image)
+    bool busy[2] = { false, false }, fetched[2] = { false, false };
     // every caller buffer page-locked: DMA straight between it and the device staging buffers
     const bool direct = host_pinned(data_in) && host_pinned(data_out) && host_pinned(raw) && host_pinned(status)
         && host_pinned(spill);
+
+    // decode with write-back: the codewords come back only where the decode changed them
+    // (status 1), read from the chunk's status once it has landed
+    const bool lazy_raw = op == OP_DECODE && write_back;
+    // predictor: the last drained chunk changed many codewords -> fetch the next ones eagerly
+    // (queued behind the kernel, as encode does) instead of after the status has landed
+    bool eager = false;
+    auto fetch_changed = [&](int i, size_t b0, size_t nb) -> int {
+        uint8_t* h = c->h_pin[i];
+        uint8_t* d = c->d_stage[i];
+        hipStream_t s = c->hs[i];
+        const uint8_t* sts = (direct && status) ? status + b0 : h + L.status;
+        uint32_t* ix = (uint32_t*)(h + L.idx);
+        size_t nchg = 0;
+        for (size_t b = 0; b < nb; ++b)
+            if (sts[b] == 1) {
+                if (nchg <= nb / kGatherDiv)
+                    ix[nchg] = (uint32_t)b;
+                ++nchg;
+            }
+        eager = nchg > nb / kGatherDiv;
+        if (nchg == 0)
+            return 0;
+        if (fetched[i]) {
+            if (direct)
+                return 0; // the whole range landed in the caller's image (unchanged blocks: same bytes)
+            if (eager)
+                std::memcpy(raw + b0 * c->raw, h + L.raw, nb * c->raw);
+            else
+                for (size_t b = 0; b < nb; ++b)
+                    if (sts[b] == 1)
+                        std::memcpy(raw + (b0 + b) * c->raw, h + L.raw + b * c->raw, c->raw);
+            return 0;
+        }
+        if (nchg > nb / kGatherDiv) { // many: the whole range
+            uint8_t* o = direct ? raw + b0 * c->raw : h + L.raw;
+            HIP_TRY(hipMemcpyAsync(o, d + L.raw, nb * c->raw, hipMemcpyDeviceToHost, s), "D2H raw");
+            HIP_TRY(hipStreamSynchronize(s), "sync");
+            if (!direct)
+                std::memcpy(raw + b0 * c->raw, h + L.raw, nb * c->raw);
+            return 0;
+        }
+        HIP_TRY(hipMemcpyAsync(d + L.idx, ix, nchg * sizeof(uint32_t), hipMemcpyHostToDevice, s), "H2D idx");
+        HIP_TRY(ppfs_gather_rows_launch(d + L.raw, d + L.gat, (const uint32_t*)(d + L.idx), (uint32_t)nchg,
+                    (uint32_t)c->raw, s), "gather");
+        HIP_TRY(hipMemcpyAsync(h + L.gat, d + L.gat, nchg * c->raw, hipMemcpyDeviceToHost, s), "D2H gather");
+        HIP_TRY(hipStreamSynchronize(s), "sync");
+        for (size_t j = 0; j < nchg; ++j)
+            std::memcpy(raw + (b0 + ix[j]) * c->raw, h + L.gat + j * c->raw, c->raw);
+        return 0;
+    };
 
     auto drain = [&](int i) -> int {
         if (!busy[i])
             return 0;
         HIP_TRY(hipStreamSynchronize(c->hs[i]), "sync");
+        const size_t b0 = pending_first[i], nb = pending_n[i];
+        if (lazy_raw) {
+            const int e = fetch_changed(i, b0, nb);
+            if (e)
+                return e;
+        }
         if (direct) {
             busy[i] = false;
             return 0;
         }
-        const size_t b0 = pending_first[i], nb = pending_n[i];
         uint8_t* h = c->h_pin[i];
-        if (op == OP_ENCODE || op == OP_WRITE || write_back)
+        if (op == OP_ENCODE || op == OP_WRITE)
             std::memcpy(raw + b0 * c->raw, h + L.raw, nb * c->raw);
         if (op == OP_DECODE && data_out)
             std::memcpy(data_out + b0 * c->data, h + L.data, nb * c->data);
@@ -977,19 +1046,21 @@ static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t*
         if (r)
             return r;
         // outputs device -> pinned staging (or straight to page-locked caller buffers)
-        const bool want_raw = op == OP_ENCODE || op == OP_WRITE || write_back;
+        const bool want_raw = op == OP_ENCODE || op == OP_WRITE || (lazy_raw && eager);
         const bool want_data = op == OP_DECODE && data_out;
-        const bool want_st = status && op != OP_ENCODE;
+        const bool want_st = (status || lazy_raw) && op != OP_ENCODE;
         if (!direct && nb * (c->raw + c->data) <= (64u << 10)) {
             // small batches (the per-block IBlockDevice calls): one D2H of the staging span
             // instead of up to four -- each copy is a few us of latency on the critical path
             const size_t lo = want_data ? L.data : L.raw;
             const size_t hi = spill ? L.spill + nb * spill_b : (want_st ? L.status + nb : L.raw + nb * c->raw);
             HIP_TRY(hipMemcpyAsync(h + lo, d + lo, hi - lo, hipMemcpyDeviceToHost, s), "D2H");
+            fetched[slot] = true;
         } else {
+            fetched[slot] = want_raw;
             uint8_t* o_raw = direct ? raw + b0 * c->raw : h + L.raw;
             uint8_t* o_data = direct ? (data_out ? data_out + b0 * c->data : nullptr) : h + L.data;
-            uint8_t* o_st = direct ? (status ? status + b0 : nullptr) : h + L.status;
+            uint8_t* o_st = (direct && status) ? status + b0 : h + L.status;
             uint8_t* o_sp = direct ? (spill ? spill + b0 * spill_b : nullptr) : h + L.spill;
             if (want_raw)
                 HIP_TRY(hipMemcpyAsync(o_raw, d + L.raw, nb * c->raw, hipMemcpyDeviceToHost, s), "D2H raw");

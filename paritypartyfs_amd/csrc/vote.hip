@@ -44,3 +44,35 @@ extern "C" hipError_t ppfs_vote3_launch(const uint8_t* a, const uint8_t* b, cons
     hipLaunchKernelGGL(ppfs::vote3_kernel, dim3(grid), dim3(256), 0, s, a, b, c, out, rec_bytes, nbytes, damaged);
     return hipGetLastError();
 }
+
+// ---- gather of the rows a host decode has to return (api.cpp host_run) ----
+// dst row i = src row idx[i] (row_bytes each): the codewords a decode with write-back changed
+// (status 1), packed for one D2H copy when they are few.  One workgroup per row, 16-byte pieces
+// where source and destination are 16-byte aligned, else bytes.
+namespace ppfs {
+__global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+    const uint32_t* __restrict__ idx, uint32_t nrows, uint32_t row_bytes)
+{
+    for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+        const uint8_t* s = src + (uint64_t)idx[r] * row_bytes;
+        uint8_t* d = dst + (uint64_t)r * row_bytes;
+        if ((((uintptr_t)s | (uintptr_t)d | row_bytes) & 15u) == 0) {
+            for (uint32_t p = threadIdx.x; 16u * p < row_bytes; p += blockDim.x)
+                *(uint4*)(d + 16u * p) = *(const uint4*)(s + 16u * p);
+        } else {
+            for (uint32_t b = threadIdx.x; b < row_bytes; b += blockDim.x)
+                d[b] = s[b];
+        }
+    }
+}
+} // namespace ppfs
+
+extern "C" hipError_t ppfs_gather_rows_launch(const uint8_t* src, uint8_t* dst, const uint32_t* idx, uint32_t nrows,
+    uint32_t row_bytes, hipStream_t s)
+{
+    if (nrows == 0)
+        return hipSuccess;
+    const uint32_t grid = nrows < 4096u ? nrows : 4096u;
+    hipLaunchKernelGGL(ppfs::gather_rows_kernel, dim3(grid), dim3(256), 0, s, src, dst, idx, nrows, row_bytes);
+    return hipGetLastError();
+}

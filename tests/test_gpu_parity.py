@@ -489,3 +489,61 @@ def test_host_path_pinned_equals_pageable(typ, bs, t, poly):
         outs.append((raw, out, st))
     for a, b in zip(*outs):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("kind", ["pageable", "pinned"])
+@pytest.mark.parametrize("codec", ["rs512", "ham1024"])
+def test_host_decode_returns_only_changed_codewords(oracle, kind, codec):
+    """decode_host with write-back fetches codewords back only where the decode changed them
+    (status 1): not at all for a clean chunk, as a packed gather for a few, as the whole range for
+    many.  Chunks of 32 Ki blocks: clean / 100 errors / every block / 5,000 blocks / a short tail;
+    every path must leave the caller's image equal to the oracle's write-back."""
+    from paritypartyfs_amd import pinned
+
+    ch = 1 << 15
+    nb = 4 * ch + 777
+    rng = rng_for("lazyraw", codec, kind)
+    if codec == "rs512":
+        eng = EccEngine(ECC_REED_SOLOMON, 512, 3)
+    else:
+        eng = EccEngine(ECC_HAMMING, 1024, 0)
+    n, k = eng.raw_block_size, eng.data_size
+    data = rng.integers(0, 256, nb * k, dtype=np.uint8)
+    raw = np.zeros(nb * n, np.uint8)
+    eng.encode_host(data, raw)
+    bad = raw.reshape(nb, n).copy()
+    sets = [np.array([], np.int64), ch + rng.choice(ch, 100, replace=False), 2 * ch + np.arange(ch),
+            3 * ch + rng.choice(ch, 5000, replace=False), 4 * ch + rng.choice(777, 9, replace=False)]
+    hit = np.concatenate(sets)
+    if codec == "rs512":
+        bad[hit, rng.integers(0, n, hit.size)] ^= rng.integers(1, 256, hit.size, dtype=np.uint8)
+    else:  # single bit flips (corrected, 1 byte written back); a few double flips (status 5, no write)
+        pos = rng.integers(0, 8 * n, hit.size)
+        bad[hit, pos // 8] ^= (0x80 >> (pos % 8)).astype(np.uint8)
+        dbl = hit[::7]
+        bad[dbl, 3] ^= 0x01
+    bad = bad.reshape(-1)
+    if codec == "rs512":
+        o_data, o_st, o_fixed, _, _ = oracle.rs_decode(512, 3, bad)
+    else:
+        o_data, o_st, o_fixed, _ = oracle.ham_decode(1024, bad)
+    img = bad.copy()
+    out = np.zeros(nb * k, np.uint8)
+    st = np.full(nb, 77, np.uint8)
+    ctx = pinned(img, out, st) if kind == "pinned" else None
+    if ctx:
+        ctx.__enter__()
+    try:
+        eng.decode_host(img, out, st, write_back=True)
+    finally:
+        if ctx:
+            ctx.__exit__(None, None, None)
+    assert np.array_equal(st, o_st)
+    assert np.array_equal(img, o_fixed)
+    ok = o_st != 5
+    assert np.array_equal(out.reshape(nb, k)[ok], o_data.reshape(nb, k)[ok])
+    # status-only decode (the scrub's form): same image
+    img2 = bad.copy()
+    st2 = np.full(nb, 77, np.uint8)
+    eng.decode_host(img2, None, st2, write_back=True)
+    assert np.array_equal(st2, o_st) and np.array_equal(img2, o_fixed)

@@ -2,7 +2,7 @@
 """Host-inclusive rates (BASELINE north_star: the path starts and ends in host memory).
 
 RS(255,249) t=3, 2^20 blocks: encode_host, decode_host (1 error per block, payload + status out,
-write-back) and scrub_host over numpy buffers, pageable (one CPU copy each way through the
+write-back) and scrub_host over numpy buffers, and decode_host / scrub_host of clean codewords, pageable (one CPU copy each way through the
 library's pinned staging) and page-locked (ppfs_ecc_host_register: direct DMA).  GiB/s =
 algorithmic bytes (payload + codeword per block) / wall time; median of --reps.  One JSON line
 per (operation, memory kind).
@@ -64,12 +64,17 @@ def main():
             assert np.array_equal(out, data) and np.array_equal(raw, clean) and bool((st == 1).all())
             t_scr = timed(lambda: eng.scrub_host(raw, nblocks=nb, status=st), lambda: np.copyto(raw, bad))
             assert np.array_equal(raw, clean)
+            # clean codewords (the common read): nothing changes, no codeword comes back
+            t_decc = timed(lambda: eng.decode_host(raw, out, st, write_back=True), lambda: None)
+            assert np.array_equal(out, data) and np.array_equal(raw, clean) and not st.any()
+            t_scrc = timed(lambda: eng.scrub_host(raw, nblocks=nb, status=st), lambda: None)
         finally:
             if ctx:
                 ctx.__exit__(None, None, None)
         per = nb * (n + k)
-        for op, t in (("encode_host", t_enc), ("decode_host", t_dec), ("scrub_host", t_scr)):
-            by = per if op != "scrub_host" else nb * n * 2
+        for op, t in (("encode_host", t_enc), ("decode_host", t_dec), ("scrub_host", t_scr),
+                      ("decode_host_clean", t_decc), ("scrub_host_clean", t_scrc)):
+            by = per if not op.startswith("scrub_host") else nb * n * 2
             print(json.dumps({"op": op, "memory": kind, "blocks": nb, "ms": round(t * 1e3, 3),
                               "GiB_per_s": round(by / t / gib, 2)}), flush=True)
 
