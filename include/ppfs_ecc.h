@@ -171,6 +171,27 @@ int ppfs_vote3_host(int device, const uint8_t* a, const uint8_t* b, const uint8_
 int ppfs_ecc_host_register(void* ptr, size_t bytes);
 int ppfs_ecc_host_unregister(void* ptr);
 
+/*
+ * Multi-GPU host path: a group of contexts, one per listed HIP device (a device may
+ * repeat), over which the *_host calls shard a batch into contiguous block ranges -- shard g =
+ * blocks [g*N/G, (g+1)*N/G), one contiguous range of the packed image -- each run by its own host
+ * thread on its context's streams and pinned staging.  Blocks are independent codewords: no data
+ * moves between devices and no collective runs; the call returns when every shard's results are in
+ * host memory, with the first failing shard's error.  Status / spill are split like the blocks.
+ * (Reference: the caller side of IBlockDevice, file_io.cpp:12-104, issues the same per-block work
+ * serially on one CPU thread.)
+ */
+typedef struct ppfs_ecc_group ppfs_ecc_group;
+int ppfs_ecc_group_create(const ppfs_ecc_params* params, const int* devices, int ndevices, ppfs_ecc_group** out);
+void ppfs_ecc_group_destroy(ppfs_ecc_group* group);
+int ppfs_ecc_group_size(const ppfs_ecc_group* group);
+ppfs_ecc_ctx* ppfs_ecc_group_ctx(ppfs_ecc_group* group, int index);
+int ppfs_ecc_group_encode_host(ppfs_ecc_group* group, const uint8_t* data, uint8_t* raw, size_t nblocks);
+int ppfs_ecc_group_decode_host(ppfs_ecc_group* group, uint8_t* raw, uint8_t* data, uint8_t* status, size_t nblocks,
+    int write_back, uint8_t* spill);
+int ppfs_ecc_group_write_host(ppfs_ecc_group* group, const uint8_t* data, uint8_t* raw, uint8_t* status,
+    size_t nblocks);
+
 /* Last HIP error string recorded by this thread (diagnostics). */
 const char* ppfs_ecc_last_error(void);
 

@@ -38,6 +38,13 @@ EXPORTED_SYMBOLS = (
     "ppfs_vote3_host",
     "ppfs_ecc_host_register",
     "ppfs_ecc_host_unregister",
+    "ppfs_ecc_group_create",
+    "ppfs_ecc_group_destroy",
+    "ppfs_ecc_group_size",
+    "ppfs_ecc_group_ctx",
+    "ppfs_ecc_group_encode_host",
+    "ppfs_ecc_group_decode_host",
+    "ppfs_ecc_group_write_host",
     "ppfs_ecc_last_error",
 )
 
@@ -115,6 +122,20 @@ def lib() -> ctypes.CDLL:
     L.ppfs_ecc_host_register.argtypes = [c_void_p, c_size_t]
     L.ppfs_ecc_host_unregister.restype = c_int
     L.ppfs_ecc_host_unregister.argtypes = [c_void_p]
+    L.ppfs_ecc_group_create.restype = c_int
+    L.ppfs_ecc_group_create.argtypes = [POINTER(EccParams), POINTER(c_int), c_int, POINTER(c_void_p)]
+    L.ppfs_ecc_group_destroy.restype = None
+    L.ppfs_ecc_group_destroy.argtypes = [c_void_p]
+    L.ppfs_ecc_group_size.restype = c_int
+    L.ppfs_ecc_group_size.argtypes = [c_void_p]
+    L.ppfs_ecc_group_ctx.restype = c_void_p
+    L.ppfs_ecc_group_ctx.argtypes = [c_void_p, c_int]
+    L.ppfs_ecc_group_encode_host.restype = c_int
+    L.ppfs_ecc_group_encode_host.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t]
+    L.ppfs_ecc_group_decode_host.restype = c_int
+    L.ppfs_ecc_group_decode_host.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_void_p]
+    L.ppfs_ecc_group_write_host.restype = c_int
+    L.ppfs_ecc_group_write_host.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]
     L.ppfs_ecc_last_error.restype = c_char_p
     L.ppfs_ecc_last_error.argtypes = []
     _ = u8p

@@ -17,6 +17,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ppfs_ecc.h"
@@ -1281,4 +1282,107 @@ extern "C" int ppfs_ecc_host_unregister(void* ptr)
         return fail(PPFS_ECC_EINVAL, "host_unregister: null pointer");
     HIP_TRY(hipHostUnregister(ptr), "hipHostUnregister");
     return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// Multi-GPU host path: contiguous shards, one host thread per context
+// ------------------------------------------------------------------------------------------
+struct ppfs_ecc_group {
+    std::vector<ppfs_ecc_ctx*> ctx;
+};
+
+extern "C" int ppfs_ecc_group_create(const ppfs_ecc_params* params, const int* devices, int ndevices,
+    ppfs_ecc_group** out)
+{
+    if (!out || !devices || ndevices <= 0)
+        return fail(PPFS_ECC_EINVAL, "group: devices");
+    *out = nullptr;
+    ppfs_ecc_group* g = new (std::nothrow) ppfs_ecc_group();
+    if (!g)
+        return fail(PPFS_ECC_ENOMEM, "group alloc");
+    for (int i = 0; i < ndevices; ++i) {
+        ppfs_ecc_ctx* c = nullptr;
+        const int r = ppfs_ecc_create(params, devices[i], &c);
+        if (r) {
+            ppfs_ecc_group_destroy(g);
+            return r;
+        }
+        g->ctx.push_back(c);
+    }
+    *out = g;
+    return 0;
+}
+
+extern "C" void ppfs_ecc_group_destroy(ppfs_ecc_group* g)
+{
+    if (!g)
+        return;
+    for (ppfs_ecc_ctx* c : g->ctx)
+        ppfs_ecc_destroy(c);
+    delete g;
+}
+
+extern "C" int ppfs_ecc_group_size(const ppfs_ecc_group* g) { return g ? (int)g->ctx.size() : 0; }
+
+extern "C" ppfs_ecc_ctx* ppfs_ecc_group_ctx(ppfs_ecc_group* g, int i)
+{
+    return (g && i >= 0 && i < (int)g->ctx.size()) ? g->ctx[(size_t)i] : nullptr;
+}
+
+namespace {
+// run(ctx, first block, count) for every shard on its own thread; the first failing shard's
+// code and message come back to the calling thread
+int group_run(ppfs_ecc_group* g, size_t nblocks, const std::function<int(ppfs_ecc_ctx*, size_t, size_t)>& run)
+{
+    if (!g || g->ctx.empty())
+        return fail(PPFS_ECC_EINVAL, "null group");
+    const size_t G = g->ctx.size();
+    if (G == 1 || nblocks < G)
+        return run(g->ctx[0], 0, nblocks);
+    std::vector<int> rc(G, 0);
+    std::vector<std::string> msg(G);
+    std::vector<std::thread> th;
+    th.reserve(G);
+    for (size_t i = 0; i < G; ++i) {
+        const size_t b0 = nblocks * i / G, b1 = nblocks * (i + 1) / G;
+        th.emplace_back([&, i, b0, b1] {
+            rc[i] = run(g->ctx[i], b0, b1 - b0);
+            if (rc[i])
+                msg[i] = g_last_error;
+        });
+    }
+    for (auto& t : th)
+        t.join();
+    for (size_t i = 0; i < G; ++i)
+        if (rc[i]) {
+            g_last_error = msg[i];
+            return rc[i];
+        }
+    return 0;
+}
+} // namespace
+
+extern "C" int ppfs_ecc_group_encode_host(ppfs_ecc_group* g, const uint8_t* data, uint8_t* raw, size_t nblocks)
+{
+    return group_run(g, nblocks, [&](ppfs_ecc_ctx* c, size_t b0, size_t nb) {
+        return ppfs_ecc_encode_host(c, data + b0 * c->data, raw + b0 * c->raw, nb);
+    });
+}
+
+extern "C" int ppfs_ecc_group_decode_host(ppfs_ecc_group* g, uint8_t* raw, uint8_t* data, uint8_t* status,
+    size_t nblocks, int write_back, uint8_t* spill)
+{
+    return group_run(g, nblocks, [&](ppfs_ecc_ctx* c, size_t b0, size_t nb) {
+        const size_t sp = 256 - std::min<size_t>(c->raw, 255);
+        return ppfs_ecc_decode_host(c, raw + b0 * c->raw, data ? data + b0 * c->data : nullptr,
+            status ? status + b0 : nullptr, nb, write_back, spill ? spill + b0 * sp : nullptr);
+    });
+}
+
+extern "C" int ppfs_ecc_group_write_host(ppfs_ecc_group* g, const uint8_t* data, uint8_t* raw, uint8_t* status,
+    size_t nblocks)
+{
+    return group_run(g, nblocks, [&](ppfs_ecc_ctx* c, size_t b0, size_t nb) {
+        return ppfs_ecc_write_host(c, data + b0 * c->data, raw + b0 * c->raw, status ? status + b0 : nullptr, nb);
+    });
 }

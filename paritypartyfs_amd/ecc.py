@@ -117,6 +117,49 @@ class EccEngine:
                                           _stream_handle(stream)))
 
 
+class EccGroup:
+    """Multi-GPU host path (include/ppfs_ecc.h ppfs_ecc_group_*): one context per
+    listed device (a device may repeat); the *_host calls shard a batch into contiguous block
+    ranges, one host thread per context, with no data exchanged between devices."""
+
+    def __init__(self, ecc_type: int, block_size: int, rs_correctable_bytes: int = 3,
+                 crc_polynomial_explicit: int = 0, devices=(0,)):
+        p = EccParams(int(ecc_type), int(block_size), int(rs_correctable_bytes), 0, int(crc_polynomial_explicit))
+        devs = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+        h = c_void_p()
+        check(lib().ppfs_ecc_group_create(byref(p), devs, len(devices), byref(h)))
+        self._h = h
+        self.devices = tuple(int(d) for d in devices)
+        c0 = lib().ppfs_ecc_group_ctx(h, 0)
+        self.raw_block_size = int(lib().ppfs_ecc_raw_block_size(c0))
+        self.data_size = int(lib().ppfs_ecc_data_size(c0))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().ppfs_ecc_group_destroy(self._h)
+            self._h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def encode_host(self, data: np.ndarray, raw: np.ndarray) -> None:
+        n = data.size // self.data_size
+        check(lib().ppfs_ecc_group_encode_host(self._h, _ptr(data), _ptr(raw), n))
+
+    def decode_host(self, raw: np.ndarray, data: Optional[np.ndarray] = None, status: Optional[np.ndarray] = None,
+                    write_back: bool = True, spill: Optional[np.ndarray] = None) -> None:
+        n = raw.size // self.raw_block_size
+        check(lib().ppfs_ecc_group_decode_host(self._h, _ptr(raw), _ptr(data), _ptr(status), n,
+                                               int(bool(write_back)), _ptr(spill)))
+
+    def write_host(self, data: np.ndarray, raw: np.ndarray, status: Optional[np.ndarray] = None) -> None:
+        n = data.size // self.data_size
+        check(lib().ppfs_ecc_group_write_host(self._h, _ptr(data), _ptr(raw), _ptr(status), n))
+
+
 class pinned:
     """Page-lock numpy arrays for the duration of a `with` block (ppfs_ecc_host_register): the
     *_host calls then DMA them directly instead of copying through staging buffers."""

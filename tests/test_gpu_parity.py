@@ -547,3 +547,62 @@ def test_host_decode_returns_only_changed_codewords(oracle, kind, codec):
     st2 = np.full(nb, 77, np.uint8)
     eng.decode_host(img2, None, st2, write_back=True)
     assert np.array_equal(st2, o_st) and np.array_equal(img2, o_fixed)
+
+
+@pytest.mark.parametrize("devices", [(0, 0), (0, 0, 0)], ids=["g2", "g3"])
+@pytest.mark.parametrize("codec", ["rs512", "crc4096", "ham1024"])
+def test_group_host_path_matches_single_context(oracle, devices, codec):
+    """ppfs_ecc_group_* (SURVEY 8e host path): contiguous shards, one host thread per context
+    (here several contexts on GPU 0).  Every shard boundary must leave results byte-identical to
+    one context's calls and to the oracle."""
+    from paritypartyfs_amd import EccGroup
+
+    if codec == "rs512":
+        args = (ECC_REED_SOLOMON, 512, 3, 0)
+    elif codec == "crc4096":
+        args = (ECC_CRC, 4096, 0, (0x9960034C << 1) + 1)
+    else:
+        args = (ECC_HAMMING, 1024, 0, 0)
+    grp = EccGroup(*args, devices=devices)
+    one = EccEngine(*args)
+    n, k = one.raw_block_size, one.data_size
+    assert (grp.raw_block_size, grp.data_size) == (n, k)
+    nb = 40007 if n <= 512 else 3001
+    rng = rng_for("group", codec, len(devices))
+    data = rng.integers(0, 256, nb * k, dtype=np.uint8)
+    raw_g = np.zeros(nb * n, np.uint8)
+    raw_1 = np.zeros(nb * n, np.uint8)
+    grp.encode_host(data, raw_g)
+    one.encode_host(data, raw_1)
+    assert np.array_equal(raw_g, raw_1)
+    bad = raw_g.reshape(nb, n).copy()
+    hit = rng.choice(nb, nb // 3, replace=False)
+    if codec == "rs512":
+        bad[hit, rng.integers(0, n, hit.size)] ^= rng.integers(1, 256, hit.size, dtype=np.uint8)
+    else:
+        pos = rng.integers(0, 8 * n, hit.size)
+        bad[hit, pos // 8] ^= (0x80 >> (pos % 8)).astype(np.uint8)
+    bad = bad.reshape(-1)
+    outs = []
+    for eng in (grp, one):
+        img = bad.copy()
+        out = np.zeros(nb * k, np.uint8)
+        st = np.full(nb, 77, np.uint8)
+        eng.decode_host(img, out, st, write_back=True)
+        outs.append((img, out, st))
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+    if codec == "rs512":
+        o_data, o_st, o_fixed, _, _ = oracle.rs_decode(512, 3, bad)
+        assert np.array_equal(outs[0][2], o_st) and np.array_equal(outs[0][0], o_fixed)
+        assert np.array_equal(outs[0][1], o_data)
+    # read-modify-write of new payloads over the corrupted image
+    new = rng.integers(0, 256, nb * k, dtype=np.uint8)
+    res = []
+    for eng in (grp, one):
+        img = bad.copy()
+        st = np.full(nb, 77, np.uint8)
+        eng.write_host(new, img, st)
+        res.append((img, st))
+    assert np.array_equal(res[0][0], res[1][0]) and np.array_equal(res[0][1], res[1][1])
+    grp.close()

@@ -7,7 +7,10 @@ library's pinned staging) and page-locked (ppfs_ecc_host_register: direct DMA). 
 algorithmic bytes (payload + codeword per block) / wall time; median of --reps.  One JSON line
 per (operation, memory kind).
 
-usage: python3 tools/bench_host.py [--blocks N] [--reps R]
+--devices 0,0,...: run encode / decode through an EccGroup (ppfs_ecc_group_*: contiguous shards,
+one host thread per listed device; the scrub rows are single-context).
+
+usage: python3 tools/bench_host.py [--blocks N] [--reps R] [--devices D0,D1,...]
 """
 import argparse
 import json
@@ -24,13 +27,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--blocks", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--devices", default=None)
     a = ap.parse_args()
     import torch  # noqa: F401  (HIP runtime order, see paritypartyfs_amd/_native.py)
 
-    from paritypartyfs_amd import ECC_REED_SOLOMON, EccEngine, pinned
+    from paritypartyfs_amd import ECC_REED_SOLOMON, EccEngine, EccGroup, pinned
 
     nb = a.blocks
     eng = EccEngine(ECC_REED_SOLOMON, 512, 3)
+    devs = tuple(int(x) for x in a.devices.split(",")) if a.devices else None
+    grp = EccGroup(ECC_REED_SOLOMON, 512, 3, devices=devs) if devs else eng
     n, k = eng.raw_block_size, eng.data_size
     rng = np.random.default_rng(1)
     data = rng.integers(0, 256, nb * k, dtype=np.uint8)
@@ -58,14 +64,14 @@ def main():
         if ctx:
             ctx.__enter__()
         try:
-            t_enc = timed(lambda: eng.encode_host(data, raw), lambda: None)
+            t_enc = timed(lambda: grp.encode_host(data, raw), lambda: None)
             assert np.array_equal(raw, clean)
-            t_dec = timed(lambda: eng.decode_host(raw, out, st, write_back=True), lambda: np.copyto(raw, bad))
+            t_dec = timed(lambda: grp.decode_host(raw, out, st, write_back=True), lambda: np.copyto(raw, bad))
             assert np.array_equal(out, data) and np.array_equal(raw, clean) and bool((st == 1).all())
             t_scr = timed(lambda: eng.scrub_host(raw, nblocks=nb, status=st), lambda: np.copyto(raw, bad))
             assert np.array_equal(raw, clean)
             # clean codewords (the common read): nothing changes, no codeword comes back
-            t_decc = timed(lambda: eng.decode_host(raw, out, st, write_back=True), lambda: None)
+            t_decc = timed(lambda: grp.decode_host(raw, out, st, write_back=True), lambda: None)
             assert np.array_equal(out, data) and np.array_equal(raw, clean) and not st.any()
             t_scrc = timed(lambda: eng.scrub_host(raw, nblocks=nb, status=st), lambda: None)
         finally:
@@ -75,7 +81,8 @@ def main():
         for op, t in (("encode_host", t_enc), ("decode_host", t_dec), ("scrub_host", t_scr),
                       ("decode_host_clean", t_decc), ("scrub_host_clean", t_scrc)):
             by = per if not op.startswith("scrub_host") else nb * n * 2
-            print(json.dumps({"op": op, "memory": kind, "blocks": nb, "ms": round(t * 1e3, 3),
+            print(json.dumps({"op": op, "memory": kind, "blocks": nb, "devices": list(devs) if devs and
+                              not op.startswith("scrub") else [0], "ms": round(t * 1e3, 3),
                               "GiB_per_s": round(by / t / gib, 2)}), flush=True)
 
 
