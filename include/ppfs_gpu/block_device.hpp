@@ -45,6 +45,11 @@
 #include <utility>
 #include <vector>
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include "ppfs_ecc.h"
 
 #define MAX_BLOCK_SIZE 4096
@@ -240,6 +245,10 @@ struct IDisk {
     virtual expected<void> read(size_t address, size_t size, static_vector<uint8_t>& data) = 0;
     virtual expected<size_t> write(size_t address, const static_vector<uint8_t>& data) = 0;
     virtual size_t size() = 0;
+    // Extension: a disk whose whole image is addressable host memory (size() bytes, writes
+    // through it are the disk's writes).  The batch calls of the engine devices then run the
+    // engine on the image in place -- no copy into and out of a staging vector.  nullptr: no.
+    virtual uint8_t* mapped() { return nullptr; }
 };
 
 // In-memory disk with StackDisk's semantics (stack_disk.hpp:19-44: out-of-range accesses
@@ -269,9 +278,110 @@ public:
         return data.size();
     }
     uint8_t* image() { return _data.data(); }
+    uint8_t* mapped() override { return _data.data(); }
 
 private:
     std::vector<uint8_t> _data;
+};
+
+// File-backed disk with FileDisk's interface and checks (file_disk.hpp, file_disk.cpp:8-101:
+// open an existing file / create a zero-filled one of a fixed size; read checks open, bounds,
+// then capacity; write checks open and bounds), over a shared mmap of the file instead of
+// fstream seek + read / write.  The mapping is page-locked for the engine when the
+// HIP runtime allows it (ppfs_ecc_host_register; a file mapping it cannot pin stays pageable), so
+// the batch calls DMA straight between the page cache and HBM.
+class MappedFileDisk : public IDisk {
+public:
+    MappedFileDisk() = default;
+    ~MappedFileDisk() override { close(); }
+    MappedFileDisk(const MappedFileDisk&) = delete;
+    MappedFileDisk& operator=(const MappedFileDisk&) = delete;
+
+    expected<void> open(const std::string& path)
+    {
+        close();
+        const int fd = ::open(path.c_str(), O_RDWR);
+        if (fd < 0)
+            return unexpected(FsError::Disk_IOError);
+        struct stat st;
+        if (::fstat(fd, &st) != 0) {
+            ::close(fd);
+            return unexpected(FsError::Disk_IOError);
+        }
+        _size = (size_t)st.st_size;
+        if (_size) {
+            void* m = ::mmap(nullptr, _size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            if (m == MAP_FAILED) {
+                ::close(fd);
+                _size = 0;
+                return unexpected(FsError::Disk_IOError);
+            }
+            _map = (uint8_t*)m;
+            _pinned = ppfs_ecc_host_register(_map, _size) == 0;
+        }
+        _fd = fd;
+        return {};
+    }
+    expected<void> create(const std::string& path, size_t size)
+    {
+        if (_fd >= 0)
+            return unexpected(FsError::Disk_InvalidRequest); // file_disk.cpp:37-38
+        const int fd = ::open(path.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0644);
+        if (fd < 0)
+            return unexpected(FsError::Disk_IOError);
+        const bool ok = ::ftruncate(fd, (off_t)size) == 0;
+        ::close(fd);
+        if (!ok)
+            return unexpected(FsError::Disk_IOError);
+        return open(path);
+    }
+    void close()
+    {
+        if (_map) {
+            if (_pinned)
+                (void)ppfs_ecc_host_unregister(_map);
+            ::msync(_map, _size, MS_SYNC);
+            ::munmap(_map, _size);
+        }
+        if (_fd >= 0)
+            ::close(_fd);
+        _map = nullptr;
+        _fd = -1;
+        _size = 0;
+        _pinned = false;
+    }
+    size_t size() override { return _size; }
+    bool pinned() const { return _pinned; }
+    uint8_t* mapped() override { return _map; }
+    expected<void> read(size_t address, size_t size, static_vector<uint8_t>& data) override
+    {
+        if (_fd < 0)
+            return unexpected(FsError::Disk_IOError);
+        if (address + size > _size)
+            return unexpected(FsError::Disk_OutOfBounds);
+        if (data.capacity() < size)
+            return unexpected(FsError::Disk_InvalidRequest);
+        data.resize(size);
+        if (size)
+            std::memcpy(data.data(), _map + address, size);
+        return {};
+    }
+    expected<size_t> write(size_t address, const static_vector<uint8_t>& data) override
+    {
+        if (_fd < 0)
+            return unexpected(FsError::Disk_IOError);
+        if (address + data.size() > _size)
+            return unexpected(FsError::Disk_OutOfBounds);
+        if (data.size())
+            std::memcpy(_map + address, data.data(), data.size());
+        return data.size();
+    }
+
+private:
+    int _fd = -1;
+    uint8_t* _map = nullptr;
+    size_t _size = 0;
+    bool _pinned = false;
 };
 
 // ------------------------------------------------------------------------------------------
@@ -519,6 +629,26 @@ public:
     {
         if (err)
             std::memset(err, 0, count);
+        if (uint8_t* img = _disk.mapped(); img && !has_spill()) {
+            // in place on the disk image: the engine writes corrected codewords back into it
+            // (RS: whole codeword, Hamming: the flipped byte, as the reference's write-back)
+            if (((size_t)first + count) * _raw > _disk.size())
+                return unexpected(FsError::Disk_OutOfBounds);
+            std::vector<uint8_t> status(count);
+            EccEngine::check(ppfs_ecc_decode_host(_eng.ctx(), img + (size_t)first * _raw, out, status.data(), count,
+                                 1, nullptr),
+                "decode");
+            for (size_t i = 0; i < count; ++i) {
+                if (status[i] == PPFS_ECC_CORRECTION_ERROR) {
+                    if (err)
+                        err[i] = (uint8_t)FsError::BlockDevice_CorrectionError;
+                    std::memset(out + i * _ds, 0, _ds);
+                } else if (status[i] == PPFS_ECC_CORRECTED) {
+                    log(first + (block_index_t)i);
+                }
+            }
+            return {};
+        }
         size_t done = 0;
         while (done < count) {
             const size_t nb = count - done;
@@ -575,11 +705,19 @@ public:
             }
             return {};
         }
-        std::vector<uint8_t> raw(count * _raw), status(count);
-        auto rr = detail::disk_read(_disk, (size_t)first * _raw, count * _raw, raw.data());
-        if (!rr)
-            return unexpected(rr.error());
-        EccEngine::check(ppfs_ecc_write_host(_eng.ctx(), payloads, raw.data(), status.data(), count), "write");
+        uint8_t* img = _disk.mapped();
+        if (img && ((size_t)first + count) * _raw > _disk.size())
+            return unexpected(FsError::Disk_OutOfBounds);
+        std::vector<uint8_t> raw(img ? 0 : count * _raw), status(count);
+        if (img) { // in place on the disk image
+            EccEngine::check(
+                ppfs_ecc_write_host(_eng.ctx(), payloads, img + (size_t)first * _raw, status.data(), count), "write");
+        } else {
+            auto rr = detail::disk_read(_disk, (size_t)first * _raw, count * _raw, raw.data());
+            if (!rr)
+                return unexpected(rr.error());
+            EccEngine::check(ppfs_ecc_write_host(_eng.ctx(), payloads, raw.data(), status.data(), count), "write");
+        }
         for (size_t i = 0; i < count; ++i) {
             if (status[i] == PPFS_ECC_CORRECTION_ERROR) {
                 if (err)
@@ -589,6 +727,8 @@ public:
             }
         }
         // blocks that failed their check were left untouched by the engine
+        if (img)
+            return {};
         auto w = detail::disk_write(_disk, (size_t)first * _raw, raw.data(), count * _raw);
         if (!w)
             return unexpected(w.error());
@@ -605,6 +745,21 @@ public:
         const size_t base = (size_t)first * _raw;
         if (base + count * _raw > _disk.size())
             return unexpected(FsError::Disk_OutOfBounds);
+        if (uint8_t* img = _disk.mapped()) { // in place on the disk image
+            std::vector<uint8_t> status(count);
+            size_t c3[3] = { 0, 0, 0 };
+            EccEngine::check(
+                ppfs_ecc_scrub_host(_eng.ctx(), img + base, _disk.size() - base, count, status.data(), c3), "scrub");
+            for (size_t i = 0; i < count; ++i) {
+                if (status[i] == PPFS_ECC_CORRECTION_ERROR && err)
+                    err[i] = (uint8_t)FsError::BlockDevice_CorrectionError;
+                else if (status[i] == PPFS_ECC_CORRECTED)
+                    log(first + (block_index_t)i);
+            }
+            if (counts)
+                std::memcpy(counts, c3, sizeof c3);
+            return {};
+        }
         std::vector<uint8_t> image(_disk.size() - base), status(count);
         auto rr = detail::disk_read(_disk, base, image.size(), image.data());
         if (!rr)

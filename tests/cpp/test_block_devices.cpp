@@ -341,10 +341,29 @@ static std::unique_ptr<IBlockDevice> make_dev(const Cfg& c, IDisk& disk, std::sh
     }
 }
 
-static void differential(const Cfg& c, uint64_t seed, int nops)
+// Disks for the differential runs: the in-memory disk with the engine batch calls in place on its
+// image (mapped) or through a copy (not mapped), and the mmap'd file disk.
+template <bool MAP> struct TestStackDisk : public StackDisk<20> {
+    uint8_t* mapped() override { return MAP ? image() : nullptr; }
+};
+struct TestFileDisk : public MappedFileDisk {
+    TestFileDisk()
+    {
+        char path[] = "/tmp/ppfs_mfd_XXXXXX";
+        const int fd = mkstemp(path);
+        if (fd >= 0)
+            ::close(fd);
+        EXPECT_TRUE(create(path, size_t(1) << 20).has_value());
+        EXPECT_TRUE(!create(path, 16).has_value()); // file_disk.cpp:37-38: already open
+        ::unlink(path);                             // the mapping stays valid
+    }
+    uint8_t* image() { return mapped(); }
+};
+
+template <class D> static void differential(const Cfg& c, uint64_t seed, int nops)
 {
     constexpr size_t NB = 48;
-    StackDisk<20> disk; // 1 MiB
+    D disk; // 1 MiB
     auto lg = std::make_shared<Logger>();
     auto dev = make_dev(c, disk, lg);
     const size_t raw = dev->rawBlockSize(), ds = dev->dataSize();
@@ -493,7 +512,52 @@ TEST(Differential, AllCodecsVsOracleDeviceModel)
 {
     for (const Cfg& c : kCfgs)
         for (uint64_t seed = 1; seed <= 3; ++seed)
-            differential(c, seed * 7919 + (uint64_t)c.type, 160);
+            differential<TestStackDisk<true>>(c, seed * 7919 + (uint64_t)c.type, 160);
+}
+
+TEST(Differential, AllCodecsThroughCopiesVsOracleDeviceModel)
+{
+    for (const Cfg& c : kCfgs)
+        for (uint64_t seed = 1; seed <= 2; ++seed)
+            differential<TestStackDisk<false>>(c, seed * 104729 + (uint64_t)c.type, 160);
+}
+
+TEST(Differential, MappedFileDiskVsOracleDeviceModel)
+{
+    for (const Cfg& c : kCfgs)
+        differential<TestFileDisk>(c, 31337 + (uint64_t)c.type, 160);
+}
+
+TEST(MappedFileDisk, FileDiskChecks)
+{
+    MappedFileDisk d;
+    uint8_t buf[64];
+    static_vector<uint8_t> v(buf, 64);
+    EXPECT_EQ((int)d.read(0, 8, v).error(), (int)FsError::Disk_IOError); // not open
+    EXPECT_EQ((int)d.open("/nonexistent/ppfs").error(), (int)FsError::Disk_IOError);
+    char path[] = "/tmp/ppfs_mfd_XXXXXX";
+    const int fd = mkstemp(path);
+    EXPECT_TRUE(fd >= 0);
+    ::close(fd);
+    EXPECT_TRUE(d.create(path, 4096).has_value());
+    EXPECT_EQ(d.size(), (size_t)4096);
+    EXPECT_EQ((int)d.read(4090, 8, v).error(), (int)FsError::Disk_OutOfBounds);
+    static_vector<uint8_t> small(buf, 4);
+    EXPECT_EQ((int)d.read(0, 8, small).error(), (int)FsError::Disk_InvalidRequest);
+    for (int i = 0; i < 64; ++i)
+        buf[i] = (uint8_t)(i * 7);
+    static_vector<uint8_t> w(buf, 64, 64);
+    EXPECT_EQ(d.write(100, w).value(), (size_t)64);
+    EXPECT_EQ((int)d.write(4090, w).error(), (int)FsError::Disk_OutOfBounds);
+    d.close();
+    MappedFileDisk e; // reopen: the bytes reached the file
+    EXPECT_TRUE(e.open(path).has_value());
+    uint8_t rb[64] = { 0 };
+    static_vector<uint8_t> r(rb, 64);
+    EXPECT_TRUE(e.read(100, 64, r).has_value());
+    EXPECT_TRUE(std::memcmp(rb, buf, 64) == 0);
+    e.close();
+    ::unlink(path);
 }
 
 int main(int argc, char** argv)
