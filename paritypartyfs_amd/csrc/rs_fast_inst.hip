@@ -85,7 +85,21 @@ constexpr bool PAIR_IMG = PPFS_PAIR_IMG && (PPFS_T2 % 16 == 0);
 constexpr int PAIR_ENC_WPC = PAIR_IMG ? PPFS_PAIR_IMG_WPC : pair::wpc_of(PPFS_PAIR_ENC), PAIR_DEC_WPC = pair::wpc_of(PPFS_PAIR_DEC);
 #endif
 // 8 < 2t <= 16: lane-per-block kernels (rs_fast.hpp); the column path leaves half of its lanes on
-// all-zero state columns there and measured slower on decode
+// all-zero state columns there and measured slower on decode.  2t = 16
+// encodes with the solo image kernel (rs_pair.hpp) over the same slicing tables.
+#if PPFS_T2 > 8 && PPFS_T2 <= 16
+#ifndef PPFS_SOLO_IMG
+#define PPFS_SOLO_IMG 1
+#endif
+#ifndef PPFS_SOLO_NW
+#define PPFS_SOLO_NW 2
+#endif
+#ifndef PPFS_SOLO_WPC
+#define PPFS_SOLO_WPC 4
+#endif
+constexpr bool SOLO_IMG = PPFS_SOLO_IMG && PPFS_T2 == 16;
+constexpr int SOLO_NW = PPFS_SOLO_NW, SOLO_WPC = PPFS_SOLO_WPC;
+#endif
 
 extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d, uint8_t* r, uint64_t nb,
     const uint8_t* tab, hipStream_t s)
@@ -101,7 +115,11 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
         hipLaunchKernelGGL((pair::rs_pair_encode_kernel<PPFS_T2, PPFS_PAIR_ENC>), dim3(rs_tile_grid(nb, PAIR_ENC_WPC)),
             dim3(pair::NTHR), 0, s, d, r, nb, tab);
 #else
-    hipLaunchKernelGGL(rs255_encode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, d, r, nb, tab);
+    if constexpr (SOLO_IMG)
+        hipLaunchKernelGGL((pair::rs_solo_encode_img_kernel<PPFS_T2, SOLO_WPC, SOLO_NW>),
+            dim3(rs_tile_grid(nb, SOLO_WPC, 64 * SOLO_NW)), dim3(64 * SOLO_NW), 0, s, d, r, nb, tab);
+    else
+        hipLaunchKernelGGL(rs255_encode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, d, r, nb, tab);
 #endif
     return hipGetLastError();
 }

@@ -104,27 +104,31 @@ __device__ __forceinline__ void xor4(uint32_t (&a)[4], const uint4& e)
 
 // the 16 nibble lookups of one chunk (lo, hi): entries XORed into acc.  tb = lane's plane base
 // (SL + 256 c, offset into lds[]); table t = 2i + h sits at tb + 512 t.
+// TS: byte stride between the 16 tables (512: the pair layout's two column planes per table;
+// 256: one plane per table, the lane-per-block slicing tables of 8 < 2t <= 16 used by the solo
+// kernels)
+template <int TS = 512>
 __device__ __forceinline__ void pair_lookups(uint32_t (&acc)[4], const uint8_t* lds, uint32_t tb, uint32_t lo, uint32_t hi)
 {
     const uint32_t Ll = (lo << 4) & 0xF0F0F0F0u, Hl = lo & 0xF0F0F0F0u;
     const uint32_t Lh = (hi << 4) & 0xF0F0F0F0u, Hh = hi & 0xF0F0F0F0u;
     uint4 e[16];
-    e[0] = ld16(lds, add_byte<0>(Ll, tb) + 0 * 512);
-    e[1] = ld16(lds, add_byte<0>(Hl, tb) + 1 * 512);
-    e[2] = ld16(lds, add_byte<1>(Ll, tb) + 2 * 512);
-    e[3] = ld16(lds, add_byte<1>(Hl, tb) + 3 * 512);
-    e[4] = ld16(lds, add_byte<2>(Ll, tb) + 4 * 512);
-    e[5] = ld16(lds, add_byte<2>(Hl, tb) + 5 * 512);
-    e[6] = ld16(lds, add_byte<3>(Ll, tb) + 6 * 512);
-    e[7] = ld16(lds, add_byte<3>(Hl, tb) + 7 * 512);
-    e[8] = ld16(lds, add_byte<0>(Lh, tb) + 8 * 512);
-    e[9] = ld16(lds, add_byte<0>(Hh, tb) + 9 * 512);
-    e[10] = ld16(lds, add_byte<1>(Lh, tb) + 10 * 512);
-    e[11] = ld16(lds, add_byte<1>(Hh, tb) + 11 * 512);
-    e[12] = ld16(lds, add_byte<2>(Lh, tb) + 12 * 512);
-    e[13] = ld16(lds, add_byte<2>(Hh, tb) + 13 * 512);
-    e[14] = ld16(lds, add_byte<3>(Lh, tb) + 14 * 512);
-    e[15] = ld16(lds, add_byte<3>(Hh, tb) + 15 * 512);
+    e[0] = ld16(lds, add_byte<0>(Ll, tb) + 0 * TS);
+    e[1] = ld16(lds, add_byte<0>(Hl, tb) + 1 * TS);
+    e[2] = ld16(lds, add_byte<1>(Ll, tb) + 2 * TS);
+    e[3] = ld16(lds, add_byte<1>(Hl, tb) + 3 * TS);
+    e[4] = ld16(lds, add_byte<2>(Ll, tb) + 4 * TS);
+    e[5] = ld16(lds, add_byte<2>(Hl, tb) + 5 * TS);
+    e[6] = ld16(lds, add_byte<3>(Ll, tb) + 6 * TS);
+    e[7] = ld16(lds, add_byte<3>(Hl, tb) + 7 * TS);
+    e[8] = ld16(lds, add_byte<0>(Lh, tb) + 8 * TS);
+    e[9] = ld16(lds, add_byte<0>(Hh, tb) + 9 * TS);
+    e[10] = ld16(lds, add_byte<1>(Lh, tb) + 10 * TS);
+    e[11] = ld16(lds, add_byte<1>(Hh, tb) + 11 * TS);
+    e[12] = ld16(lds, add_byte<2>(Lh, tb) + 12 * TS);
+    e[13] = ld16(lds, add_byte<2>(Hh, tb) + 13 * TS);
+    e[14] = ld16(lds, add_byte<3>(Lh, tb) + 14 * TS);
+    e[15] = ld16(lds, add_byte<3>(Hh, tb) + 15 * TS);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         auto w = [&](int i) -> uint32_t { return q == 0 ? e[i].x : q == 1 ? e[i].y : q == 2 ? e[i].z : e[i].w; };
@@ -140,9 +144,14 @@ __device__ __forceinline__ void pair_lookups(uint32_t (&acc)[4], const uint8_t* 
 }
 
 // Remainder column c of a LEN-byte row at LDS byte `row` (s = state bytes [16c, 16c+16)).
-template <int LEN>
+// SOLO (2t <= 16): one lane per block holds the whole state as column 1 (column 0 is all zero):
+// no partner exchange, c = 1, tables at a 256-byte stride.
+template <int LEN, bool SOLO = false>
 __device__ __forceinline__ void pair_remainder(uint32_t (&s)[4], const uint8_t* lds, uint32_t row, uint32_t tb, uint32_t c)
 {
+    constexpr int TS = SOLO ? 256 : 512;
+    if constexpr (SOLO)
+        c = 1;
     constexpr int NC = (LEN + 7) / 8;
     constexpr int TOPN = LEN - 8 * (NC - 1);
     const uint32_t sh = (row & 3u) * 8u;
@@ -165,13 +174,13 @@ __device__ __forceinline__ void pair_remainder(uint32_t (&s)[4], const uint8_t* 
                 hi &= (1u << (8 * (TOPN - 4))) - 1u;
             }
             s[0] = s[1] = s[2] = s[3] = 0;
-            pair_lookups(s, lds, tb, lo, hi);
+            pair_lookups<TS>(s, lds, tb, lo, hi);
         } else {
-            const uint32_t p2 = pair_xchg(s[2]), p3 = pair_xchg(s[3]);
+            const uint32_t p2 = SOLO ? 0u : pair_xchg(s[2]), p3 = SOLO ? 0u : pair_xchg(s[3]);
             lo ^= c ? s[2] : p2; // fold the top 8 coefficients (column 1's upper half)
             hi ^= c ? s[3] : p3;
             uint32_t n[4] = { p2 & cm, p3 & cm, s[0], s[1] }; // state * x^8
-            pair_lookups(n, lds, tb, lo, hi);
+            pair_lookups<TS>(n, lds, tb, lo, hi);
             s[0] = n[0];
             s[1] = n[1];
             s[2] = n[2];
@@ -544,6 +553,96 @@ __device__ __forceinline__ void pair_cmodg(uint32_t (&s)[4], const uint8_t* lds,
 }
 
 // RM: decode from c mod g (pair_cmodg) and the x^p mod g rows; else from x^2t c mod g
+// ---- Solo encode into a codeword image (2t = 16): one lane per block ----
+// The state fits one 16-byte column, so a lane owns a block: half the lookups per block of the
+// pair kernels.  Tables: the lane-per-block slicing tables (16 tables x 16 nibbles x 16 B, top-
+// aligned entries = column 1 of the pair layout).  Tiles of 64 NW blocks into the output image as
+// rs_pair_encode_img_kernel; half-wave h takes rows h + 2 NW i so a ds_read_b32 group's 32 rows
+// start on distinct banks (4 rows apart at NW = 2).
+template <int T2, int WPC = 4, int NW = 2, int NTST = 1>
+__global__ __launch_bounds__(64 * NW, 2) void rs_solo_encode_img_kernel(const uint8_t* __restrict__ data,
+    uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables)
+{
+    static_assert(T2 == 16, "parity bytes = the lane's 16 state bytes; aligned image pieces need 16 | 2t");
+    constexpr int TBL = 16 * 256;
+    constexpr int IMG = TBL;
+    constexpr int TBK = 64 * NW, NT = 64 * NW;
+    constexpr int BYTES = IMG + img_bytes<TBK>();
+    constexpr int LDS_ALLOC = wg::lds_alloc<BYTES, WPC>();
+    static_assert(WPC * LDS_ALLOC <= 163840, "LDS for WPC workgroups per CU");
+    constexpr int K = 255 - T2;
+    constexpr int PIECES = TBK * 255 / 16;
+    constexpr int KP = (PIECES + NT - 1) / NT;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_ALLOC];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
+    const uint32_t blk = (uint32_t)(2 * NW) * (lane & 31u) + 2u * wave + (lane >> 5);
+    for (uint32_t p = tid; p < (uint32_t)TBL / 16; p += NT)
+        *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
+    const uint32_t img_base = __builtin_amdgcn_readfirstlane(lds_addr(lds + IMG) + (tid & ~63u) * 16u);
+    auto dma_img = [&](const uint8_t* __restrict__ src) {
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+            const uint32_t i = tid + (uint32_t)NT * k;
+            const int so = img_src<T2>(i);
+            if (((k + 1) * NT <= PIECES || i < (uint32_t)PIECES) && so >= 0)
+                dma16(src + so, img_base + 16u * NT * k);
+        }
+    };
+    const uint64_t nfull = nblocks / TBK, ntiles = (nblocks + TBK - 1) / TBK;
+    uint64_t t = blockIdx.x;
+    if (t < nfull)
+        dma_img(data + t * (TBK * K));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t row = IMG + 255u * blk + (uint32_t)T2;
+    uint8_t* const gap = lds + IMG + 255u * blk; // the block's 16 parity bytes
+    for (; t < nfull; t += gridDim.x) {
+        barrier_lds(); // A: tile t in the image, the last tile's emission reads done
+        uint32_t s[4];
+        pair_remainder<K, true>(s, lds, row, 0u, 1u);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            gap[k] = (uint8_t)(s[k >> 2] >> (8 * (k & 3)));
+        barrier_lds(); // B: parity in the image
+        uint8_t* dst = raw + t * (TBK * 255);
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+            const uint32_t i = tid + (uint32_t)NT * k;
+            if ((k + 1) * NT <= PIECES || i < (uint32_t)PIECES)
+                st_nt<NTST>(dst + 16u * i, ld16(lds, IMG + 16u * i));
+        }
+        barrier_lds(); // C: the image is free
+        const uint64_t nx = t + gridDim.x;
+        if (nx < nfull)
+            dma_img(data + nx * (TBK * K));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (t == nfull && nfull < ntiles) {
+        barrier_lds();
+        const uint32_t nb = (uint32_t)(nblocks - t * TBK);
+        const uint8_t* src = data + t * (TBK * K);
+        for (uint32_t j = tid; j < nb * (uint32_t)K; j += NT) {
+            const uint32_t b = j / (uint32_t)K;
+            lds[IMG + T2 + 255u * b + (j - (uint32_t)K * b)] = src[j];
+        }
+        barrier_lds();
+        uint32_t s[4];
+        pair_remainder<K, true>(s, lds, row, 0u, 1u);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            gap[k] = (uint8_t)(s[k >> 2] >> (8 * (k & 3)));
+        barrier_lds();
+        uint8_t* dst = raw + t * (TBK * 255);
+        const uint32_t nout = nb * 255u;
+        for (uint32_t i = tid; 16u * i < nout; i += NT) {
+            const uint4 v = ld16(lds, IMG + 16u * i);
+            if (16u * i + 16u <= nout)
+                *(uint4*)(dst + 16u * i) = v;
+            else
+                st_bytes(dst + 16u * i, v, nout - 16u * i);
+        }
+    }
+}
+
 template <int T2, int WPC = 3, int NBUF = 2, int NTST = 1, bool RM = (T2 == 32)>
 __global__ __launch_bounds__(NTHR, (WPC >= 5 ? 3 : 2)) void rs_pair_decode_kernel(uint8_t* __restrict__ raw,
     uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables,

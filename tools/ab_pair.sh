@@ -10,7 +10,7 @@ rc=$?; tail -2 gpurun_out/pair_t_$V.log; [ $rc -eq 0 ] || exit $rc
 for r in 1 2; do
 for v in new $V; do
   if [ $v = new ]; then L=$PWD/paritypartyfs_amd/_lib/libppfs_ecc.so; else L=$A; fi
-  PPFS_ECC_LIB=$L timeout -k 10 120 python tools/bench_configs.py --only t16 > gpurun_out/abpair_${v}_$r.log 2>&1 || exit 1
+  PPFS_ECC_LIB=$L timeout -k 10 120 python tools/bench_configs.py --only ${ONLY:-t16} > gpurun_out/abpair_${v}_$r.log 2>&1 || exit 1
 done
 done
 for f in gpurun_out/abpair_*; do echo $f; grep config $f | cut -c150-330; done
