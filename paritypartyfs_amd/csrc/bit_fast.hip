@@ -4,8 +4,8 @@
 // streaming; these kernels keep every byte's work to a few VALU ops so they run at the HBM rate.
 // One wave per block, NP = block_size / 1024 pieces of 16 B per lane, coalesced: lane l of a wave
 // holds raw bytes [16 (64 k + l), +16) for k < NP, i.e. big-endian raw words w = 256 k + 4 l + u.
-// Waves are persistent (grid-stride over blocks) and prefetch the next block into VGPRs while the
-// current one is computed.  Smaller blocks use bit_kernels.hip.
+// The grid covers the batch (one wave per block, workgroups dispatched in address order); see
+// BF_PREFETCH below.  Smaller blocks use bit_kernels.hip.
 //
 // Reference semantics (lib/blockdevice/src/hamming_block_device.cpp, MSB-first bit numbering of
 // lib/common/include/ppfs/common/bit_helpers.hpp:8-52):
@@ -58,6 +58,16 @@ __device__ __forceinline__ void gst16(uint8_t* p, uint4 v)
 }
 
 constexpr int WAVES = 4;
+// Grid and prefetch.  The kernels launch one wave per block over the whole batch (a full grid,
+// not a persistent one): the dispatcher then walks workgroups in address order, so the blocks in
+// flight form one contiguous window of HBM.  A persistent grid-stride walk spreads them over
+// gridDim x 4 KiB and ran 9-22 % slower on cfg4 (A/B in DESIGN.md section 4.3).  With one block
+// per wave the register prefetch of the next block is dead weight, so it is off by default
+// (loads at the loop end, which only runs for grids capped below the batch).
+#ifndef PPFS_BF_PREFETCH
+#define PPFS_BF_PREFETCH 0
+#endif
+constexpr bool BF_PREFETCH = PPFS_BF_PREFETCH;
 
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 
@@ -162,7 +172,7 @@ __global__ __launch_bounds__(256) void ham_fast_encode_kernel(const uint8_t* __r
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         const uint64_t nx = blk + stride;
-        if (nx < nblocks)
+        if (BF_PREFETCH && nx < nblocks)
             ham_stage_load<NP>(st, data, nx, a, lane); // lands while this block is computed
         const uint32_t m = (uint32_t)((blk * a.ds) & 15u); // payload byte 0 sits at LDS byte m
         uint8_t* rb = raw + blk * a.bs;
@@ -235,6 +245,8 @@ __global__ __launch_bounds__(256) void ham_fast_encode_kernel(const uint8_t* __r
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); // LDS reads done before the rewrite
         __builtin_amdgcn_wave_barrier();
+        if (!BF_PREFETCH && nx < nblocks)
+            ham_stage_load<NP>(st, data, nx, a, lane);
     }
 }
 
@@ -353,7 +365,7 @@ __global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restric
             X[k][3] = R[k].w;
         }
         const uint64_t nx = blk + stride;
-        if (nx < nblocks) {
+        if (BF_PREFETCH && nx < nblocks) {
 #pragma unroll
             for (int k = 0; k < NP; ++k)
                 R[k] = gld16(raw + nx * a.bs + 16u * (64u * k + lane));
@@ -450,6 +462,11 @@ __global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restric
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         (void)lastw;
+        if (!BF_PREFETCH && nx < nblocks) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                R[k] = gld16(raw + nx * a.bs + 16u * (64u * k + lane));
+        }
     }
 }
 
@@ -509,7 +526,7 @@ __global__ __launch_bounds__(256) void parity_fast_encode_kernel(const uint8_t* 
         ham_stage_load<NP>(cur, data, blk, ha, lane);
     for (; blk < nblocks; blk += stride) {
         const uint64_t nx = blk + stride;
-        if (nx < nblocks)
+        if (BF_PREFETCH && nx < nblocks)
             ham_stage_load<NP>(nxt, data, nx, ha, lane);
         const uint32_t m = (uint32_t)((blk * ds) & 15u);
         uint8_t* rb = raw + blk * a.bs;
@@ -539,7 +556,10 @@ __global__ __launch_bounds__(256) void parity_fast_encode_kernel(const uint8_t* 
                 gst16(rb + 16u * (64u * k + lane), o);
             }
         }
-        cur = nxt;
+        if (BF_PREFETCH)
+            cur = nxt;
+        else if (nx < nblocks)
+            ham_stage_load<NP>(cur, data, nx, ha, lane);
     }
 }
 
@@ -558,7 +578,7 @@ __global__ __launch_bounds__(256) void parity_fast_check_kernel(const uint8_t* _
             R[k] = gld16(raw + blk * a.bs + 16u * (64u * k + lane));
     for (; blk < nblocks; blk += stride) {
         const uint64_t nx = blk + stride;
-        if (nx < nblocks)
+        if (BF_PREFETCH && nx < nblocks)
 #pragma unroll
             for (int k = 0; k < NP; ++k)
                 N[k] = gld16(raw + nx * a.bs + 16u * (64u * k + lane));
@@ -603,9 +623,15 @@ __global__ __launch_bounds__(256) void parity_fast_check_kernel(const uint8_t* _
                 }
             }
         }
+        if (BF_PREFETCH) {
 #pragma unroll
-        for (int k = 0; k < NP; ++k)
-            R[k] = N[k];
+            for (int k = 0; k < NP; ++k)
+                R[k] = N[k];
+        } else if (nx < nblocks) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                R[k] = gld16(raw + nx * a.bs + 16u * (64u * k + lane));
+        }
     }
 }
 
@@ -715,7 +741,7 @@ __global__ __launch_bounds__(256) void crc_fast_encode_kernel(const uint8_t* __r
         ham_stage_load<NP>(cur, data, blk, ha, lane);
     for (; blk < nblocks; blk += stride) {
         const uint64_t nx = blk + stride;
-        if (nx < nblocks)
+        if (BF_PREFETCH && nx < nblocks)
             ham_stage_load<NP>(nxt, data, nx, ha, lane);
         const uint32_t m = (uint32_t)((blk * a.ds) & 15u); // payload byte 0 = superset byte m
         uint8_t* rb = raw + blk * a.bs;
@@ -768,7 +794,10 @@ __global__ __launch_bounds__(256) void crc_fast_encode_kernel(const uint8_t* __r
                 gst16(rb + 16u * (64u * k + lane), o);
             }
         }
-        cur = nxt;
+        if (BF_PREFETCH)
+            cur = nxt;
+        else if (nx < nblocks)
+            ham_stage_load<NP>(cur, data, nx, ha, lane);
     }
 }
 
@@ -793,7 +822,7 @@ __global__ __launch_bounds__(256) void crc_fast_check_kernel(const uint8_t* __re
             R[k] = gld16(raw + blk * a.bs + 16u * (64u * k + lane));
     for (; blk < nblocks; blk += stride) {
         const uint64_t nx = blk + stride;
-        if (nx < nblocks)
+        if (BF_PREFETCH && nx < nblocks)
 #pragma unroll
             for (int k = 0; k < NP; ++k)
                 N[k] = gld16(raw + nx * a.bs + 16u * (64u * k + lane));
@@ -849,9 +878,15 @@ __global__ __launch_bounds__(256) void crc_fast_check_kernel(const uint8_t* __re
                 }
             }
         }
+        if (BF_PREFETCH) {
 #pragma unroll
-        for (int k = 0; k < NP; ++k)
-            R[k] = N[k];
+            for (int k = 0; k < NP; ++k)
+                R[k] = N[k];
+        } else if (nx < nblocks) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                R[k] = gld16(raw + nx * a.bs + 16u * (64u * k + lane));
+        }
     }
 }
 
@@ -860,29 +895,12 @@ __global__ __launch_bounds__(256) void crc_fast_check_kernel(const uint8_t* __re
 
 using namespace ppfs;
 
-// Persistent grid = the kernel's resident workgroups per CU (occupancy query, i.e. what its
-// VGPR/LDS use allows) x CUs, capped by the work: a grid larger than what is resident would run
-// its last workgroups after the others finish.
-static int bf_cus()
+// Full grid: one wave per block, 4 blocks per 256-thread workgroup (see BF_PREFETCH above), capped
+// far above any batch a context stages (the kernels' loops then walk the rest).
+template <typename K> static uint32_t bf_grid(K, uint64_t nb)
 {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0, c = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
-            c = 256;
-        cus = c;
-    }
-    return cus;
-}
-
-template <typename K> static uint32_t bf_grid(K kernel, uint64_t nb)
-{
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0)
-        per_cu = 1;
     const uint64_t want = (nb + bf::WAVES - 1) / bf::WAVES;
-    const uint64_t cap = (uint64_t)per_cu * (uint64_t)bf_cus();
+    const uint64_t cap = 1ull << 30;
     return (uint32_t)(want < cap ? (want ? want : 1) : cap);
 }
 
