@@ -293,7 +293,21 @@ def main():
         cp_dst.copy_(cp_src)
     ev[5].record(stream)
     ev[5].synchronize()
-    copy_gbs = 2 * cp_src.numel() / (ev[4].elapsed_time(ev[5]) / 10 * 1e-3) / 1e9
+    torch_copy_gbs = 2 * cp_src.numel() / (ev[4].elapsed_time(ev[5]) / 10 * 1e-3) / 1e9
+    # the engine's full-grid 16-byte copy kernel (ppfs_copy_device): the HBM ceiling this access
+    # shape reaches, timed like the kernels (fence-free events on the launch stream, median)
+    from paritypartyfs_amd import device_copy
+
+    for _ in range(3):
+        device_copy(cp_dst, cp_src, stream=stream)
+    hc = HipEvents(20)
+    for i in range(10):
+        hc.record(2 * i, stream)
+        device_copy(cp_dst, cp_src, stream=stream)
+        hc.record(2 * i + 1, stream)
+    torch.cuda.synchronize()
+    copy_ms = float(np.median([hc.ms(2 * i, 2 * i + 1) for i in range(10)]))
+    copy_gbs = 2 * cp_src.numel() / (copy_ms * 1e-3) / 1e9
     del cp_src, cp_dst
 
     alg_per_block = k + n  # 504 B for RS(255,249), both for encode and decode
@@ -367,6 +381,8 @@ def main():
             "encode_GBps": round(alg_per_block * nb / (enc_avg * 1e-3) / 1e9, 1),
             "decode_GBps": round(alg_per_block * nb / (dec_avg * 1e-3) / 1e9, 1),
             "device_copy_GBps": round(copy_gbs, 1),
+            "device_copy_kernel": "ppfs_copy_device (full-grid 16-B copy, same bytes as one encode)",
+            "torch_copy_GBps": round(torch_copy_gbs, 1),
             # payload rate beside the algorithmic one, and the dominant kernel
             # against the device-to-device copy measured above
             "payload_GiBps": round(value * k / alg_per_block, 3),

@@ -164,6 +164,13 @@ int ppfs_vote3_host(int device, const uint8_t* a, const uint8_t* b, const uint8_
     size_t nrec, uint32_t* damaged);
 
 /*
+ * Device-to-device copy of `bytes` (any alignment) on `stream`: the measurement reference for
+ * the HBM roofline ("also measure a device-to-device copy kernel on the box and report
+ * both fractions").  Not a reference interface: full-grid 16-byte copy, see DESIGN.md section 5.
+ */
+int ppfs_copy_device(void* d_dst, const void* d_src, size_t bytes, void* stream);
+
+/*
  * Page-lock / release a caller buffer (hipHostRegister), e.g. the host mirror of a disk image
  * (replacing FileDisk's seekp + fstream I/O, lib/disk/src/file_disk.cpp:56-101,
  * by an mmap'd or resident image the *_host calls then DMA directly).

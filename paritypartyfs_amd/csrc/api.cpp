@@ -53,6 +53,7 @@ hipError_t ppfs_gather_rows_launch(const uint8_t* src, uint8_t* dst, const uint3
     uint32_t row_bytes, hipStream_t s);
 hipError_t ppfs_vote3_launch(const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* out, uint64_t rec_bytes,
     uint64_t nrec, uint32_t* damaged, hipStream_t s);
+hipError_t ppfs_copy_launch(uint8_t* dst, const uint8_t* src, uint64_t bytes, hipStream_t s);
 }
 
 namespace {
@@ -1228,6 +1229,13 @@ extern "C" int ppfs_vote3_device(const uint8_t* d_a, const uint8_t* d_b, const u
     if (nrec && !rec_bytes)
         return fail(PPFS_ECC_EINVAL, "vote3: zero record size");
     return check_hip(ppfs_vote3_launch(d_a, d_b, d_c, d_out, rec_bytes, nrec, d_damaged, (hipStream_t)stream), "vote3");
+}
+
+extern "C" int ppfs_copy_device(void* d_dst, const void* d_src, size_t bytes, void* stream)
+{
+    if (bytes && (!d_dst || !d_src))
+        return fail(PPFS_ECC_EINVAL, "copy: null argument");
+    return check_hip(ppfs_copy_launch((uint8_t*)d_dst, (const uint8_t*)d_src, bytes, (hipStream_t)stream), "copy");
 }
 
 extern "C" int ppfs_vote3_host(int device, const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* out,

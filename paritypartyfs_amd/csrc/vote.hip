@@ -67,6 +67,43 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* __restr
 }
 } // namespace ppfs
 
+// ---- device copy at the HBM ceiling (measurement reference for bench.py's roofline) ----
+// One thread per 16 bytes over a full grid (workgroups dispatched in address order: one
+// contiguous window of HBM in flight), plain 16-byte loads and stores; ragged ends by bytes.
+// The same shape reached 6.26 TB/s on 8.6 GB (tools/stream_ablate4.hip).
+namespace ppfs {
+__global__ __launch_bounds__(256) void copy16_kernel(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+    uint64_t n16, uint64_t head, uint64_t bytes)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n16)
+        *(uint4*)(dst + head + 16 * i) = *(const uint4*)(src + head + 16 * i);
+    if (i < head)
+        dst[i] = src[i];
+    const uint64_t tail0 = head + 16 * n16;
+    if (i < bytes - tail0)
+        dst[tail0 + i] = src[tail0 + i];
+}
+} // namespace ppfs
+
+extern "C" hipError_t ppfs_copy_launch(uint8_t* dst, const uint8_t* src, uint64_t bytes, hipStream_t s)
+{
+    if (bytes == 0)
+        return hipSuccess;
+    // 16-byte body where src and dst share their alignment, bytes elsewhere
+    uint64_t head = ((uintptr_t)src ^ (uintptr_t)dst) & 15u ? bytes : ((16u - ((uintptr_t)src & 15u)) & 15u);
+    if (head > bytes)
+        head = bytes;
+    const uint64_t n16 = (bytes - head) / 16;
+    const uint64_t tail = bytes - head - 16 * n16;
+    const uint64_t work = n16 > head ? (n16 > tail ? n16 : tail) : (head > tail ? head : tail);
+    const uint64_t grid = (work + 255) / 256;
+    if (grid > 0x7FFFFFFFull)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(ppfs::copy16_kernel, dim3((uint32_t)grid), dim3(256), 0, s, dst, src, n16, head, bytes);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t ppfs_gather_rows_launch(const uint8_t* src, uint8_t* dst, const uint32_t* idx, uint32_t nrows,
     uint32_t row_bytes, hipStream_t s)
 {

@@ -208,9 +208,18 @@ def vote3(a, b, c, out, rec_bytes: int, damaged=None, stream=None) -> None:
                                   _stream_handle(stream)))
 
 
+def device_copy(dst, src, nbytes: Optional[int] = None, stream=None) -> None:
+    """dst[:nbytes] = src[:nbytes] on the device (torch uint8 tensors): the full-grid copy kernel
+    bench.py times as the HBM ceiling next to the roofline (not part of the reference interface)."""
+    n = int(src.numel() if nbytes is None else nbytes)
+    if n > dst.numel() or n > src.numel():
+        raise ValueError("device_copy: nbytes exceeds a buffer")
+    check(lib().ppfs_copy_device(_ptr(dst), _ptr(src), n, _stream_handle(stream)))
+
+
 def crc_implicit_to_explicit(p: int) -> int:
     """CrcPolynomial::MsgImplicit (crc_polynomial.cpp:41-54) -> explicit form."""
     return int(lib().ppfs_ecc_crc_implicit_to_explicit(ctypes.c_uint64(p)))
 
 
-__all__ = ["EccEngine", "crc_implicit_to_explicit", "pinned", "vote3", "vote3_host", "_native"]
+__all__ = ["EccEngine", "crc_implicit_to_explicit", "device_copy", "pinned", "vote3", "vote3_host", "_native"]

@@ -180,3 +180,24 @@ def test_block_device_scrub_matches_reads(oracle):
         assert np.array_equal(disk.buf, od.disk)
         assert [x[1] for x in log.corrections] == od.log_entries()
         assert ok + corrected + failed == nb and corrected == len(log.corrections)
+
+
+@pytest.mark.gpu
+def test_device_copy_ragged():
+    """ppfs_copy_device (bench.py's HBM-ceiling reference): every alignment of source and
+    destination, sizes around the 16-byte body, bytes outside the range untouched."""
+    import torch
+
+    from paritypartyfs_amd import device_copy
+
+    rng = np.random.default_rng(11)
+    src = torch.from_numpy(rng.integers(0, 256, 1 << 16, dtype=np.uint8)).cuda()
+    for so, do, n in [(0, 0, 0), (0, 0, 1), (0, 0, 16), (0, 0, 65536 - 64), (3, 3, 1000), (5, 1, 4099),
+                      (15, 15, 17), (1, 0, 31), (7, 9, 60000), (0, 8, 48)]:
+        dst = torch.full((1 << 16,), 0xA5, dtype=torch.uint8, device="cuda")
+        device_copy(dst[do:], src[so:], n)
+        torch.cuda.synchronize()
+        d = dst.cpu().numpy()
+        s = src.cpu().numpy()
+        assert np.array_equal(d[do:do + n], s[so:so + n]), (so, do, n)
+        assert (d[:do] == 0xA5).all() and (d[do + n:] == 0xA5).all(), (so, do, n)
