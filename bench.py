@@ -94,7 +94,7 @@ def cpu_baseline(bs, t, nblocks, seed=1234):
         "unit": "GiB/s",
         "cores": cores,
         "kind": "port",
-        "sample": f"{nblocks} RS(255,249) blocks: encode + 1-byte-error decode, oracle/ppfs_oracle.c "
+        "sample": f"{nblocks} RS({n},{k}) blocks: encode + 1-byte-error decode, oracle/ppfs_oracle.c "
                   f"on {cores} host threads over disjoint block ranges",
         "encode_blocks_per_s": round(nblocks / t_enc),
         "decode_blocks_per_s": round(nblocks / t_dec),
@@ -311,13 +311,27 @@ def main():
     del cp_src, cp_dst
 
     alg_per_block = k + n  # 504 B for RS(255,249), both for encode and decode
+    if (args.block_size, args.t) == (512, 3):
+        cfg_ref = "BASELINE configs[1]+[2]"
+    elif (args.block_size, args.t) == (4096, 16):
+        cfg_ref = "BASELINE configs[4], one GPU's shard"
+    else:
+        cfg_ref = "not a BASELINE config"
     total_bytes = 2 * alg_per_block * nb * world * args.steps
     value = total_bytes / elapsed / GIB
     ms_per_step = elapsed / args.steps * 1e3
 
     dom_ms = max(enc_avg, dec_avg)
-    fam = "rs_wg" if eng.kernel_name.startswith("rs255-wg") else "rs255"
-    dom_name = f"{fam}_{'decode' if dec_avg >= enc_avg else 'encode'}_kernel<{n - k}>"
+    which = "decode" if dec_avg >= enc_avg else "encode"
+    kn = eng.kernel_name
+    if kn.startswith("rs255-wg"):
+        dom_name = f"rs_wg_{which}_kernel<{n - k}>"
+    elif kn.startswith("rs255-pair"):  # 16 < 2t <= 32 (rs_pair.hpp)
+        dom_name = f"rs_pair_{'decode' if which == 'decode' else 'encode_img'}_kernel<{n - k}>"
+    elif kn.startswith("rs255-slice8") and which == "encode" and n - k == 16:
+        dom_name = f"rs_solo_encode_img_kernel<{n - k}>"
+    else:
+        dom_name = f"rs255_{which}_kernel<{n - k}>"
     achieved = alg_per_block * nb / (dom_ms * 1e-3) / 1e9
     traffic = None
     pmc = load_traffic()
@@ -359,8 +373,8 @@ def main():
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": f"RS(255,{k}) t={args.t} block_size={args.block_size}: encode + 1-byte-error "
-                            f"inject + decode with write-back, {nb} blocks per GPU (BASELINE configs[1]+[2])",
+                "workload": f"RS({n},{k}) t={args.t} block_size={args.block_size}: encode + 1-byte-error "
+                            f"inject + decode with write-back, {nb} blocks per GPU ({cfg_ref})",
                 "blocks_per_gpu": nb,
                 "global_blocks": nb * world,
                 "parallelism": f"shard{world}",
