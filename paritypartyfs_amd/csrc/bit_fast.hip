@@ -68,6 +68,12 @@ constexpr int WAVES = 4;
 #define PPFS_BF_PREFETCH 0
 #endif
 constexpr bool BF_PREFETCH = PPFS_BF_PREFETCH;
+// Blocks per wave of the Hamming / parity kernels: a workgroup walks BF_BPW consecutive 4-block
+// groups (one contiguous range, so the grid keeps its address order).
+#ifndef PPFS_BF_BPW
+#define PPFS_BF_BPW 1
+#endif
+constexpr int BF_BPW = PPFS_BF_BPW;
 
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 
@@ -155,15 +161,17 @@ __device__ __forceinline__ void ham_stage_write(uint8_t* buf, const HamEncStage<
 
 template <int NP>
 __global__ __launch_bounds__(256) void ham_fast_encode_kernel(const uint8_t* __restrict__ data, uint8_t* __restrict__ raw,
-    const uint8_t* __restrict__ skip, uint64_t nblocks, HamFast a)
+    const uint8_t* __restrict__ skip, uint64_t nblocks_all, HamFast a)
 {
     constexpr int BUF = (NP + 1) * 1024 + 32; // NP + 1 staged pieces per lane + read slack
     __shared__ __attribute__((aligned(16))) uint8_t lds[WAVES * BUF];
     const uint32_t lane = lane_id(), wave = wave_id();
     uint8_t* buf = lds + wave * BUF;
     const uint32_t nwords = a.bs / 4, lastw = nwords - 1;
-    const uint64_t stride = (uint64_t)gridDim.x * WAVES;
-    uint64_t blk = (uint64_t)blockIdx.x * WAVES + wave;
+    const uint64_t wg0 = (uint64_t)blockIdx.x * (WAVES * BF_BPW);
+    const uint64_t nblocks = nblocks_all < wg0 + WAVES * BF_BPW ? nblocks_all : wg0 + WAVES * BF_BPW;
+    const uint64_t stride = WAVES;
+    uint64_t blk = wg0 + wave;
     HamEncStage<NP> st;
     if (blk < nblocks)
         ham_stage_load<NP>(st, data, blk, a, lane);
@@ -340,15 +348,17 @@ __device__ __forceinline__ void ham_mid_piece(const uint8_t* img, uint32_t b0, u
 
 template <int NP>
 __global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
-    uint8_t* __restrict__ status, uint64_t nblocks, int write_back, HamFast a)
+    uint8_t* __restrict__ status, uint64_t nblocks_all, int write_back, HamFast a)
 {
     constexpr int BUF = NP * 1024 + 16; // raw image + zero slack
     __shared__ __attribute__((aligned(16))) uint8_t lds[WAVES * BUF];
     const uint32_t lane = lane_id(), wave = wave_id();
     uint8_t* img = lds + wave * BUF;
     const uint32_t lastw = a.bs / 4 - 1;
-    const uint64_t stride = (uint64_t)gridDim.x * WAVES;
-    uint64_t blk = (uint64_t)blockIdx.x * WAVES + wave;
+    const uint64_t wg0 = (uint64_t)blockIdx.x * (WAVES * BF_BPW);
+    const uint64_t nblocks = nblocks_all < wg0 + WAVES * BF_BPW ? nblocks_all : wg0 + WAVES * BF_BPW;
+    const uint64_t stride = WAVES;
+    uint64_t blk = wg0 + wave;
     uint4 R[NP];
     if (blk < nblocks) {
 #pragma unroll
@@ -514,13 +524,15 @@ struct ParFast {
 
 template <int NP>
 __global__ __launch_bounds__(256) void parity_fast_encode_kernel(const uint8_t* __restrict__ data,
-    uint8_t* __restrict__ raw, const uint8_t* __restrict__ skip, uint64_t nblocks, ParFast a)
+    uint8_t* __restrict__ raw, const uint8_t* __restrict__ skip, uint64_t nblocks_all, ParFast a)
 {
     const uint32_t lane = lane_id(), wave = wave_id();
     const uint32_t ds = a.bs - 1;
     const HamFast ha { a.bs, ds, 0, a.data_bytes };
-    const uint64_t stride = (uint64_t)gridDim.x * WAVES;
-    uint64_t blk = (uint64_t)blockIdx.x * WAVES + wave;
+    const uint64_t wg0 = (uint64_t)blockIdx.x * (WAVES * BF_BPW);
+    const uint64_t nblocks = nblocks_all < wg0 + WAVES * BF_BPW ? nblocks_all : wg0 + WAVES * BF_BPW;
+    const uint64_t stride = WAVES;
+    uint64_t blk = wg0 + wave;
     HamEncStage<NP> cur, nxt;
     if (blk < nblocks)
         ham_stage_load<NP>(cur, data, blk, ha, lane);
@@ -565,12 +577,14 @@ __global__ __launch_bounds__(256) void parity_fast_encode_kernel(const uint8_t* 
 
 template <int NP>
 __global__ __launch_bounds__(256) void parity_fast_check_kernel(const uint8_t* __restrict__ raw,
-    uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks, ParFast a)
+    uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks_all, ParFast a)
 {
     const uint32_t lane = lane_id(), wave = wave_id();
     const uint32_t ds = a.bs - 1;
-    const uint64_t stride = (uint64_t)gridDim.x * WAVES;
-    uint64_t blk = (uint64_t)blockIdx.x * WAVES + wave;
+    const uint64_t wg0 = (uint64_t)blockIdx.x * (WAVES * BF_BPW);
+    const uint64_t nblocks = nblocks_all < wg0 + WAVES * BF_BPW ? nblocks_all : wg0 + WAVES * BF_BPW;
+    const uint64_t stride = WAVES;
+    uint64_t blk = wg0 + wave;
     uint4 R[NP], N[NP];
     if (blk < nblocks)
 #pragma unroll
@@ -649,6 +663,13 @@ __global__ __launch_bounds__(256) void parity_fast_check_kernel(const uint8_t* _
 constexpr int CF_MAP = 512;                      // 8 nibbles x 16 entries x u32
 constexpr int CF_M0 = 0, CF_K = 4, CF_L = 5, CF_FENC = 11, CF_FCHK = 27, CF_NMAPS = 28;
 constexpr int CF_BYTES = CF_NMAPS * CF_MAP;     // 14 KiB
+// Blocks per wave of the CRC kernels: a workgroup stages the 14 KiB of maps once and then walks
+// CRC_BPW consecutive 4-block groups (one contiguous range, so the full grid keeps its address
+// order); with one group per workgroup the map staging read as much L2 as the blocks themselves.
+#ifndef PPFS_CRC_BPW
+#define PPFS_CRC_BPW 8
+#endif
+constexpr int CRC_BPW = PPFS_CRC_BPW;
 
 // (x >> 8k) & 0x3C (a nibble * 4, the entry's byte offset): one v_and_b32_sdwa for k > 0
 __device__ __forceinline__ uint32_t sel3c(uint32_t x, int k)
@@ -724,7 +745,7 @@ __device__ __forceinline__ uint32_t crc_lane_tree(const uint8_t* tbl, uint32_t a
 
 template <int NP>
 __global__ __launch_bounds__(256) void crc_fast_encode_kernel(const uint8_t* __restrict__ data,
-    uint8_t* __restrict__ raw, const uint8_t* __restrict__ skip, uint64_t nblocks, CrcFast a,
+    uint8_t* __restrict__ raw, const uint8_t* __restrict__ skip, uint64_t nblocks_all, CrcFast a,
     const uint8_t* __restrict__ tables)
 {
     __shared__ __attribute__((aligned(16))) uint8_t tbl[CF_BYTES];
@@ -734,8 +755,10 @@ __global__ __launch_bounds__(256) void crc_fast_encode_kernel(const uint8_t* __r
     const uint32_t lane = lane_id(), wave = wave_id();
     const HamFast ha { a.bs, a.ds, 0, a.data_bytes };
     const bool n32 = a.n == 32;
-    const uint64_t stride = (uint64_t)gridDim.x * WAVES;
-    uint64_t blk = (uint64_t)blockIdx.x * WAVES + wave;
+    const uint64_t wg0 = (uint64_t)blockIdx.x * (WAVES * CRC_BPW);
+    const uint64_t nblocks = nblocks_all < wg0 + WAVES * CRC_BPW ? nblocks_all : wg0 + WAVES * CRC_BPW;
+    const uint64_t stride = WAVES;
+    uint64_t blk = wg0 + wave;
     HamEncStage<NP> cur, nxt;
     if (blk < nblocks)
         ham_stage_load<NP>(cur, data, blk, ha, lane);
@@ -803,7 +826,7 @@ __global__ __launch_bounds__(256) void crc_fast_encode_kernel(const uint8_t* __r
 
 template <int NP>
 __global__ __launch_bounds__(256) void crc_fast_check_kernel(const uint8_t* __restrict__ raw,
-    uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks, CrcFast a,
+    uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks_all, CrcFast a,
     const uint8_t* __restrict__ tables)
 {
     __shared__ __attribute__((aligned(16))) uint8_t tbl[CF_BYTES];
@@ -813,8 +836,10 @@ __global__ __launch_bounds__(256) void crc_fast_check_kernel(const uint8_t* __re
     const uint32_t lane = lane_id(), wave = wave_id();
     const bool n32 = a.n == 32;
     const uint32_t ds = a.ds;
-    const uint64_t stride = (uint64_t)gridDim.x * WAVES;
-    uint64_t blk = (uint64_t)blockIdx.x * WAVES + wave;
+    const uint64_t wg0 = (uint64_t)blockIdx.x * (WAVES * CRC_BPW);
+    const uint64_t nblocks = nblocks_all < wg0 + WAVES * CRC_BPW ? nblocks_all : wg0 + WAVES * CRC_BPW;
+    const uint64_t stride = WAVES;
+    uint64_t blk = wg0 + wave;
     uint4 R[NP], N[NP];
     if (blk < nblocks)
 #pragma unroll
@@ -923,7 +948,9 @@ extern "C" hipError_t ppfs_ham_fast_encode(const uint8_t* d, uint8_t* r, const u
     uint32_t ds, uint32_t L, hipStream_t s)
 {
     const bf::HamFast a { bs, ds, L, nb * (uint64_t)ds };
-    PPFS_NP_DISPATCH(bs, bf::ham_fast_encode_kernel, nb, s, d, r, skip, nb, a)
+    if ((nb + 4ull * bf::BF_BPW - 1) / (4ull * bf::BF_BPW) > (1ull << 30))
+        return hipErrorInvalidValue;
+    PPFS_NP_DISPATCH(bs, bf::ham_fast_encode_kernel, (nb + bf::BF_BPW - 1) / bf::BF_BPW, s, d, r, skip, nb, a)
     return hipGetLastError();
 }
 
@@ -931,7 +958,9 @@ extern "C" hipError_t ppfs_ham_fast_decode(uint8_t* r, uint8_t* d, uint8_t* st, 
     uint32_t ds, uint32_t L, hipStream_t s)
 {
     const bf::HamFast a { bs, ds, L, nb * (uint64_t)ds };
-    PPFS_NP_DISPATCH(bs, bf::ham_fast_decode_kernel, nb, s, r, d, st, nb, wb, a)
+    if ((nb + 4ull * bf::BF_BPW - 1) / (4ull * bf::BF_BPW) > (1ull << 30))
+        return hipErrorInvalidValue;
+    PPFS_NP_DISPATCH(bs, bf::ham_fast_decode_kernel, (nb + bf::BF_BPW - 1) / bf::BF_BPW, s, r, d, st, nb, wb, a)
     return hipGetLastError();
 }
 
@@ -941,7 +970,9 @@ extern "C" hipError_t ppfs_crc_fast_encode(const uint8_t* d, uint8_t* r, const u
     uint32_t ds, uint32_t n, uint64_t mask, const uint8_t* tab, hipStream_t s)
 {
     const bf::CrcFast a { bs, ds, n, bs - ds, (uint32_t)mask, nb * (uint64_t)ds };
-    PPFS_NP_DISPATCH(bs, bf::crc_fast_encode_kernel, nb, s, d, r, skip, nb, a, tab)
+    if ((nb + 4ull * bf::CRC_BPW - 1) / (4ull * bf::CRC_BPW) > (1ull << 30))
+        return hipErrorInvalidValue;
+    PPFS_NP_DISPATCH(bs, bf::crc_fast_encode_kernel, (nb + bf::CRC_BPW - 1) / bf::CRC_BPW, s, d, r, skip, nb, a, tab)
     return hipGetLastError();
 }
 
@@ -949,7 +980,9 @@ extern "C" hipError_t ppfs_crc_fast_check(const uint8_t* r, uint8_t* d, uint8_t*
     uint32_t ds, uint32_t n, uint64_t mask, const uint8_t* tab, hipStream_t s)
 {
     const bf::CrcFast a { bs, ds, n, bs - ds, (uint32_t)mask, nb * (uint64_t)ds };
-    PPFS_NP_DISPATCH(bs, bf::crc_fast_check_kernel, nb, s, r, d, st, nb, a, tab)
+    if ((nb + 4ull * bf::CRC_BPW - 1) / (4ull * bf::CRC_BPW) > (1ull << 30))
+        return hipErrorInvalidValue;
+    PPFS_NP_DISPATCH(bs, bf::crc_fast_check_kernel, (nb + bf::CRC_BPW - 1) / bf::CRC_BPW, s, r, d, st, nb, a, tab)
     return hipGetLastError();
 }
 
@@ -957,7 +990,9 @@ extern "C" hipError_t ppfs_parity_fast_encode(const uint8_t* d, uint8_t* r, cons
     uint32_t bs, hipStream_t s)
 {
     const bf::ParFast a { bs, nb * (uint64_t)(bs - 1) };
-    PPFS_NP_DISPATCH(bs, bf::parity_fast_encode_kernel, nb, s, d, r, skip, nb, a)
+    if ((nb + 4ull * bf::BF_BPW - 1) / (4ull * bf::BF_BPW) > (1ull << 30))
+        return hipErrorInvalidValue;
+    PPFS_NP_DISPATCH(bs, bf::parity_fast_encode_kernel, (nb + bf::BF_BPW - 1) / bf::BF_BPW, s, d, r, skip, nb, a)
     return hipGetLastError();
 }
 
@@ -965,6 +1000,8 @@ extern "C" hipError_t ppfs_parity_fast_check(const uint8_t* r, uint8_t* d, uint8
     hipStream_t s)
 {
     const bf::ParFast a { bs, nb * (uint64_t)(bs - 1) };
-    PPFS_NP_DISPATCH(bs, bf::parity_fast_check_kernel, nb, s, r, d, st, nb, a)
+    if ((nb + 4ull * bf::BF_BPW - 1) / (4ull * bf::BF_BPW) > (1ull << 30))
+        return hipErrorInvalidValue;
+    PPFS_NP_DISPATCH(bs, bf::parity_fast_check_kernel, (nb + bf::BF_BPW - 1) / bf::BF_BPW, s, r, d, st, nb, a)
     return hipGetLastError();
 }
