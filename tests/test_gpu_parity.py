@@ -268,7 +268,7 @@ def test_crc_encode_check_match_oracle(oracle, imp, bs):
     assert (eng.raw_block_size, eng.data_size) == (bs, ds)
     nb = 257 if bs >= 1024 else 1001
     if (imp, bs) == (0x9960034c, 4096):
-        nb = 5003  # persistent waves walk several blocks; ragged last block
+        nb = 5003  # workgroups walk 32 blocks (CRC_BPW = 8): a ragged last workgroup
     rng = rng_for("crc", imp, bs)
     data = rng.integers(0, 256, nb * ds, dtype=np.uint8)
     old = rng.integers(0, 256, nb * bs, dtype=np.uint8)  # tail bits must survive
@@ -606,3 +606,28 @@ def test_group_host_path_matches_single_context(oracle, devices, codec):
         res.append((img, st))
     assert np.array_equal(res[0][0], res[1][0]) and np.array_equal(res[0][1], res[1][1])
     grp.close()
+
+
+@pytest.mark.parametrize("nb", [1, 3, 31, 33, 129])
+def test_crc4096_small_batches_match_oracle(oracle, nb):
+    """The CRC streaming kernels cover 32 blocks per workgroup: batches below, at and just past
+    one workgroup's range (and across several) match the oracle, encode and check."""
+    P = oracle.crc_explicit(0x9960034C)
+    eng = EccEngine(ECC_CRC, 4096, crc_polynomial_explicit=P)
+    ds = eng.data_size
+    rng = rng_for("crc-small", nb)
+    data = rng.integers(0, 256, nb * ds, dtype=np.uint8)
+    old = rng.integers(0, 256, nb * 4096, dtype=np.uint8)
+    raw_d = dev(old)
+    eng.encode(dev(data), raw_d, nblocks=nb)
+    got = host(raw_d)
+    assert np.array_equal(got, oracle.crc_encode(4096, P, data, raw_old=old))
+    bad = got.reshape(nb, 4096).copy()
+    bad[::2, 100] ^= 0x10
+    bad = bad.reshape(-1)
+    o_data, o_st = oracle.crc_check(4096, P, bad)
+    data_d = torch.zeros(nb * ds, dtype=torch.uint8, device="cuda")
+    st_d = torch.full((nb,), 77, dtype=torch.uint8, device="cuda")
+    eng.decode(dev(bad), data_d, st_d, nblocks=nb)
+    assert np.array_equal(host(st_d), o_st)
+    assert np.array_equal(host(data_d), o_data)
