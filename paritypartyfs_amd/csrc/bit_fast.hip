@@ -36,8 +36,9 @@ namespace bf {
 #endif
 typedef unsigned int bf_u32x4 __attribute__((ext_vector_type(4)));
 // streamed global traffic: every block is read once and written once.  Non-temporal variants
-// (build knobs) measured within +-3 % of plain loads / stores on cfg4 (bs 4096, 2^20 blocks):
-// NT stores 1-2 % faster on encode, 2-4 % slower on decode -- plain is the default.
+// (build knobs) on cfg4 (bs 4096, 2^20 blocks): NT loads 0-7 % slower everywhere; NT stores 1-3 %
+// faster on encode, 4-5 % slower on decode -- the encode outputs use them (gst16_raw below),
+// everything else is plain.
 __device__ __forceinline__ uint4 gld16(const uint8_t* p)
 {
     if constexpr (PPFS_BF_NTLD) {
@@ -54,6 +55,22 @@ __device__ __forceinline__ void gst16(uint8_t* p, uint4 v)
         __builtin_nontemporal_store(u, (bf_u32x4*)p);
     } else {
         *(uint4*)p = v;
+    }
+}
+
+// Encode outputs (whole raw blocks) use non-temporal stores: on the full grid (r1l A/B) they cut
+// Hamming encode 1.51 -> 1.46 ms and parity 1.59 -> 1.55 ms, while the same stores on the decode
+// outputs cost 4-5 %, so decode / check keep gst16's plain stores.
+#ifndef PPFS_BF_ENC_NTST
+#define PPFS_BF_ENC_NTST 1
+#endif
+__device__ __forceinline__ void gst16_raw(uint8_t* p, uint4 v)
+{
+    if constexpr (PPFS_BF_ENC_NTST) {
+        const bf_u32x4 u = { v.x, v.y, v.z, v.w };
+        __builtin_nontemporal_store(u, (bf_u32x4*)p);
+    } else {
+        gst16(p, v);
     }
 }
 
@@ -247,7 +264,7 @@ __global__ __launch_bounds__(256) void ham_fast_encode_kernel(const uint8_t* __r
                     const uint32_t keep = ~top_bits(a.L - 32 * lastw + 1);
                     X[k][3] = (X[k][3] & ~keep) | (old_tail & keep);
                 }
-                gst16(rb + 16u * (64u * k + lane),
+                gst16_raw(rb + 16u * (64u * k + lane),
                     make_uint4(bswap(X[k][0]), bswap(X[k][1]), bswap(X[k][2]), bswap(X[k][3])));
             }
         }
@@ -565,7 +582,7 @@ __global__ __launch_bounds__(256) void parity_fast_encode_kernel(const uint8_t* 
                 uint4 o = O[k];
                 if (k == NP - 1 && lane == 63)
                     o.w ^= odd << 24; // LSB of the last byte fixes the parity
-                gst16(rb + 16u * (64u * k + lane), o);
+                gst16_raw(rb + 16u * (64u * k + lane), o);
             }
         }
         if (BF_PREFETCH)
@@ -814,7 +831,7 @@ __global__ __launch_bounds__(256) void crc_fast_encode_kernel(const uint8_t* __r
                     }
                     o = make_uint4(w[0], w[1], w[2], w[3]);
                 }
-                gst16(rb + 16u * (64u * k + lane), o);
+                gst16_raw(rb + 16u * (64u * k + lane), o);
             }
         }
         if (BF_PREFETCH)
