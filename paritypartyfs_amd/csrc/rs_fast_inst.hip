@@ -101,6 +101,13 @@ constexpr bool SOLO_IMG = PPFS_SOLO_IMG && PPFS_T2 == 16;
 constexpr int SOLO_NW = PPFS_SOLO_NW, SOLO_WPC = PPFS_SOLO_WPC;
 #endif
 
+// pair decode grid: 1 = one workgroup per 64-block tile (workgroups dispatched in address order;
+// 1-error decode 0.203 -> 0.190 ms per 2^20 blocks, clean decode unchanged: DESIGN.md 4.1b),
+// 0 = persistent, PAIR_DEC_WPC per CU
+#ifndef PPFS_PAIR_DEC_FULL
+#define PPFS_PAIR_DEC_FULL 1
+#endif
+
 extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d, uint8_t* r, uint64_t nb,
     const uint8_t* tab, hipStream_t s)
 {
@@ -131,7 +138,8 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
     hipLaunchKernelGGL((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC, 7, PPFS_DEC_NTST>), dim3(rs_tile_grid(nb, DEC_WPC)), dim3(256),
         0, s, r, d, st, nb, tab, wb);
 #elif PPFS_T2 > 16
-    hipLaunchKernelGGL((pair::rs_pair_decode_kernel<PPFS_T2, PPFS_PAIR_DEC>), dim3(rs_tile_grid(nb, PAIR_DEC_WPC)),
+    hipLaunchKernelGGL((pair::rs_pair_decode_kernel<PPFS_T2, PPFS_PAIR_DEC>),
+        dim3(rs_tile_grid(nb, PPFS_PAIR_DEC_FULL ? (1 << 24) : PAIR_DEC_WPC)),
         dim3(pair::NTHR), 0, s, r, d, st, nb, tab, wb);
 #else
     hipLaunchKernelGGL(rs255_decode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, r, d, st, nb, tab, wb);
