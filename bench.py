@@ -4,21 +4,29 @@
 Workload (BASELINE.json configs[1]/[2]): ecc_type=reed_solomon, block_size=512,
 rs_correctable_bytes=3 -> RS(255,249) (the reference clamps codewords to 255 B,
 rs_block_device.cpp:57), 2^20 blocks per GPU, synthetic uniform payloads.
+`--block-size 4096 --t 16` runs configs[4]'s RS(255,223) shard instead (2^20 blocks per GPU).
 
 One step = encode(2^20 payloads -> codewords)            [rs255 encode kernel]
          + inject exactly one byte error into every codeword (one torch scatter of wrong bytes)
          + decode(codewords -> payloads, status, in-place write-back)   [rs255 decode kernel]
-value = algorithmic bytes of all ranks (encode 504 B + decode 504 B per block) / step time.
+value = algorithmic bytes of all ranks (encode k+n B + decode n+k B per block) / step time.
 
-Multi-GPU: one process per GPU (torchrun).  Blocks are independent, so each rank owns its own
-2^20-block shard ("scaling": "weak"); the only collectives are the barrier around the timed
-region and the max-over-ranks of the elapsed time (not on the data path).
+Multi-GPU: one process per GPU.  `python bench.py --gpus N` (N > 1, no torchrun env) starts
+`torch.distributed.run` with N ranks as a child process before anything touches a GPU and exits
+with its code; under torchrun (WORLD_SIZE set) each rank runs its own shard.  Blocks are
+independent, so every rank owns a 2^20-block shard ("scaling": "weak"); the only collectives are
+the barrier around the timed region and the max-over-ranks of the elapsed time (not on the data
+path).  `--dry-run-cpu` replaces the engine by a CPU stand-in (gloo, no GPU) to exercise exactly
+this launch / timing path in tests; its numbers are not measurements.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,83 +37,129 @@ sys.path.insert(0, ROOT)
 
 GIB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "device-resident GiB/s: RS encode+decode, 512 B blocks, 1 M-block batch"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--graph-steps", type=int, default=10, help="steps captured per hipGraph")
+    ap.add_argument("--gpus", type=int, default=None, help="GPUs (ranks); default: WORLD_SIZE or 1")
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--launch", choices=("eager", "graph"), default="eager",
+                    help="eager launches (default) or one hipGraph per --graph-steps steps")
+    ap.add_argument("--graph-steps", type=int, default=10, help="steps captured per hipGraph (--launch graph)")
     ap.add_argument("--blocks", type=int, default=1 << 20, help="blocks per GPU")
     ap.add_argument("--block-size", type=int, default=512)
     ap.add_argument("--t", type=int, default=3)
     ap.add_argument("--prewarm-s", type=float, default=1.0, help="untimed clock ramp before the warmup steps")
-    ap.add_argument("--no-graph", dest="graph", action="store_false", help="eager launches instead of one hipGraph per step")
+    ap.add_argument("--standalone-launches", type=int, default=30, help="back-to-back launches per kernel")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-blocks", type=int, default=1 << 18)
-    ap.add_argument("--host-inclusive", action="store_true", help="also time the pinned H2D+kernel+D2H path")
-    ap.add_argument("--verify", action="store_true", help="check a sample of outputs against the oracle")
-    return ap.parse_args()
+    ap.add_argument("--cpu-sample-blocks", type=int, default=1 << 20)
+    ap.add_argument("--cpu-faithful-blocks", type=int, default=1 << 18)
+    ap.add_argument("--no-host-inclusive", dest="host_inclusive", action="store_false",
+                    help="skip the H2D + kernel + D2H leg (rank 0, N=1)")
+    ap.add_argument("--dry-run-cpu", action="store_true", help="CPU stand-in for the engine (launcher tests)")
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(bs, t, nblocks, seed=1234):
-    """Oracle ('port') timed on host cores over a bounded sample (rank 0, N=1 only)."""
+# ------------------------------------------------------------------------------------------
+# launcher: N ranks as a child process (nothing has touched a GPU yet)
+# ------------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(nranks: int, argv) -> int:
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nranks}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+# ------------------------------------------------------------------------------------------
+# CPU baseline (rank 0, N = 1): the oracle on the host cores
+# ------------------------------------------------------------------------------------------
+def _pool_time(fn, nparts):
     from concurrent.futures import ThreadPoolExecutor
 
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(nparts) as ex:
+        res = list(ex.map(fn, range(nparts)))
+    return time.perf_counter() - t0, res
+
+
+def cpu_baseline(bs, t, nblocks, nfaithful, seed=1234):
+    """Two CPU columns on the same synthetic workload (encode, then a 1-byte-error decode), one
+    thread per core over disjoint block ranges (the ctypes calls release the GIL):
+      value / "port": the oracle's table-driven codec (LFSR encode, table syndromes; blocks with
+          a non-zero syndrome run the restated reference decode) -- the strong CPU baseline;
+      "faithful": the oracle's reference-faithful restatement (schoolbook long-division encode,
+          Horner syndromes, BM / 255-point root search / Forney), SURVEY 8(d)'s
+          "reference-faithful variant", on a smaller sample."""
     from tests.oracle_lib import Oracle
 
     o = Oracle()
     n, k, _ = o.rs_sizes(bs, t)
-    rng = np.random.default_rng(seed)
-    data = rng.integers(0, 256, nblocks * k, dtype=np.uint8)
     cores = min(16, os.cpu_count() or 1)
-    parts = np.array_split(np.arange(nblocks), cores)
-    bufs = []
-    for p in parts:
-        bufs.append(np.ascontiguousarray(data.reshape(nblocks, k)[p]).reshape(-1))
-    pos = rng.integers(0, n, nblocks)
-    val = rng.integers(1, 256, nblocks, dtype=np.uint8)
-    o.rs_encode(bs, t, data[:k])  # tables initialised before threads start
+    rng = np.random.default_rng(seed)
 
-    def enc(i):
-        return o.rs_encode(bs, t, bufs[i])
+    def run(nb, enc_fn, dec_fn):
+        data = rng.integers(0, 256, nb * k, dtype=np.uint8)
+        parts = np.array_split(np.arange(nb), cores)
+        bufs = [np.ascontiguousarray(data.reshape(nb, k)[p]).reshape(-1) for p in parts]
+        pos = rng.integers(0, n, nb)
+        val = rng.integers(1, 256, nb, dtype=np.uint8)
+        enc_fn(data[:k])  # tables initialised before the threads start
+        t_enc, cws = _pool_time(lambda i: enc_fn(bufs[i]), cores)
+        bads = []
+        for i, p in enumerate(parts):
+            c = cws[i].reshape(-1, n).copy()
+            c[np.arange(len(p)), pos[p]] ^= val[p]
+            bads.append(c.reshape(-1))
+        t_dec, outs = _pool_time(lambda i: dec_fn(bads[i]), cores)
+        ok = all(np.array_equal(outs[i][0], bufs[i]) for i in range(cores))
+        return t_enc, t_dec, ok
 
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(cores) as ex:
-        cws = list(ex.map(enc, range(cores)))
-    t_enc = time.perf_counter() - t0
-    bads = []
-    for i, p in enumerate(parts):
-        c = cws[i].reshape(-1, n).copy()
-        c[np.arange(len(p)), pos[p]] ^= val[p]
-        bads.append(c.reshape(-1))
-
-    def dec(i):
-        return o.rs_decode(bs, t, bads[i])
-
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(cores) as ex:
-        list(ex.map(dec, range(cores)))
-    t_dec = time.perf_counter() - t0
-    alg = (k + n) * nblocks
+    te, td, ok = run(nblocks, lambda d: o.rs_encode_table(bs, t, d), lambda r: o.rs_decode_table(bs, t, r))
+    fe, fd, fok = run(nfaithful, lambda d: o.rs_encode(bs, t, d), lambda r: o.rs_decode(bs, t, r))
+    alg = k + n
     return {
-        "value": round(2 * alg / (t_enc + t_dec) / GIB, 4),
+        "value": round(2 * alg * nblocks / (te + td) / GIB, 4),
         "unit": "GiB/s",
         "cores": cores,
         "kind": "port",
-        "sample": f"{nblocks} RS({n},{k}) blocks: encode + 1-byte-error decode, oracle/ppfs_oracle.c "
-                  f"on {cores} host threads over disjoint block ranges",
-        "encode_blocks_per_s": round(nblocks / t_enc),
-        "decode_blocks_per_s": round(nblocks / t_dec),
+        "sample": f"{nblocks} RS({n},{k}) blocks (the whole workload): encode + 1-byte-error decode, "
+                  f"oracle/ppfs_oracle.c table codec on {cores} host threads over disjoint block ranges",
+        "encode_blocks_per_s": round(nblocks / te),
+        "decode_blocks_per_s": round(nblocks / td),
+        "verified": bool(ok),
+        "faithful": {
+            "value": round(2 * alg * nfaithful / (fe + fd) / GIB, 4),
+            "unit": "GiB/s",
+            "cores": cores,
+            "kind": "port (reference-faithful algorithm)",
+            "sample": f"{nfaithful} RS({n},{k}) blocks: schoolbook long-division encode + Horner-syndrome / BM / "
+                      f"255-point root search / Forney decode (restated rs_block_device.cpp:95-280)",
+            "encode_blocks_per_s": round(nfaithful / fe),
+            "decode_blocks_per_s": round(nfaithful / fd),
+            "verified": bool(fok),
+        },
     }
 
 
+# ------------------------------------------------------------------------------------------
+# timing helpers
+# ------------------------------------------------------------------------------------------
 class HipEvents:
     """Timing events without the system-scope fence (hipEventDisableSystemFence): a default event
     record writes back and invalidates the caches, which charges the previous kernel's dirty lines
-    to the next interval and slows the kernel after it.  Created through libamdhip64 directly
-    (torch's events use the default flags)."""
+    to the next interval and slows the kernel after it.  Created through the HIP runtime torch
+    loaded (same library instance as the engine's launches)."""
 
     FLAGS = 0x20000000  # hipEventDisableSystemFence (hip_runtime_api.h)
 
@@ -127,6 +181,10 @@ class HipEvents:
         rc = self.L.hipEventElapsedTime(self.ct.byref(f), self.ev[i], self.ev[j])
         assert rc == 0, f"hipEventElapsedTime: {rc}"
         return f.value
+
+    def close(self):
+        for e in self.ev:
+            self.L.hipEventDestroy(e)
 
 
 def timed_steps(step, steps, world, sync, device=None):
@@ -152,22 +210,79 @@ def timed_steps(step, steps, world, sync, device=None):
     return elapsed
 
 
-def load_traffic(path=os.path.join(ROOT, "profiles", "pmc_latest.json")):
+def lib_sha256():
+    from paritypartyfs_amd import _native
+
+    h = hashlib.sha256()
+    with open(_native.LIB_PATH, "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()
+
+
+def load_traffic(kernel, nblocks, path=os.path.join(ROOT, "profiles", "pmc_latest.json")):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_summary.py), used
+    only when it was collected on THIS build of the library (sha256 of libppfs_ecc.so) for the
+    same kernel and block count; otherwise None (never a stale figure)."""
     try:
         with open(path) as f:
-            return json.load(f)
+            pmc = json.load(f)
     except Exception:
-        return None
+        return None, "no profiles/pmc_latest.json"
+    kp = pmc.get("kernels", {}).get(kernel)
+    if not kp or kp.get("blocks") != nblocks:
+        return None, f"pmc_latest.json ({pmc.get('tag')}) has no {kernel} over {nblocks} blocks"
+    if pmc.get("lib_sha256") != lib_sha256():
+        return None, f"pmc_latest.json ({pmc.get('tag')}) was collected on another build of libppfs_ecc.so"
+    return round(kp["hbm_bytes_per_launch"]), f"rocprofv3 PMC {pmc.get('tag')} (same library build)"
 
 
-def main():
-    args = parse()
+# ------------------------------------------------------------------------------------------
+# dry run: the launch / timing path with a CPU stand-in for the engine (tests only)
+# ------------------------------------------------------------------------------------------
+def dry_run(args, world, rank):
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    buf = np.zeros(1 << 16, np.uint8)
+
+    def step():  # stand-in work: no ECC, no GPU
+        np.bitwise_xor(buf, 1, out=buf)
+        time.sleep(0.001 * (rank + 1))
+
+    for _ in range(args.warmup):
+        step()
+    elapsed = timed_steps(step, args.steps, world, lambda: None, None)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "dry_run": True, "value": None, "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+                          "scaling": "weak", "note": "CPU stand-in for the engine: launcher / timing test only"}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------------------------------
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        # the driver's command form `python bench.py --gpus N`: start N ranks, report their line
+        return launch_ranks(args.gpus, argv)
+    world = int(env_world or 1)
+    if args.gpus is not None and args.gpus != world:
+        print(json.dumps({"error": f"--gpus {args.gpus} but WORLD_SIZE={world}"}), file=sys.stderr)
+        return 2
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run_cpu:
+        dry_run(args, world, rank)
+        return 0
+
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -175,13 +290,13 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    from paritypartyfs_amd import ECC_REED_SOLOMON, EccEngine
+    from paritypartyfs_amd import ECC_REED_SOLOMON, EccEngine, device_copy, pinned
 
     eng = EccEngine(ECC_REED_SOLOMON, args.block_size, args.t, device=dev.index)
     n, k = eng.raw_block_size, eng.data_size
     nb = args.blocks
     gen = torch.Generator(device=dev)
-    gen.manual_seed(0x50504653 ^ rank)  # "PPFS" ^ rank
+    gen.manual_seed(0x50504653 ^ rank)  # "PPFS" ^ rank: every rank its own shard
     data = torch.randint(0, 256, (nb * k,), dtype=torch.uint8, device=dev, generator=gen)
     cw = torch.empty(nb * n, dtype=torch.uint8, device=dev)
     out = torch.empty(nb * k, dtype=torch.uint8, device=dev)
@@ -195,6 +310,7 @@ def main():
     # byte of block b is always clean[b, pos_b] ^ val_b.  Precompute it once; the per-step
     # injection is then a single scatter of 2^20 wrong bytes into the fresh codewords.
     eng.encode(data, cw, nblocks=nb)
+    clean_cw = cw.clone()
     bad_bytes = cw[err_pos] ^ err_val
     torch.cuda.synchronize()
 
@@ -209,13 +325,11 @@ def main():
     for _ in range(2):  # eager once (also loads every kernel) before any capture
         step()
     torch.cuda.synchronize()
-    run = step
-    graph = None
     group = max(1, args.graph_steps)
-    if args.graph:
-        # hipGraphs of whole steps: `group` consecutive steps per graph (one replay = `group` full
-        # encode + inject + decode steps, no host launch overhead and no graph boundary between
-        # them); K = q * group + r timed steps run as q group replays + r single-step replays.
+    graph = graph_g = None
+    if args.launch == "graph":
+        # hipGraphs of whole steps: `group` consecutive steps per graph; K = q * group + r timed
+        # steps run as q group replays + r single-step replays
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             step()
@@ -225,16 +339,15 @@ def main():
             with torch.cuda.graph(graph_g):
                 for _ in range(group):
                     step()
-        run = graph.replay
 
-    def run_steps(k):
-        if graph is None or group == 1:
-            for _ in range(k):
-                run()
+    def run_steps(kk):
+        if graph is None:
+            for _ in range(kk):
+                step()
             return
-        for _ in range(k // group):
+        for _ in range(kk // group):
             graph_g.replay()
-        for _ in range(k % group):
+        for _ in range(kk % group):
             graph.replay()
 
     # Clock ramp: a GPU that was idle runs its first milliseconds of work at lower clocks (the first
@@ -252,16 +365,17 @@ def main():
         ok = bool(torch.equal(out, data)) and int(status.min()) == 1 and int(status.max()) == 1
         if not ok:
             print(json.dumps({"error": "verification failed"}), file=sys.stderr)
-            sys.exit(3)
+            return 3
 
     elapsed = timed_steps(lambda: run_steps(args.steps), 1, world, torch.cuda.synchronize, dev)
 
-    # Kernel durations (roofline.achieved): eager steps bracketed by fence-free HIP events on the
-    # launch stream, all K queued before one synchronize (host issue ~30 us/step << device time),
-    # so an event pair brackets its kernel plus the ~1-2 us dependent-launch boundary.
-    he = HipEvents(4 * args.steps + 2)
+    # ---- everything below is outside the timed region ----
+    # (1) in-step kernel durations (roofline.achieved): eager steps bracketed by fence-free HIP
+    # events on the launch stream, all K queued before one synchronize
+    K = args.steps
+    he = HipEvents(4 * K + 2)
     t_issue = time.perf_counter()
-    for i in range(args.steps):
+    for i in range(K):
         he.record(4 * i, stream)
         eng.encode(data, cw, nblocks=nb)
         he.record(4 * i + 1, stream)
@@ -269,102 +383,133 @@ def main():
         he.record(4 * i + 2, stream)
         eng.decode(cw, out, status, write_back=True, nblocks=nb)
         he.record(4 * i + 3, stream)
-    t_issue = (time.perf_counter() - t_issue) / args.steps
+    t_issue = (time.perf_counter() - t_issue) / K
     torch.cuda.synchronize()
-    enc_ms = [he.ms(4 * i, 4 * i + 1) for i in range(args.steps)]
-    inj_ms = [he.ms(4 * i + 1, 4 * i + 2) for i in range(args.steps)]
-    dec_ms = [he.ms(4 * i + 2, 4 * i + 3) for i in range(args.steps)]
+    enc_ms = [he.ms(4 * i, 4 * i + 1) for i in range(K)]
+    inj_ms = [he.ms(4 * i + 1, 4 * i + 2) for i in range(K)]
+    dec_ms = [he.ms(4 * i + 2, 4 * i + 3) for i in range(K)]
     enc_avg, dec_avg, inj_avg = float(np.mean(enc_ms)), float(np.mean(dec_ms)), float(np.mean(inj_ms))
-    # device time of the timed region itself (same K steps again, two events around them)
-    he.record(4 * args.steps, stream)
-    run_steps(args.steps)
-    he.record(4 * args.steps + 1, stream)
+    # device time of the timed region's launch form (same K steps again, two events around them)
+    he.record(4 * K, stream)
+    run_steps(K)
+    he.record(4 * K + 1, stream)
     torch.cuda.synchronize()
-    gpu_ms_per_step = he.ms(4 * args.steps, 4 * args.steps + 1) / args.steps
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    gpu_ms_per_step = he.ms(4 * K, 4 * K + 1) / K
+    he.close()
 
-    # device copy reference peak (same bytes as one encode: read k, write n per block)
+    # (2) standalone kernels: L back-to-back launches of one kernel, fence-free events between
+    # them (the north-star measurement: RS encode over the 1 M-block batch on its own)
+    L = max(3, args.standalone_launches)
+    hs = HipEvents(L + 1)
+    for _ in range(3):
+        eng.encode(data, cw, nblocks=nb)
+    hs.record(0, stream)
+    for i in range(L):
+        eng.encode(data, cw, nblocks=nb)
+        hs.record(i + 1, stream)
+    torch.cuda.synchronize()
+    enc_sa = [hs.ms(i, i + 1) for i in range(L)]
+    assert torch.equal(cw, clean_cw), "standalone encode output differs"
+    # clean decode (status + write-back enabled, nothing to correct): the read path of a scrub
+    for _ in range(3):
+        eng.decode(cw, out, status, write_back=True, nblocks=nb)
+    hs.record(0, stream)
+    for i in range(L):
+        eng.decode(cw, out, status, write_back=True, nblocks=nb)
+        hs.record(i + 1, stream)
+    torch.cuda.synchronize()
+    dec_sa = [hs.ms(i, i + 1) for i in range(L)]
+    hs.close()
+
+    # (3) device copy ceiling: the engine's full-grid 16-byte copy kernel over the bytes of one
+    # encode (read k, write n per block), timed like the kernels
     cp_src = torch.empty(nb * (k + n) // 2, dtype=torch.uint8, device=dev)
     cp_dst = torch.empty_like(cp_src)
     for _ in range(3):
-        cp_dst.copy_(cp_src)
-    ev[4].record(stream)
-    for _ in range(10):
-        cp_dst.copy_(cp_src)
-    ev[5].record(stream)
-    ev[5].synchronize()
-    torch_copy_gbs = 2 * cp_src.numel() / (ev[4].elapsed_time(ev[5]) / 10 * 1e-3) / 1e9
-    # the engine's full-grid 16-byte copy kernel (ppfs_copy_device): the HBM ceiling this access
-    # shape reaches, timed like the kernels (fence-free events on the launch stream, median)
-    from paritypartyfs_amd import device_copy
-
-    for _ in range(3):
         device_copy(cp_dst, cp_src, stream=stream)
-    hc = HipEvents(20)
-    for i in range(10):
-        hc.record(2 * i, stream)
+    hc = HipEvents(21)
+    hc.record(0, stream)
+    for i in range(20):
         device_copy(cp_dst, cp_src, stream=stream)
-        hc.record(2 * i + 1, stream)
+        hc.record(i + 1, stream)
     torch.cuda.synchronize()
-    copy_ms = float(np.median([hc.ms(2 * i, 2 * i + 1) for i in range(10)]))
+    copy_ms = float(np.median([hc.ms(i, i + 1) for i in range(20)]))
     copy_gbs = 2 * cp_src.numel() / (copy_ms * 1e-3) / 1e9
+    hc.close()
     del cp_src, cp_dst
 
     alg_per_block = k + n  # 504 B for RS(255,249), both for encode and decode
+    alg_launch = alg_per_block * nb
     if (args.block_size, args.t) == (512, 3):
         cfg_ref = "BASELINE configs[1]+[2]"
     elif (args.block_size, args.t) == (4096, 16):
         cfg_ref = "BASELINE configs[4], one GPU's shard"
     else:
         cfg_ref = "not a BASELINE config"
-    total_bytes = 2 * alg_per_block * nb * world * args.steps
+    total_bytes = 2 * alg_launch * world * K
     value = total_bytes / elapsed / GIB
-    ms_per_step = elapsed / args.steps * 1e3
+    ms_per_step = elapsed / K * 1e3
 
-    dom_ms = max(enc_avg, dec_avg)
+    def kname(which):
+        kn = eng.kernel_name
+        if kn.startswith("rs255-wg"):
+            return f"rs_wg_{which}_kernel<{n - k}>"
+        if kn.startswith("rs255-pair"):  # 16 < 2t <= 32 (rs_pair.hpp)
+            return f"rs_pair_{'decode' if which == 'decode' else 'encode_img'}_kernel<{n - k}>"
+        if kn.startswith("rs255-slice8") and which == "encode" and n - k == 16:
+            return f"rs_solo_encode_img_kernel<{n - k}>"
+        return f"rs255_{which}_kernel<{n - k}>"
+
     which = "decode" if dec_avg >= enc_avg else "encode"
-    kn = eng.kernel_name
-    if kn.startswith("rs255-wg"):
-        dom_name = f"rs_wg_{which}_kernel<{n - k}>"
-    elif kn.startswith("rs255-pair"):  # 16 < 2t <= 32 (rs_pair.hpp)
-        dom_name = f"rs_pair_{'decode' if which == 'decode' else 'encode_img'}_kernel<{n - k}>"
-    elif kn.startswith("rs255-slice8") and which == "encode" and n - k == 16:
-        dom_name = f"rs_solo_encode_img_kernel<{n - k}>"
-    else:
-        dom_name = f"rs255_{which}_kernel<{n - k}>"
-    achieved = alg_per_block * nb / (dom_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = load_traffic()
-    kp = (pmc or {}).get("kernels", {}).get(dom_name)
-    if kp and kp.get("blocks") == nb:
-        traffic = round(kp["hbm_bytes_per_launch"])  # profiles/pmc_latest.json, tools/pmc_summary.py
+    dom_ms = max(enc_avg, dec_avg)
+    dom_name = kname(which)
+    achieved = alg_launch / (dom_ms * 1e-3) / 1e9
+    traffic, traffic_src = load_traffic(dom_name, nb)
+    frac = lambda ms: round(alg_launch / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)  # noqa: E731
 
+    # (4) host-inclusive rate (north_star: the path starts and ends in host memory): H2D + kernel
+    # + D2H through the engine's host entry points, pageable and page-locked, rank 0 at N=1
     host_incl = None
-    if args.host_inclusive and rank == 0:
+    if args.host_inclusive and rank == 0 and world == 1:
         hd = data.cpu().numpy()
         hraw = np.empty(nb * n, np.uint8)
         hout = np.empty(nb * k, np.uint8)
         hst = np.empty(nb, np.uint8)
-        eng.encode_host(hd, hraw)
-        t1 = time.perf_counter()
-        eng.encode_host(hd, hraw)
-        t2 = time.perf_counter()
-        eng.decode_host(hraw, hout, hst, write_back=True)
-        t3 = time.perf_counter()
-        host_incl = {"encode_GiBps": round(alg_per_block * nb / (t2 - t1) / GIB, 3),
-                     "decode_GiBps": round(alg_per_block * nb / (t3 - t2) / GIB, 3)}
+        host_incl = {}
+        for mode in ("pageable", "pinned"):
+            ctx = pinned(hd, hraw, hout, hst) if mode == "pinned" else None
+            if ctx:
+                ctx.__enter__()
+            try:
+                eng.encode_host(hd, hraw)  # staging warm
+                t1 = time.perf_counter()
+                eng.encode_host(hd, hraw)
+                t2 = time.perf_counter()
+                hraw[np.arange(nb) * n + (np.arange(nb) * 37) % n] ^= 0x5A  # one error per block
+                t3 = time.perf_counter()
+                eng.decode_host(hraw, hout, hst, write_back=True)
+                t4 = time.perf_counter()
+            finally:
+                if ctx:
+                    ctx.__exit__(None, None, None)
+            ok = bool(np.array_equal(hout, hd)) and int(hst.min()) == 1
+            host_incl[mode] = {"encode_GiBps": round(alg_launch / (t2 - t1) / GIB, 3),
+                               "decode_1err_GiBps": round(alg_launch / (t4 - t3) / GIB, 3), "verified": ok}
+        host_incl["note"] = ("ppfs_ecc_{encode,decode}_host over the same 2^20 blocks: H2D + kernel + D2H wall "
+                             "time, algorithmic bytes; never `value`")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.block_size, args.t, min(args.cpu_sample_blocks, nb))
+        cpu = cpu_baseline(args.block_size, args.t, min(args.cpu_sample_blocks, nb),
+                           min(args.cpu_faithful_blocks, nb))
 
     if rank == 0:
         line = {
-            "metric": "device-resident GiB/s: RS encode+decode, 512 B blocks, 1 M-block batch",
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "GiB/s",
             "n_gpus": world,
-            "steps": args.steps,
+            "steps": K,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
@@ -387,16 +532,25 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "algorithmic_bytes_per_launch": alg_per_block * nb,
+                "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": alg_launch,
                 "avg_launch_ms": round(dom_ms, 5),
             },
             "cpu_baseline": cpu,
             "kernels_ms": {"encode": round(enc_avg, 5), "inject": round(inj_avg, 5), "decode": round(dec_avg, 5)},
-            "encode_GBps": round(alg_per_block * nb / (enc_avg * 1e-3) / 1e9, 1),
-            "decode_GBps": round(alg_per_block * nb / (dec_avg * 1e-3) / 1e9, 1),
+            "in_step_frac": {"encode": frac(enc_avg), "decode": frac(dec_avg)},
+            "standalone": {
+                "launches": L,
+                "encode_ms_median": round(float(np.median(enc_sa)), 5),
+                "encode_ms_mean": round(float(np.mean(enc_sa)), 5),
+                "encode_frac": frac(float(np.median(enc_sa))),
+                "clean_decode_ms_median": round(float(np.median(dec_sa)), 5),
+                "clean_decode_frac": frac(float(np.median(dec_sa))),
+                "note": "back-to-back launches of one kernel, fence-free events between them, outside the "
+                        "timed region (north-star: >= 70 % on RS t=3 encode over 1 M blocks)",
+            },
             "device_copy_GBps": round(copy_gbs, 1),
             "device_copy_kernel": "ppfs_copy_device (full-grid 16-B copy, same bytes as one encode)",
-            "torch_copy_GBps": round(torch_copy_gbs, 1),
             # payload rate beside the algorithmic one, and the dominant kernel
             # against the device-to-device copy measured above
             "payload_GiBps": round(value * k / alg_per_block, 3),
@@ -408,9 +562,11 @@ def main():
             "device_ms_per_step": round(gpu_ms_per_step, 4),
         }
         print(json.dumps(line), flush=True)
+    eng.close()
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -26,8 +26,9 @@
  * All codec arithmetic (RS encode / syndromes / Berlekamp-Massey / Chien / Forney, CRC,
  * Hamming SECDED, parity) runs in the HIP kernels behind the C ABI.  This layer moves bytes
  * between the disk and the engine and reproduces the reference's read-modify-write,
- * write-back and logging order.  There is no CPU fallback: constructing a device without a
- * usable engine (no GPU, missing library) aborts with the ABI's error message.
+ * write-back and logging order.  There is no CPU fallback: every engine error (including a
+ * device whose engine could not be created: no GPU, bad parameters) is reported as
+ * FsError::Disk_IOError, with the ABI's message on stderr; nothing throws or aborts.
  *
  * Extension: readBlocks / writeBlocks run a contiguous range of whole blocks
  * through ONE engine call; results, disk contents and log are those of the per-block loop.
@@ -441,10 +442,12 @@ public:
         p.block_size = block_size;
         p.rs_correctable_bytes = t;
         p.crc_polynomial = poly;
+        // the reference's constructors cannot fail: a device whose engine could not be created
+        // (no GPU, bad parameters) reports Disk_IOError from every call instead -- no CPU fallback
         const int rc = ppfs_ecc_create(&p, device, &_ctx);
         if (rc != 0 || !_ctx) {
             std::fprintf(stderr, "ppfs_gpu: ppfs_ecc_create failed (%d): %s\n", rc, ppfs_ecc_last_error());
-            std::abort(); // no CPU fallback
+            _ctx = nullptr;
         }
     }
     ~EccEngine() { ppfs_ecc_destroy(_ctx); }
@@ -453,12 +456,16 @@ public:
     size_t raw() const { return ppfs_ecc_raw_block_size(_ctx); }
     size_t data() const { return ppfs_ecc_data_size(_ctx); }
     ppfs_ecc_ctx* ctx() const { return _ctx; }
-    static void check(int rc, const char* what)
+    bool valid() const { return _ctx != nullptr; }
+    // An engine call's return code: 0 -> true; else the ABI's message goes to stderr and the
+    // caller returns FsError::Disk_IOError (the reference's code for a failed device operation)
+    static bool ok(int rc, const char* what)
     {
         if (rc != 0) {
             std::fprintf(stderr, "ppfs_gpu: %s failed (%d): %s\n", what, rc, ppfs_ecc_last_error());
-            std::abort();
+            return false;
         }
+        return true;
     }
 
 private:
@@ -573,15 +580,15 @@ class EngineBlockDevice : public IBlockDevice {
 public:
     size_t rawBlockSize() const override { return _raw; }
     size_t dataSize() const override { return _ds; }
-    size_t numOfBlocks() const override { return _disk.size() / _raw; }
+    size_t numOfBlocks() const override { return _raw ? _disk.size() / _raw : 0; }
 
     expected<void> formatBlock(unsigned int block_index) override
     {
         // rs:15-23, hamming:164-172, parity:22-29 write an all-zero raw block; crc:124-134 an
         // all-zero payload with its CRC -- the engine's encode of a zero payload is exactly that
         std::vector<uint8_t> raw(_raw, 0), zero(_ds, 0);
-        if (_type == PPFS_ECC_CRC)
-            EccEngine::check(ppfs_ecc_encode_host(_eng.ctx(), zero.data(), raw.data(), 1), "encode");
+        if (_type == PPFS_ECC_CRC && !EccEngine::ok(ppfs_ecc_encode_host(_eng.ctx(), zero.data(), raw.data(), 1), "encode"))
+            return unexpected(FsError::Disk_IOError);
         auto r = detail::disk_write(_disk, (size_t)block_index * _raw, raw.data(), _raw);
         if (!r)
             return unexpected(r.error());
@@ -618,11 +625,29 @@ public:
             return unexpected(fx.error());
         std::memcpy(dec.data() + loc.offset, data.data(), to_write);
         // encode over the old block: CRC tail bits / Hamming unused bits keep their contents
-        EccEngine::check(ppfs_ecc_encode_host(_eng.ctx(), dec.data(), raw.data(), 1), "encode");
+        if (!EccEngine::ok(ppfs_ecc_encode_host(_eng.ctx(), dec.data(), raw.data(), 1), "encode"))
+            return unexpected(FsError::Disk_IOError);
         auto w = detail::disk_write(_disk, (size_t)loc.block_index * _raw, raw.data(), _raw);
         if (!w)
             return unexpected(w.error());
         return to_write;
+    }
+
+    // readBlock({first + i, 0}) for i in [from, count): each block's own error (e.g.
+    // Disk_OutOfBounds past the disk end) in err[i], decoded payloads (zeros on error) in out --
+    // the per-block contract, for ranges the batch path cannot read in one piece
+    expected<void> per_block_reads(block_index_t first, size_t from, size_t count, uint8_t* out, uint8_t* err)
+    {
+        for (size_t i = from; i < count; ++i) {
+            static_vector<uint8_t> v(out + i * _ds, _ds, 0);
+            auto r = readBlock(DataLocation((int)(first + (block_index_t)i), 0), _ds, v);
+            if (!r) {
+                std::memset(out + i * _ds, 0, _ds);
+                if (err)
+                    err[i] = (uint8_t)r.error();
+            }
+        }
+        return {};
     }
 
     expected<void> readBlocks(block_index_t first, size_t count, uint8_t* out, uint8_t* err) override
@@ -633,11 +658,12 @@ public:
             // in place on the disk image: the engine writes corrected codewords back into it
             // (RS: whole codeword, Hamming: the flipped byte, as the reference's write-back)
             if (((size_t)first + count) * _raw > _disk.size())
-                return unexpected(FsError::Disk_OutOfBounds);
+                return per_block_reads(first, 0, count, out, err); // range runs off the disk
             std::vector<uint8_t> status(count);
-            EccEngine::check(ppfs_ecc_decode_host(_eng.ctx(), img + (size_t)first * _raw, out, status.data(), count,
-                                 1, nullptr),
-                "decode");
+            if (!EccEngine::ok(ppfs_ecc_decode_host(_eng.ctx(), img + (size_t)first * _raw, out, status.data(), count,
+                                   1, nullptr),
+                    "decode"))
+                return unexpected(FsError::Disk_IOError);
             for (size_t i = 0; i < count; ++i) {
                 if (status[i] == PPFS_ECC_CORRECTION_ERROR) {
                     if (err)
@@ -656,13 +682,13 @@ public:
             std::vector<uint8_t> raw(nb * _raw), fixed, status(nb), spill;
             auto rr = detail::disk_read(_disk, (size_t)b0 * _raw, nb * _raw, raw.data());
             if (!rr)
-                return unexpected(rr.error());
+                return per_block_reads(first, done, count, out, err); // range not on the disk
             fixed = raw;
             if (has_spill())
                 spill.assign(nb * spill_stride(), 0);
-            EccEngine::check(ppfs_ecc_decode_host(_eng.ctx(), fixed.data(), out + done * _ds, status.data(), nb,
-                                 1, spill.empty() ? nullptr : spill.data()),
-                "decode");
+            if (!EccEngine::ok(ppfs_ecc_decode_host(_eng.ctx(), fixed.data(), out + done * _ds, status.data(), nb,
+                                 1, spill.empty() ? nullptr : spill.data()), "decode"))
+                return unexpected(FsError::Disk_IOError);
             size_t i = 0;
             for (; i < nb; ++i) {
                 const block_index_t b = b0 + (block_index_t)i;
@@ -710,13 +736,15 @@ public:
             return unexpected(FsError::Disk_OutOfBounds);
         std::vector<uint8_t> raw(img ? 0 : count * _raw), status(count);
         if (img) { // in place on the disk image
-            EccEngine::check(
-                ppfs_ecc_write_host(_eng.ctx(), payloads, img + (size_t)first * _raw, status.data(), count), "write");
+            if (!EccEngine::ok(
+                ppfs_ecc_write_host(_eng.ctx(), payloads, img + (size_t)first * _raw, status.data(), count), "write"))
+                return unexpected(FsError::Disk_IOError);
         } else {
             auto rr = detail::disk_read(_disk, (size_t)first * _raw, count * _raw, raw.data());
             if (!rr)
                 return unexpected(rr.error());
-            EccEngine::check(ppfs_ecc_write_host(_eng.ctx(), payloads, raw.data(), status.data(), count), "write");
+            if (!EccEngine::ok(ppfs_ecc_write_host(_eng.ctx(), payloads, raw.data(), status.data(), count), "write"))
+                return unexpected(FsError::Disk_IOError);
         }
         for (size_t i = 0; i < count; ++i) {
             if (status[i] == PPFS_ECC_CORRECTION_ERROR) {
@@ -748,8 +776,9 @@ public:
         if (uint8_t* img = _disk.mapped()) { // in place on the disk image
             std::vector<uint8_t> status(count);
             size_t c3[3] = { 0, 0, 0 };
-            EccEngine::check(
-                ppfs_ecc_scrub_host(_eng.ctx(), img + base, _disk.size() - base, count, status.data(), c3), "scrub");
+            if (!EccEngine::ok(
+                ppfs_ecc_scrub_host(_eng.ctx(), img + base, _disk.size() - base, count, status.data(), c3), "scrub"))
+                return unexpected(FsError::Disk_IOError);
             for (size_t i = 0; i < count; ++i) {
                 if (status[i] == PPFS_ECC_CORRECTION_ERROR && err)
                     err[i] = (uint8_t)FsError::BlockDevice_CorrectionError;
@@ -766,7 +795,8 @@ public:
             return unexpected(rr.error());
         const std::vector<uint8_t> before = image;
         size_t c3[3] = { 0, 0, 0 };
-        EccEngine::check(ppfs_ecc_scrub_host(_eng.ctx(), image.data(), image.size(), count, status.data(), c3), "scrub");
+        if (!EccEngine::ok(ppfs_ecc_scrub_host(_eng.ctx(), image.data(), image.size(), count, status.data(), c3), "scrub"))
+            return unexpected(FsError::Disk_IOError);
         for (size_t i = 0; i < count; ++i) {
             if (status[i] == PPFS_ECC_CORRECTION_ERROR && err)
                 err[i] = (uint8_t)FsError::BlockDevice_CorrectionError;
@@ -801,7 +831,7 @@ protected:
     {
     }
 
-    bool has_spill() const { return _type == PPFS_ECC_REED_SOLOMON && _raw < 255; }
+    bool has_spill() const { return _type == PPFS_ECC_REED_SOLOMON && _raw > 0 && _raw < 255; }
     size_t spill_stride() const { return 256 - std::min<size_t>(_raw, 255); }
 
     void log(block_index_t b)
@@ -845,9 +875,10 @@ protected:
         if (has_spill())
             spill.assign(spill_stride(), 0);
         const int wb = (_type == PPFS_ECC_REED_SOLOMON || _type == PPFS_ECC_HAMMING) ? 1 : 0;
-        EccEngine::check(ppfs_ecc_decode_host(_eng.ctx(), fixed.data(), dec, &status, 1, wb,
-                             spill.empty() ? nullptr : spill.data()),
-            "decode");
+        if (!EccEngine::ok(ppfs_ecc_decode_host(_eng.ctx(), fixed.data(), dec, &status, 1, wb,
+                               spill.empty() ? nullptr : spill.data()),
+                "decode"))
+            return unexpected(FsError::Disk_IOError);
         if (status == PPFS_ECC_CORRECTION_ERROR)
             return unexpected(FsError::BlockDevice_CorrectionError);
         if (status == PPFS_ECC_CORRECTED && wb) {

@@ -7,9 +7,12 @@
  * The product path (paritypartyfs_amd/csrc) never links or calls it.
  *
  * Every function cites the reference file:line it restates (paths relative to the
- * reference repository root, lib/...).  The reference itself cannot be compiled in this
- * image (it needs C++23 <expected>, absent from libstdc++ 11 and there are no libc++
- * headers), so this restatement is pinned by:
+ * reference repository root, lib/...).  Only the reference's GF256 (gf256.cpp) compiles in this
+ * image; the rest needs C++23 <expected>, absent from libstdc++ 11 (no libc++ headers).  So
+ * this restatement is pinned by:
+ *   - the reference's GF256 binary itself (oracle/_ref, built by oracle/Makefile from the
+ *     unmodified gf256.cpp): every product, quotient, inverse, log and power, exhaustively
+ *     (tests/golden/gf256_ref.npz, tests/test_oracle_kats.py),
  *   - the reference's own known-answer tests (unit_tests/test_crc_block_device.cpp:39-71,
  *     unit_tests/test_bits.cpp:5-34) and round-trip tests (test_rs/crc/hamming/parity),
  *   - known-answer vectors recorded from a reference build in SURVEY.md section 8(a)
@@ -101,6 +104,26 @@ EXPORT void oracle_gf_tables(uint8_t* exp_out, uint8_t* log_out)
 EXPORT uint8_t oracle_gf_mul(uint8_t a, uint8_t b) { gf_init(); return gf_mul(a, b); }
 EXPORT uint8_t oracle_gf_div(uint8_t a, uint8_t b) { gf_init(); return gf_div(a, b); }
 EXPORT uint8_t oracle_gf_inv(uint8_t a) { gf_init(); return gf_inv(a); }
+
+/* Whole-field dump for the exhaustive pin against the reference binary (tests/golden/
+ * gf256_ref.npz, oracle/_ref): mul / div [a * 256 + b], inv, log, pow[i] = alpha^i. */
+EXPORT void oracle_gf_dump(uint8_t* mul, uint8_t* div, uint8_t* inv, uint8_t* log, uint8_t* pow)
+{
+    gf_init();
+    for (int a = 0; a < 256; ++a) {
+        for (int b = 0; b < 256; ++b) {
+            mul[a * 256 + b] = gf_mul((uint8_t)a, (uint8_t)b);
+            div[a * 256 + b] = gf_div((uint8_t)a, (uint8_t)b);
+        }
+        inv[a] = gf_inv((uint8_t)a);
+        log[a] = LOG[a];
+    }
+    uint8_t p = 1;
+    for (int i = 0; i < 256; ++i) {
+        pow[i] = p;
+        p = gf_mul(p, 2);
+    }
+}
 
 /* ------------------------------------------------------------------------------------ */
 /* PolynomialGF256 -- lib/ecc_helpers/src/polynomial_gf256.cpp                           */
@@ -443,6 +466,198 @@ EXPORT int oracle_rs_decode_one_full(int block_size, int t, const uint8_t* raw, 
     *wb_len = wl;
     *nroots = nr;
     return poly_ub ? FS_UNDEFINED : st;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Table-driven CPU codec: bench.py's "optimised" CPU column, next to the long-division      */
+/* restatement above ("faithful").  Same outputs (tests/test_oracle_kats.py cross-checks):  */
+/*   encode  LFSR form of m(x) x^2t mod g (rs_block_device.cpp:95-117): for j = k-1 .. 0,   */
+/*           fb = d[j] ^ r[2t-1]; r[q] = r[q-1] ^ fb g[q]; r[0] = fb g[0]                    */
+/*   decode  S_i = c(alpha^i) by Horner with one product table per root (:131-141); all     */
+/*           zero -> extract (:143-146); otherwise the restated reference decode above.     */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+    rs_code rs;
+    int t2, k;
+    uint8_t gmul[256][64];   /* gmul[fb][q] = fb * g[q] */
+    uint64_t gw[256];        /* 2t <= 8: the same products packed, byte q = coefficient q */
+    uint8_t amul[64][256];   /* amul[i][v] = v * alpha^(i+1) */
+} rs_tab;
+
+static void rs_tab_setup(rs_tab* T, int block_size, int t)
+{
+    rs_setup(&T->rs, block_size, t);
+    T->t2 = 2 * T->rs.t;
+    T->k = T->rs.n - T->t2;
+    for (int v = 0; v < 256; ++v) {
+        uint64_t w = 0;
+        for (int q = 0; q < T->t2 && q < 64; ++q) {
+            T->gmul[v][q] = gf_mul((uint8_t)v, T->rs.gen.c[q]);
+            if (q < 8)
+                w |= (uint64_t)T->gmul[v][q] << (8 * q);
+        }
+        T->gw[v] = w;
+    }
+    uint8_t a = 2;
+    for (int i = 0; i < T->t2 && i < 64; ++i) {
+        for (int v = 0; v < 256; ++v)
+            T->amul[i][v] = gf_mul((uint8_t)v, a);
+        a = gf_mul(a, 2);
+    }
+}
+
+static void rs_tab_encode_one(const rs_tab* T, const uint8_t* d, uint8_t* out)
+{
+    const int t2 = T->t2, k = T->k;
+    if (t2 <= 8) {
+        const uint64_t mask = t2 == 8 ? ~0ull : ((1ull << (8 * t2)) - 1);
+        uint64_t r = 0;
+        for (int j = k - 1; j >= 0; --j) {
+            const uint8_t fb = (uint8_t)(d[j] ^ (t2 ? (r >> (8 * (t2 - 1))) : 0));
+            r = ((r << 8) & mask) ^ T->gw[fb];
+        }
+        for (int q = 0; q < t2; ++q)
+            out[q] = (uint8_t)(r >> (8 * q));
+    } else {
+        uint8_t r[64] = { 0 };
+        for (int j = k - 1; j >= 0; --j) {
+            const uint8_t fb = (uint8_t)(d[j] ^ r[t2 - 1]);
+            for (int q = t2 - 1; q >= 1; --q)
+                r[q] = (uint8_t)(r[q - 1] ^ T->gmul[fb][q]);
+            r[0] = T->gmul[fb][0];
+        }
+        memcpy(out, r, (size_t)t2);
+    }
+    memcpy(out + t2, d, (size_t)k);
+}
+
+/* Correction of a full-length (n = 255) codeword with syndromes S: the reference's steps on
+ * coefficient arrays instead of PolynomialGF256 objects -- BM exactly as :234-269 (rs_bm above),
+ * every root v in 1..255 of sigma (:271-280), Omega = S sigma mod x^2t (:224-232), e = Omega(v) /
+ * sigma'(v) with a/0 = 0 (:210-222), c[log(1/v)] ^= e for every root (:165-168).  With n = 255
+ * the write-back is the whole corrected codeword (every position is < 255). */
+static uint8_t arr_eval(const uint8_t* p, int len, uint8_t x)
+{
+    uint8_t r = 0;
+    for (int i = len - 1; i >= 0; --i)
+        r = (uint8_t)(gf_mul(r, x) ^ p[i]);
+    return r;
+}
+
+static void rs_tab_correct(const uint8_t* S, int t2, uint8_t* cw)
+{
+    enum { M = 160 };
+    uint8_t sig[M] = { 1 }, B[M] = { 1 }, T[M];
+    uint8_t bb = 1;
+    int L = 0, m = 1;
+    for (int r = 0; r < t2; ++r) {
+        uint8_t d = S[r];
+        for (int i = 1; i <= L; ++i)
+            d ^= gf_mul(sig[i], S[r - i]);
+        if (d) {
+            memcpy(T, sig, M);
+            const uint8_t f = gf_div(d, bb);
+            for (int i = 0; i + m < M; ++i)
+                sig[i + m] ^= gf_mul(f, B[i]);
+            if (2 * L <= r) {
+                L = r + 1 - L;
+                memcpy(B, T, M);
+                bb = d;
+                m = 1;
+            } else {
+                m++;
+            }
+        } else {
+            m++;
+        }
+    }
+    int len = M;
+    while (len > 0 && !sig[len - 1])
+        len--;
+    uint8_t om[64] = { 0 }, ds[M] = { 0 };
+    for (int i = 0; i < t2; ++i) /* (S sigma) mod x^2t */
+        for (int j = 0; j <= i && j < len; ++j)
+            om[i] ^= gf_mul(S[i - j], sig[j]);
+    for (int i = 1; i < len; i += 2) /* odd terms of sigma' */
+        ds[i - 1] = sig[i];
+    for (int v = 1; v <= 255; ++v)
+        if (arr_eval(sig, len, (uint8_t)v) == 0) {
+            const uint8_t e = gf_div(arr_eval(om, t2, (uint8_t)v), arr_eval(ds, len, (uint8_t)v));
+            cw[LOG[gf_inv((uint8_t)v)]] ^= e;
+        }
+}
+
+EXPORT int oracle_rs_encode_table(int block_size, int t, const uint8_t* data, uint8_t* raw, size_t nblocks)
+{
+    rs_tab* T = (rs_tab*)malloc(sizeof(rs_tab));
+    if (!T)
+        return -1;
+    rs_tab_setup(T, block_size, t);
+    const int n = T->rs.n;
+    for (size_t b = 0; b < nblocks; ++b)
+        rs_tab_encode_one(T, data + b * (size_t)T->k, raw + b * (size_t)n);
+    free(T);
+    return 0;
+}
+
+/* status / raw_fixed as oracle_rs_decode (no wb_len); the restated decode runs for blocks with
+ * a non-zero syndrome only */
+EXPORT int oracle_rs_decode_table(int block_size, int t, const uint8_t* raw, uint8_t* data, uint8_t* status,
+    uint8_t* raw_fixed, size_t nblocks)
+{
+    rs_tab* T = (rs_tab*)malloc(sizeof(rs_tab));
+    if (!T)
+        return -1;
+    rs_tab_setup(T, block_size, t);
+    const int n = T->rs.n, t2 = T->t2, k = T->k;
+    uint8_t fixed[PMAX];
+    int ub = 0;
+    for (size_t b = 0; b < nblocks; ++b) {
+        const uint8_t* c = raw + b * (size_t)n;
+        unsigned any = 0; /* OR of S_1 .. S_2t */
+        uint8_t S[64];
+        for (int i = 0; i < t2; ++i) {
+            uint8_t s = 0;
+            const uint8_t* am = T->amul[i];
+            for (int j = n - 1; j >= 0; --j)
+                s = (uint8_t)(am[s] ^ c[j]);
+            S[i] = s;
+            any |= s;
+        }
+        uint8_t* o = raw_fixed ? raw_fixed + b * (size_t)n : NULL;
+        if (!any) {
+            memcpy(data + b * (size_t)k, c + t2, (size_t)k);
+            if (status)
+                status[b] = FS_OK;
+            if (o)
+                memcpy(o, c, (size_t)n);
+            continue;
+        }
+        if (n == 255) { /* full-length code: array BM / root search / Forney, nothing spills */
+            uint8_t cw[255];
+            memcpy(cw, c, 255);
+            rs_tab_correct(S, t2, cw);
+            memcpy(data + b * (size_t)k, cw + t2, (size_t)k);
+            if (status)
+                status[b] = FS_CORRECTED;
+            if (o)
+                memcpy(o, cw, 255);
+            continue;
+        }
+        int wl = 0;
+        poly_ub = 0;
+        const int st = rs_decode_one(&T->rs, c, data + b * (size_t)k, fixed, &wl, NULL);
+        ub |= poly_ub;
+        if (status)
+            status[b] = (uint8_t)st;
+        if (o) {
+            memcpy(o, c, (size_t)n);
+            for (int i = 0; i < wl && i < n; ++i)
+                o[i] = fixed[i];
+        }
+    }
+    free(T);
+    return ub ? -1 : 0;
 }
 
 /* ------------------------------------------------------------------------------------ */

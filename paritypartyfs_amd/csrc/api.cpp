@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <functional>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -242,39 +243,6 @@ template <int T2> std::vector<uint8_t> build_rs_wg_tables_t()
                         G.mul((uint8_t)(v << (4 * h)), G.exp[e]);
                 }
     build_gf_block(out.data() + L::OFF_GF);
-    return out;
-}
-
-// tables of the column-split RS path, 8 < 2t <= 32 (layout: rs_layout.hpp RsColLayout)
-[[maybe_unused]] std::vector<uint8_t> build_rs_col_tables(int t2)
-{
-    const GfHost& G = gf();
-    std::vector<uint8_t> out((size_t)ppfs::rs_col_table_bytes(), 0);
-    const std::vector<uint8_t> g = rs_generator(t2);
-    for (int k = 0; k < 4; ++k) {
-        const std::vector<uint8_t> xk = rs_xpow_mod(t2 + k, g, t2);
-        for (int v = 0; v < 256; ++v)
-            for (int q = 0; q < t2; ++q)
-                out[(size_t)k * 8192 + (size_t)v * 32 + (size_t)(32 - t2 + q)] = G.mul((uint8_t)v, xk[q]);
-    }
-    build_gf_block(out.data() + 4 * 8192);
-    uint8_t* xp = out.data() + 4 * 8192 + 1024;
-    std::memset(xp, 0xFF, 255 * 32);
-    for (int p = 0; p < 255; ++p) {
-        const std::vector<uint8_t> xr = rs_xpow_mod(p + t2, g, t2);
-        for (int q = 0; q < t2; ++q)
-            if (xr[q])
-                xp[p * 32 + (32 - t2 + q)] = G.log[xr[q]];
-    }
-    // the same rows for x^p mod g: the single-error check on c mod g (rs_pair.hpp, RM decode)
-    uint8_t* xpm = xp + 255 * 32;
-    std::memset(xpm, 0xFF, 255 * 32);
-    for (int p = 0; p < 255; ++p) {
-        const std::vector<uint8_t> xr = rs_xpow_mod(p, g, t2);
-        for (int q = 0; q < t2; ++q)
-            if (xr[q])
-                xpm[p * 32 + (32 - t2 + q)] = G.log[xr[q]];
-    }
     return out;
 }
 
@@ -599,6 +567,16 @@ extern "C" void ppfs_ecc_destroy(ppfs_ecc_ctx* c)
     if (!c)
         return;
     DeviceGuard guard(c->device);
+    // Nothing the context queued may outlive it: its own streams drain before they are destroyed
+    // and before the staging buffers their copies and kernels use are freed.  Work the caller
+    // queued on its own streams (device entry points) is the caller's to order; the device-wide
+    // synchronize below covers it for the buffers this context owns (tables, scratch).
+    for (int i = 0; i < 2; ++i)
+        if (c->hs[i])
+            (void)hipStreamSynchronize(c->hs[i]);
+    if (c->d_tables || c->d_scratch)
+        (void)hipDeviceSynchronize();
+    (void)hipGetLastError();
     for (int i = 0; i < 2; ++i) {
         if (c->hs[i])
             (void)hipStreamDestroy(c->hs[i]);
@@ -629,7 +607,29 @@ static int check_hip(hipError_t e, const char* what)
     return 0;
 }
 
-extern "C" int ppfs_ecc_encode_device(ppfs_ecc_ctx* c, const uint8_t* d_data, uint8_t* d_raw, size_t nblocks,
+// PPFS_ECC_SYNC_CHECK=1 (debug runs): every device-resident entry point drains its stream and
+// reports an asynchronous fault of the work it queued under its own name, instead of at some later
+// unrelated call.  Off by default: the entry points are asynchronous.
+static bool sync_check_enabled()
+{
+    static const bool on = [] {
+        const char* v = std::getenv("PPFS_ECC_SYNC_CHECK");
+        return v && *v && *v != '0';
+    }();
+    return on;
+}
+
+static int sync_check(int r, void* stream, const char* what)
+{
+    if (r || !sync_check_enabled())
+        return r;
+    hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+    if (e == hipSuccess)
+        e = hipGetLastError();
+    return e != hipSuccess ? fail(PPFS_ECC_EHIP, what, e) : 0;
+}
+
+static int ppfs_ecc_encode_device_impl(ppfs_ecc_ctx* c, const uint8_t* d_data, uint8_t* d_raw, size_t nblocks,
     void* stream)
 {
     if (!c || (nblocks && (!d_data || !d_raw)))
@@ -664,7 +664,7 @@ extern "C" int ppfs_ecc_encode_device(ppfs_ecc_ctx* c, const uint8_t* d_data, ui
     return fail(PPFS_ECC_EINVAL, "bad ctx");
 }
 
-extern "C" int ppfs_ecc_decode_device(ppfs_ecc_ctx* c, uint8_t* d_raw, uint8_t* d_data, uint8_t* d_status,
+static int ppfs_ecc_decode_device_impl(ppfs_ecc_ctx* c, uint8_t* d_raw, uint8_t* d_data, uint8_t* d_status,
     size_t nblocks, int write_back, uint8_t* d_spill, void* stream)
 {
     if (!c || (nblocks && !d_raw))
@@ -713,12 +713,15 @@ extern "C" int ppfs_ecc_decode_device(ppfs_ecc_ctx* c, uint8_t* d_raw, uint8_t* 
     return fail(PPFS_ECC_EINVAL, "bad ctx");
 }
 
-static int ensure_scratch(ppfs_ecc_ctx* c, size_t bytes)
+static int ensure_scratch(ppfs_ecc_ctx* c, size_t bytes, hipStream_t s)
 {
     if (c->scratch_bytes >= bytes)
         return 0;
-    if (c->d_scratch)
+    if (c->d_scratch) {
+        // an earlier write on this stream may still read the old scratch status
+        HIP_TRY(hipStreamSynchronize(s), "scratch sync");
         (void)hipFree(c->d_scratch);
+    }
     c->d_scratch = nullptr;
     c->scratch_bytes = 0;
     HIP_TRY(hipMalloc(&c->d_scratch, bytes), "scratch alloc");
@@ -726,7 +729,7 @@ static int ensure_scratch(ppfs_ecc_ctx* c, size_t bytes)
     return 0;
 }
 
-extern "C" int ppfs_ecc_write_device(ppfs_ecc_ctx* c, const uint8_t* d_data, uint8_t* d_raw, uint8_t* d_status,
+static int ppfs_ecc_write_device_impl(ppfs_ecc_ctx* c, const uint8_t* d_data, uint8_t* d_raw, uint8_t* d_status,
     size_t nblocks, void* stream)
 {
     if (!c || (nblocks && (!d_data || !d_raw)))
@@ -736,7 +739,7 @@ extern "C" int ppfs_ecc_write_device(ppfs_ecc_ctx* c, const uint8_t* d_data, uin
     hipStream_t s = (hipStream_t)stream;
     uint8_t* st = d_status;
     if (!st) {
-        int r = ensure_scratch(c, (nblocks + 15) & ~(size_t)15);
+        int r = ensure_scratch(c, (nblocks + 15) & ~(size_t)15, s);
         if (r)
             return r;
         st = c->d_scratch;
@@ -773,6 +776,27 @@ extern "C" int ppfs_ecc_write_device(ppfs_ecc_ctx* c, const uint8_t* d_data, uin
     return fail(PPFS_ECC_EINVAL, "bad ctx");
 }
 
+extern "C" int ppfs_ecc_encode_device(ppfs_ecc_ctx* c, const uint8_t* d_data, uint8_t* d_raw, size_t nblocks,
+    void* stream)
+{
+    return sync_check(ppfs_ecc_encode_device_impl(c, d_data, d_raw, nblocks, stream), stream, "encode (async)");
+}
+
+extern "C" int ppfs_ecc_decode_device(ppfs_ecc_ctx* c, uint8_t* d_raw, uint8_t* d_data, uint8_t* d_status,
+    size_t nblocks, int write_back, uint8_t* d_spill, void* stream)
+{
+    return sync_check(
+        ppfs_ecc_decode_device_impl(c, d_raw, d_data, d_status, nblocks, write_back, d_spill, stream), stream,
+        "decode (async)");
+}
+
+extern "C" int ppfs_ecc_write_device(ppfs_ecc_ctx* c, const uint8_t* d_data, uint8_t* d_raw, uint8_t* d_status,
+    size_t nblocks, void* stream)
+{
+    return sync_check(ppfs_ecc_write_device_impl(c, d_data, d_raw, d_status, nblocks, stream), stream,
+        "write (async)");
+}
+
 // ---------------------------------------------------------------------------------------
 // Host-memory paths: chunked, double-buffered pinned staging, H2D / kernel / D2H overlapped.
 // ---------------------------------------------------------------------------------------
@@ -780,6 +804,9 @@ static int ensure_staging(ppfs_ecc_ctx* c, size_t bytes)
 {
     if (c->stage_bytes >= bytes)
         return 0;
+    for (int i = 0; i < 2; ++i)
+        if (c->hs[i])
+            HIP_TRY(hipStreamSynchronize(c->hs[i]), "staging sync");
     for (int i = 0; i < 2; ++i) {
         if (c->h_pin[i])
             (void)hipHostFree(c->h_pin[i]);
@@ -833,16 +860,41 @@ static bool raw_is_rmw(const ppfs_ecc_ctx* c)
 
 // page-locked host memory (hipHostMalloc / hipHostRegister, e.g. ppfs_ecc_host_register): the
 // DMA engines can reach it directly, so the host paths skip the CPU copy through staging
-static bool host_pinned(const void* p)
+static bool host_pinned_byte(const void* p)
 {
-    if (!p)
-        return true;
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
         return false;
     }
     return a.type == hipMemoryTypeHost;
+}
+
+// The whole range [p, p + bytes) must be page-locked before the DMA engines may touch it: a buffer
+// that starts inside a registered region and runs past its end would otherwise be DMA'd from / to
+// unlocked pages.  The runtime's allocation record of the first byte (hipMemGetAddressRange: the
+// hipHostMalloc / hipHostRegister extent) has to cover the last byte; where the runtime keeps no
+// such record the range is probed at both ends and every 64 KiB in between.
+static bool host_pinned(const void* p, size_t bytes)
+{
+    if (!p || !bytes)
+        return true;
+    const uintptr_t a = (uintptr_t)p, last = a + bytes - 1;
+    if (!host_pinned_byte(p) || !host_pinned_byte((const void*)last))
+        return false;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) == hipSuccess && base && size) {
+        const uintptr_t b = (uintptr_t)base;
+        if (b <= a && last < b + size)
+            return true;
+    }
+    (void)hipGetLastError();
+    constexpr uintptr_t kStride = 64 << 10;
+    for (uintptr_t q = (a & ~(kStride - 1)) + kStride; q < last; q += kStride)
+        if (!host_pinned_byte((const void*)q))
+            return false;
+    return true;
 }
 
 static int device_op(ppfs_ecc_ctx* c, HostOp op, uint8_t* d, const Layout& L, size_t nb, int write_back, bool want_data,
@@ -869,6 +921,8 @@ static int host_run_small(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, ui
 {
     const Layout L = layout_for(c, nb);
     if (c->zc_bytes < L.total) {
+        if (c->h_zc && c->hs[0])
+            HIP_TRY(hipStreamSynchronize(c->hs[0]), "zero-copy sync");
         if (c->h_zc)
             (void)hipHostFree(c->h_zc);
         c->h_zc = c->d_zc = nullptr;
@@ -905,6 +959,13 @@ static int host_run_small(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, ui
     return 0;
 }
 
+static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t* data_out, uint8_t* raw,
+    uint8_t* status, uint8_t* spill, size_t nblocks, int write_back);
+
+// A host call returns only once nothing it queued is still in flight: on an error part-way through
+// (a failed copy or launch in one slot) the other slot's H2D / kernel / D2H may still be running,
+// and its DMA targets the caller's buffers (direct mode) and the staging the next call reuses.
+// Both streams are drained before the error goes back; the first error's message is kept.
 static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t* data_out, uint8_t* raw,
     uint8_t* status, uint8_t* spill, size_t nblocks, int write_back)
 {
@@ -914,8 +975,22 @@ static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t*
         return 0;
     DeviceGuard guard(c->device);
     HIP_TRY(guard.err, "set device");
-    if (nblocks <= kSmallBlocks)
-        return host_run_small(c, op, data_in, data_out, raw, status, spill, nblocks, write_back);
+    const int r = nblocks <= kSmallBlocks
+        ? host_run_small(c, op, data_in, data_out, raw, status, spill, nblocks, write_back)
+        : host_run_chunks(c, op, data_in, data_out, raw, status, spill, nblocks, write_back);
+    if (r) {
+        const std::string msg = g_last_error;
+        for (int i = 0; i < 2; ++i)
+            if (c->hs[i])
+                (void)hipStreamSynchronize(c->hs[i]);
+        g_last_error = msg;
+    }
+    return r;
+}
+
+static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t* data_out, uint8_t* raw,
+    uint8_t* status, uint8_t* spill, size_t nblocks, int write_back)
+{
     const size_t chunk = std::min(nblocks, kChunkBlocks);
     const Layout L = layout_for(c, chunk);
     int r = ensure_staging(c, L.total);
@@ -926,8 +1001,8 @@ static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t*
     // fetched: the chunk's codewords already came back (staging, or the caller's page-locked image)
     bool busy[2] = { false, false }, fetched[2] = { false, false };
     // every caller buffer page-locked: DMA straight between it and the device staging buffers
-    const bool direct = host_pinned(data_in) && host_pinned(data_out) && host_pinned(raw) && host_pinned(status)
-        && host_pinned(spill);
+    const bool direct = host_pinned(data_in, nblocks * c->data) && host_pinned(data_out, nblocks * c->data)
+        && host_pinned(raw, nblocks * c->raw) && host_pinned(status, nblocks) && host_pinned(spill, nblocks * spill_b);
 
     // decode with write-back: the codewords come back only where the decode changed them
     // (status 1), read from the chunk's status once it has landed
@@ -1228,14 +1303,18 @@ extern "C" int ppfs_vote3_device(const uint8_t* d_a, const uint8_t* d_b, const u
         return fail(PPFS_ECC_EINVAL, "vote3: null argument");
     if (nrec && !rec_bytes)
         return fail(PPFS_ECC_EINVAL, "vote3: zero record size");
-    return check_hip(ppfs_vote3_launch(d_a, d_b, d_c, d_out, rec_bytes, nrec, d_damaged, (hipStream_t)stream), "vote3");
+    return sync_check(
+        check_hip(ppfs_vote3_launch(d_a, d_b, d_c, d_out, rec_bytes, nrec, d_damaged, (hipStream_t)stream), "vote3"),
+        stream, "vote3 (async)");
 }
 
 extern "C" int ppfs_copy_device(void* d_dst, const void* d_src, size_t bytes, void* stream)
 {
     if (bytes && (!d_dst || !d_src))
         return fail(PPFS_ECC_EINVAL, "copy: null argument");
-    return check_hip(ppfs_copy_launch((uint8_t*)d_dst, (const uint8_t*)d_src, bytes, (hipStream_t)stream), "copy");
+    return sync_check(
+        check_hip(ppfs_copy_launch((uint8_t*)d_dst, (const uint8_t*)d_src, bytes, (hipStream_t)stream), "copy"), stream,
+        "copy (async)");
 }
 
 extern "C" int ppfs_vote3_host(int device, const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* out,
@@ -1251,25 +1330,33 @@ extern "C" int ppfs_vote3_host(int device, const uint8_t* a, const uint8_t* b, c
     }
     DeviceGuard guard(device);
     HIP_TRY(guard.err, "set device");
+    // its own non-blocking stream, drained before anything is freed (not the legacy null stream,
+    // which does not order against other non-blocking streams)
+    hipStream_t s = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "vote3 stream");
     uint8_t* d = nullptr;
     const size_t dmg_off = (4 * nbytes + 255) & ~(size_t)255;
-    HIP_TRY(hipMalloc(&d, dmg_off + nrec * sizeof(uint32_t)), "vote3 alloc");
-    int r = 0;
-    hipError_t e = hipMemcpy(d, a, nbytes, hipMemcpyHostToDevice);
+    hipError_t e = hipMalloc(&d, dmg_off + nrec * sizeof(uint32_t));
     if (e == hipSuccess)
-        e = hipMemcpy(d + nbytes, b, nbytes, hipMemcpyHostToDevice);
+        e = hipMemcpyAsync(d, a, nbytes, hipMemcpyHostToDevice, s);
     if (e == hipSuccess)
-        e = hipMemcpy(d + 2 * nbytes, c, nbytes, hipMemcpyHostToDevice);
+        e = hipMemcpyAsync(d + nbytes, b, nbytes, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(d + 2 * nbytes, c, nbytes, hipMemcpyHostToDevice, s);
     if (e == hipSuccess)
         e = ppfs_vote3_launch(d, d + nbytes, d + 2 * nbytes, d + 3 * nbytes, rec_bytes, nrec,
-            damaged ? (uint32_t*)(d + dmg_off) : nullptr, nullptr);
+            damaged ? (uint32_t*)(d + dmg_off) : nullptr, s);
     if (e == hipSuccess)
-        e = hipMemcpy(out, d + 3 * nbytes, nbytes, hipMemcpyDeviceToHost);
+        e = hipMemcpyAsync(out, d + 3 * nbytes, nbytes, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess && damaged)
-        e = hipMemcpy(damaged, d + dmg_off, nrec * sizeof(uint32_t), hipMemcpyDeviceToHost);
-    if (e != hipSuccess)
-        r = fail(PPFS_ECC_EHIP, "vote3", e);
-    (void)hipFree(d);
+        e = hipMemcpyAsync(damaged, d + dmg_off, nrec * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+    const hipError_t es = hipStreamSynchronize(s);
+    if (e == hipSuccess)
+        e = es;
+    const int r = e != hipSuccess ? fail(PPFS_ECC_EHIP, "vote3", e) : 0;
+    if (d)
+        (void)hipFree(d);
+    (void)hipStreamDestroy(s);
     return r;
 }
 

@@ -1,7 +1,6 @@
 // rs_fast_inst.hip -- one fast-path instantiation (2t = PPFS_T2), compiled once per 2t.
 #include "rs_fast.hpp"
 #include "rs_wg.hpp"
-#include "rs_col.hpp"
 #include "rs_pair.hpp"
 
 #ifndef PPFS_T2
@@ -61,7 +60,7 @@ constexpr int DEC_NBUF = 2, DEC_WPC = 3;
 // Single-buffered tiles let 6 (encode) / 4 (decode) workgroups share a CU: the chains are
 // latency-bound, and more resident tiles beat the in-workgroup prefetch (measured at 2t = 32:
 // encode 270 -> 197 us, decode 241 -> 206 us vs 3 double-buffered workgroups).  The column
-// kernels of rs_col.hpp are kept for ablation.
+// kernels of tools/ablations/rs_col.hpp are kept for ablation.
 #ifndef PPFS_PAIR_ENC
 #define PPFS_PAIR_ENC 6, 1
 #endif

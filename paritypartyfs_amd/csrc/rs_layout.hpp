@@ -35,35 +35,16 @@ constexpr int rs_wg_table_bytes(int t2)
     return 16 * 128 + 3 * 2 * t2 * 128 + 2 * t2 * 128 + GF_BYTES;
 }
 
-// Column-split RS path (rs_col.hpp), 8 < 2t <= 32: the remainder is a 32-byte top-aligned state
-// (coefficient q at byte 32 - 2t + q), four lanes per block each holding one 8-byte column.
-//   SL   slicing-by-4, byte-indexed: table k, value v -> v * x^(2t+k) mod g as a 32-byte entry
-//        (4 tables x 256 x 32 B); lane c reads bytes [8c, 8c+8) of an entry
-//   GF   the 1 KiB EXP2 / LOG / QS block of gf_common.hpp
-//   XP   decode only: row p (32 B, state layout) = LOG of each coefficient of x^(p+2t) mod g, 0xFF
-//        for a zero coefficient -- the remainder of a single error e at byte p is e * row p,
-//        which is how the decoder confirms the single-error case (see rs_col.hpp)
-template <int T2> struct RsColLayout {
-    static_assert(T2 > 8 && T2 <= 32 && (T2 % 2) == 0, "column RS path: 2t in (8, 32]");
-    static constexpr int N = 255, K = N - T2;
-    static constexpr int ES = 32;
-    static constexpr int TBL = 256 * ES;
-    static constexpr int OFF_SL = 0;
-    static constexpr int OFF_GF = OFF_SL + 4 * TBL;
-    static constexpr int OFF_XP = OFF_GF + GF_BYTES;
-    static constexpr int ENC_BYTES = OFF_GF;              // what encode loads
-    static constexpr int TABLE_BYTES = OFF_XP + 255 * 32; // what decode loads
-    static constexpr int POFF = 32 - T2; // state byte of parity / remainder coefficient 0
-};
-
-constexpr int rs_col_table_bytes() { return 4 * 256 * 32 + GF_BYTES + 255 * 32; }
-
 // Pair RS path (rs_pair.hpp), 16 < 2t <= 32: the same 32-byte top-aligned state, two lanes per
 // block each holding a 16-byte column.
 //   SL   slicing-by-8, nibble-indexed: table t = 2i + h (byte i of the chunk, nibble h), column
 //        plane c: 16 entries x 16 B = bytes [16c, 16c+16) of (v << 4h) * x^(2t+i) mod g, at
 //        512 t + 256 c + 16 v (each plane is exactly the 64 LDS banks)
-//   GF   the 1 KiB EXP2 / LOG / QS block;  XP  as RsColLayout (decode only)
+//   GF   the 1 KiB EXP2 / LOG / QS block
+//   XP   decode only: row p (32 B, state layout) = LOG of each coefficient of x^(p+2t) mod g, 0xFF
+//        for a zero coefficient -- the remainder of a single error e at byte p is e * row p,
+//        which is how the decoder confirms the single-error case
+//   XPM  the same rows for x^p mod g (decode from c mod g)
 template <int T2> struct RsPairLayout {
     static_assert(T2 > 16 && T2 <= 32 && (T2 % 2) == 0, "pair RS path: 2t in (16, 32]");
     static constexpr int N = 255, K = N - T2;

@@ -3,9 +3,9 @@
 // (cfg5: t = 16, RS(255, 223)), conflict-free LDS lookups.
 //
 // Reference semantics: lib/blockdevice/src/rs_block_device.cpp (encode :95-117, decode :119-183;
-// see rs_col.hpp / rs_wg.hpp for the line map).
+// see rs_wg.hpp for the line map).
 //
-// The column kernels of rs_col.hpp (four lanes per block, byte-indexed tables) are bound by LDS
+// The column kernels of tools/ablations/rs_col.hpp (four lanes per block, byte-indexed tables) are bound by LDS
 // bank conflicts: a 32-lane ds_read_b64 group holds 8 blocks whose random table entries collide
 // (PMC: 56 % of LDS cycles are conflict cycles).  This design makes every lookup conflict-free:
 //   - Two lanes per block; lane c holds the 16-byte column [16c, 16c+16) of the block's 32-byte
@@ -21,14 +21,14 @@
 //     into the chunk, shift the state 8 bytes up (column 1 takes column 0's top half), and XOR in
 //     16 table entries (one ds_read_b128 each, address = one SDWA add).
 //   - 64-block tiles, 128-thread workgroups (2 waves, 32 blocks each), 3 per CU; LDS-DMA double
-//     buffering and the emission of rs_col.hpp / rs_wg.hpp.
+//     buffering and the emission of rs_emit.hpp / rs_wg.hpp.
 //   - Decode correction per pair: S_1, S_2 and the XP-row check for a single error, else all 2t
 //     syndromes (16 per lane) and the reference's BM / roots / Forney in lane 0, out of line.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "gf_common.hpp"
-#include "rs_col.hpp"
+#include "rs_emit.hpp"
 #include "rs_fast.hpp"
 #include "rs_layout.hpp"
 #include "rs_wg.hpp"
@@ -47,7 +47,7 @@ using wg::st_nt;
 
 constexpr int TB = 64;    // blocks per tile
 constexpr int NTHR = 128; // threads per workgroup: 2 waves x 32 blocks x 2 lanes
-static_assert(col::PAD == 48 && col::BUF == 16464, "emission helpers assume rs_col.hpp's tile buffer");
+static_assert(col::PAD == 48 && col::BUF == 16464, "emission helpers assume rs_emit.hpp's tile buffer");
 constexpr int PAD = col::PAD, BUF = col::BUF;
 constexpr int wpc_of(int wpc, int nbuf, int = 1, int = 0) { return (void)nbuf, wpc; }
 
@@ -234,7 +234,7 @@ __device__ __noinline__ void pair_correct_general(uint8_t* lds, uint32_t goff, u
 }
 
 // Decode correction for the pair's block; s = the lane's column of r' = x^2t c(x) mod g.  Single
-// error: S_1, S_2 -> X = S_2/S_1, e = S_1/X, confirmed iff r' == e * XP row LOG X (rs_col.hpp).
+// error: S_1, S_2 -> X = S_2/S_1, e = S_1/X, confirmed iff r' == e * XP row LOG X.
 template <int T2, bool RM = false>
 __device__ __forceinline__ uint32_t pair_correct(uint8_t* lds, uint32_t goff, const uint8_t* __restrict__ xp, uint32_t row,
     uint32_t slot,

@@ -31,6 +31,26 @@ def _ptr(x) -> Optional[int]:
     return x.data_ptr()
 
 
+def _size(x) -> int:
+    """Bytes of a uint8 buffer (numpy array or torch tensor)."""
+    return int(x.size) if isinstance(x, np.ndarray) else int(x.numel())
+
+
+def _need(name: str, x, nbytes: int, kind: str) -> None:
+    """Reject a buffer shorter than the call will touch (the library trusts its sizes: a short
+    host array would overflow the heap, a short tensor would be written out of bounds in HBM),
+    and a buffer of the wrong memory kind for the entry point."""
+    if x is None:
+        return
+    if kind == "device":
+        if isinstance(x, np.ndarray) or not getattr(x, "is_cuda", False):
+            raise ValueError(f"{name}: device entry points take CUDA tensors")
+    elif not isinstance(x, np.ndarray):
+        raise ValueError(f"{name}: host entry points take numpy arrays")
+    if _size(x) < nbytes:
+        raise ValueError(f"{name}: {_size(x)} bytes < {nbytes} needed")
+
+
 def _stream_handle(stream) -> Optional[int]:
     if stream is not None:
         return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
@@ -67,35 +87,48 @@ class EccEngine:
             pass
 
     # ---------------- device-resident batches (torch CUDA uint8 tensors) ----------------
+    def _check(self, kind, n, data=None, raw=None, status=None, spill=None) -> None:
+        if n < 0:
+            raise ValueError("nblocks must be >= 0")
+        _need("data", data, n * self.data_size, kind)
+        _need("raw", raw, n * self.raw_block_size, kind)
+        _need("status", status, n, kind)
+        _need("spill", spill, n * self.spill_bytes_per_block(), kind)
+
     def encode(self, data, raw, nblocks: Optional[int] = None, stream=None) -> None:
         n = nblocks if nblocks is not None else data.numel() // self.data_size
+        self._check("device", n, data, raw)
         check(lib().ppfs_ecc_encode_device(self._h, _ptr(data), _ptr(raw), n, _stream_handle(stream)))
 
     def decode(self, raw, data=None, status=None, write_back: bool = True, spill=None,
                nblocks: Optional[int] = None, stream=None) -> None:
         n = nblocks if nblocks is not None else raw.numel() // self.raw_block_size
+        self._check("device", n, data, raw, status, spill)
         check(lib().ppfs_ecc_decode_device(self._h, _ptr(raw), _ptr(data), _ptr(status), n, int(bool(write_back)),
                                            _ptr(spill), _stream_handle(stream)))
 
     def write(self, data, raw, status=None, nblocks: Optional[int] = None, stream=None) -> None:
         n = nblocks if nblocks is not None else data.numel() // self.data_size
+        self._check("device", n, data, raw, status)
         check(lib().ppfs_ecc_write_device(self._h, _ptr(data), _ptr(raw), _ptr(status), n,
                                           _stream_handle(stream)))
 
     # ---------------- host-memory batches (numpy uint8) ----------------
     def encode_host(self, data: np.ndarray, raw: np.ndarray) -> None:
         n = data.size // self.data_size
-        assert raw.size >= n * self.raw_block_size
+        self._check("host", n, data, raw)
         check(lib().ppfs_ecc_encode_host(self._h, _ptr(data), _ptr(raw), n))
 
     def decode_host(self, raw: np.ndarray, data: Optional[np.ndarray] = None, status: Optional[np.ndarray] = None,
                     write_back: bool = True, spill: Optional[np.ndarray] = None) -> None:
         n = raw.size // self.raw_block_size
+        self._check("host", n, data, raw, status, spill)
         check(lib().ppfs_ecc_decode_host(self._h, _ptr(raw), _ptr(data), _ptr(status), n, int(bool(write_back)),
                                          _ptr(spill)))
 
     def write_host(self, data: np.ndarray, raw: np.ndarray, status: Optional[np.ndarray] = None) -> None:
         n = data.size // self.data_size
+        self._check("host", n, data, raw, status)
         check(lib().ppfs_ecc_write_host(self._h, _ptr(data), _ptr(raw), _ptr(status), n))
 
     def spill_bytes_per_block(self) -> int:
@@ -106,6 +139,7 @@ class EccEngine:
         """readBlock(i) for every block of a host image, in order, for its write-back effect only
         (include/ppfs_ecc.h ppfs_ecc_scrub_host).  Returns (ok, corrected, failed) block counts."""
         n = nblocks if nblocks is not None else image.size // self.raw_block_size
+        self._check("host", n, raw=image, status=status)
         counts = (ctypes.c_size_t * 3)()
         check(lib().ppfs_ecc_scrub_host(self._h, _ptr(image), image.size, n, _ptr(status), counts))
         return int(counts[0]), int(counts[1]), int(counts[2])
@@ -113,6 +147,7 @@ class EccEngine:
     def scrub(self, image, status=None, nblocks: Optional[int] = None, stream=None) -> None:
         """Device-resident scrub of a torch uint8 image (ppfs_ecc_scrub_device)."""
         n = nblocks if nblocks is not None else image.numel() // self.raw_block_size
+        self._check("device", n, raw=image, status=status)
         check(lib().ppfs_ecc_scrub_device(self._h, _ptr(image), image.numel(), n, _ptr(status),
                                           _stream_handle(stream)))
 
@@ -145,18 +180,27 @@ class EccGroup:
         except Exception:
             pass
 
+    def _check(self, n, data=None, raw=None, status=None, spill=None) -> None:
+        _need("data", data, n * self.data_size, "host")
+        _need("raw", raw, n * self.raw_block_size, "host")
+        _need("status", status, n, "host")
+        _need("spill", spill, n * (256 - min(self.raw_block_size, 255)), "host")
+
     def encode_host(self, data: np.ndarray, raw: np.ndarray) -> None:
         n = data.size // self.data_size
+        self._check(n, data, raw)
         check(lib().ppfs_ecc_group_encode_host(self._h, _ptr(data), _ptr(raw), n))
 
     def decode_host(self, raw: np.ndarray, data: Optional[np.ndarray] = None, status: Optional[np.ndarray] = None,
                     write_back: bool = True, spill: Optional[np.ndarray] = None) -> None:
         n = raw.size // self.raw_block_size
+        self._check(n, data, raw, status, spill)
         check(lib().ppfs_ecc_group_decode_host(self._h, _ptr(raw), _ptr(data), _ptr(status), n,
                                                int(bool(write_back)), _ptr(spill)))
 
     def write_host(self, data: np.ndarray, raw: np.ndarray, status: Optional[np.ndarray] = None) -> None:
         n = data.size // self.data_size
+        self._check(n, data, raw, status)
         check(lib().ppfs_ecc_group_write_host(self._h, _ptr(data), _ptr(raw), _ptr(status), n))
 
 
@@ -193,6 +237,8 @@ def vote3_host(a: np.ndarray, b: np.ndarray, c: np.ndarray, rec_bytes: Optional[
     if not (a.size == b.size == c.size):
         raise ValueError("vote3: copies differ in size")
     rb = int(rec_bytes) if rec_bytes is not None else a.size
+    if rb < 0 or (rb == 0 and a.size) or (rb and a.size % rb):
+        raise ValueError("vote3: the copies must hold a whole number of records")
     nrec = a.size // rb if rb else 0
     out = np.empty_like(a)
     dmg = np.zeros(nrec, dtype=np.uint32)
@@ -202,7 +248,18 @@ def vote3_host(a: np.ndarray, b: np.ndarray, c: np.ndarray, rec_bytes: Optional[
 
 def vote3(a, b, c, out, rec_bytes: int, damaged=None, stream=None) -> None:
     """Device-resident vote3 over torch uint8 tensors; damaged: int32 tensor of nrec (or None)."""
+    if rec_bytes <= 0:
+        raise ValueError("vote3: rec_bytes must be > 0")
     nrec = a.numel() // rec_bytes
+    nbytes = nrec * rec_bytes
+    for name, x in (("b", b), ("c", c), ("out", out)):
+        _need(name, x, nbytes, "device")
+    _need("a", a, nbytes, "device")
+    if damaged is not None:
+        if damaged.element_size() != 4 or not damaged.is_contiguous() or damaged.numel() < nrec:
+            raise ValueError("vote3: damaged must be a contiguous 4-byte tensor of >= nrec elements")
+        if not damaged.is_cuda:
+            raise ValueError("vote3: damaged must be a CUDA tensor")
     dptr = None if damaged is None else damaged.data_ptr()
     check(lib().ppfs_vote3_device(_ptr(a), _ptr(b), _ptr(c), _ptr(out), rec_bytes, nrec, dptr,
                                   _stream_handle(stream)))

@@ -24,3 +24,23 @@ def gpu_available() -> bool:
 def oracle():
     from tests.oracle_lib import Oracle
     return Oracle()
+
+
+@pytest.fixture(autouse=True)
+def _gpu_fault_guard(request):
+    """After every GPU test: collect the test's garbage (engine contexts destroyed here, not at some
+    later test's GC point), then drain the device.  A fault of work a test queued asynchronously
+    is then reported against that test, not at the next unrelated torch call."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import gc
+
+    gc.collect()
+    import torch
+
+    if torch.cuda.is_available():
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError as e:  # sticky asynchronous error: name the test that queued it
+            pytest.fail(f"asynchronous GPU fault after {request.node.nodeid}: {e}", pytrace=False)

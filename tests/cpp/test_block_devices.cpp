@@ -528,6 +528,86 @@ TEST(Differential, MappedFileDiskVsOracleDeviceModel)
         differential<TestFileDisk>(c, 31337 + (uint64_t)c.type, 160);
 }
 
+// readBlocks over a range that runs past the disk end == readBlock of every block: the in-range
+// blocks are decoded (and written back / logged), the off-disk ones report Disk_OutOfBounds
+template <class D> static void straddle(const Cfg& c)
+{
+    D disk;
+    auto lg = std::make_shared<Logger>();
+    auto dev = make_dev(c, disk, lg);
+    const size_t raw = dev->rawBlockSize(), ds = dev->dataSize(), nb = dev->numOfBlocks();
+    std::vector<uint8_t> odisk(disk.size(), 0);
+    std::vector<int32_t> olog(1 << 12);
+    void* od = oracle_dev_create(c.type, c.bs, c.t, c.poly, odisk.data(), odisk.size(), olog.data(), olog.size());
+    std::mt19937_64 rng(77 + (uint64_t)c.type);
+    const size_t first = nb - 5, cnt = 9; // 5 blocks on the disk, 4 past its end
+    std::vector<uint8_t> pl(ds);
+    for (size_t b = first; b < nb; ++b) {
+        for (auto& x : pl)
+            x = (uint8_t)rng();
+        static_vector<uint8_t> v(pl.data(), ds, ds);
+        EXPECT_TRUE(dev->writeBlock(v, DataLocation((int)b, 0)).has_value());
+        size_t ow = 0;
+        oracle_dev_write(od, (int)b, 0, pl.data(), ds, &ow);
+    }
+    for (size_t b = first; b < nb; b += 2) { // one error in every other block
+        const size_t pos = b * raw + (size_t)(rng() % raw);
+        const uint8_t m = c.type == PPFS_ECC_REED_SOLOMON ? (uint8_t)(1 + rng() % 255) : (uint8_t)(1u << (rng() % 8));
+        disk.image()[pos] ^= m;
+        odisk[pos] ^= m;
+    }
+    std::vector<uint8_t> out(cnt * ds, 0xEE), err(cnt, 0xEE), obuf(4096);
+    EXPECT_TRUE(dev->readBlocks((block_index_t)first, cnt, out.data(), err.data()).has_value());
+    for (size_t i = 0; i < cnt; ++i) {
+        size_t olen = 0;
+        const int orr = oracle_dev_read(od, (int)(first + i), 0, ds, 4096, obuf.data(), &olen);
+        EXPECT_EQ((int)err[i], orr);
+        if (orr == 0)
+            EXPECT_TRUE(std::memcmp(out.data() + i * ds, obuf.data(), ds) == 0);
+    }
+    EXPECT_TRUE(std::memcmp(disk.image(), odisk.data(), odisk.size()) == 0);
+    EXPECT_EQ(lg->events.size(), oracle_dev_log_len(od));
+    oracle_dev_destroy(od);
+    ++g_checks;
+}
+
+TEST(Differential, ReadBlocksStraddlingDiskEnd)
+{
+    for (const Cfg& c : kCfgs) {
+        if (c.type == PPFS_ECC_NONE)
+            continue;
+        straddle<TestStackDisk<true>>(c);
+        straddle<TestStackDisk<false>>(c);
+    }
+}
+
+// An engine error reaches the caller as FsError::Disk_IOError (no throw, no abort): here the
+// engine cannot be created at all (no such device), so every call of the device fails that way.
+TEST(EngineErrors, PropagateAsDiskIOError)
+{
+    TestStackDisk<true> disk;
+    ReedSolomonBlockDevice rs(disk, 512, 3, nullptr, /*device=*/4096);
+    EXPECT_EQ(rs.numOfBlocks(), (size_t)0);
+    uint8_t buf[512] = { 0 };
+    static_vector<uint8_t> v(buf, sizeof buf, 16);
+    auto w = rs.writeBlock(v, DataLocation(0, 0));
+    EXPECT_TRUE(!w.has_value() && w.error() == FsError::Disk_IOError);
+    static_vector<uint8_t> r(buf, sizeof buf);
+    auto rr = rs.readBlock(DataLocation(0, 0), 16, r);
+    EXPECT_TRUE(!rr.has_value() && rr.error() == FsError::Disk_IOError);
+    uint8_t err[2] = { 0, 0 };
+    auto rb = rs.readBlocks(0, 2, buf, err);
+    EXPECT_TRUE(!rb.has_value() && rb.error() == FsError::Disk_IOError);
+    auto wb = rs.writeBlocks(0, 1, buf, err);
+    EXPECT_TRUE(!wb.has_value() && wb.error() == FsError::Disk_IOError);
+    size_t counts[3];
+    auto sc = rs.scrub(0, 1, counts, err);
+    EXPECT_TRUE(!sc.has_value());
+    CrcBlockDevice crc(CrcPolynomial::MsgImplicit(0x9960034c), disk, 512, nullptr, 4096);
+    auto f = crc.formatBlock(0);
+    EXPECT_TRUE(!f.has_value() && f.error() == FsError::Disk_IOError);
+}
+
 TEST(MappedFileDisk, FileDiskChecks)
 {
     MappedFileDisk d;

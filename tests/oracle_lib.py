@@ -38,10 +38,14 @@ class Oracle:
         L.oracle_gf_div.argtypes = [c_uint8, c_uint8]
         L.oracle_gf_inv.restype = c_uint8
         L.oracle_gf_inv.argtypes = [c_uint8]
+        L.oracle_gf_dump.restype = None
+        L.oracle_gf_dump.argtypes = [vp, vp, vp, vp, vp]
         L.oracle_rs_sizes.argtypes = [c_int, c_int, POINTER(c_int), POINTER(c_int)]
         L.oracle_rs_generator.argtypes = [c_int, c_int, vp]
         L.oracle_rs_encode.argtypes = [c_int, c_int, vp, vp, c_size_t]
         L.oracle_rs_decode.argtypes = [c_int, c_int, vp, vp, vp, vp, vp, c_size_t]
+        L.oracle_rs_encode_table.argtypes = [c_int, c_int, vp, vp, c_size_t]
+        L.oracle_rs_decode_table.argtypes = [c_int, c_int, vp, vp, vp, vp, c_size_t]
         L.oracle_rs_decode_one_full.argtypes = [c_int, c_int, vp, vp, vp, POINTER(c_int32), POINTER(c_int32)]
         L.oracle_crc_implicit_to_explicit.restype = c_uint64
         L.oracle_crc_implicit_to_explicit.argtypes = [c_uint64]
@@ -70,6 +74,15 @@ class Oracle:
         L.oracle_dev_write.argtypes = [vp, c_int, c_size_t, vp, c_size_t, POINTER(c_size_t)]
 
     # ---------------- GF / RS ----------------
+    def gf_dump(self):
+        """{mul, div (256 x 256), inv, log, pow} of the oracle's GF(2^8) (oracle_gf_dump)."""
+        t = {k: np.zeros(n, np.uint8) for k, n in (("mul", 65536), ("div", 65536), ("inv", 256), ("log", 256),
+                                                     ("pow", 256))}
+        self.L.oracle_gf_dump(*[_p(t[k]) for k in ("mul", "div", "inv", "log", "pow")])
+        t["mul"] = t["mul"].reshape(256, 256)
+        t["div"] = t["div"].reshape(256, 256)
+        return t
+
     def rs_sizes(self, block_size, t):
         n, k = c_int(), c_int()
         tt = self.L.oracle_rs_sizes(block_size, t, ctypes.byref(n), ctypes.byref(k))
@@ -99,6 +112,26 @@ class Oracle:
         wbl = np.zeros(nb, np.int32)
         rc = self.L.oracle_rs_decode(block_size, t, _p(raw), _p(data), _p(status), _p(fixed), _p(wbl), nb)
         return data, status, fixed, wbl, rc
+
+    def rs_encode_table(self, block_size, t, data):
+        """The table-driven (LFSR) encode of the CPU baseline's optimised column."""
+        n, k, _ = self.rs_sizes(block_size, t)
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        nb = data.size // k
+        raw = np.zeros(nb * n, np.uint8)
+        assert self.L.oracle_rs_encode_table(block_size, t, _p(data), _p(raw), nb) == 0
+        return raw
+
+    def rs_decode_table(self, block_size, t, raw):
+        """Table syndromes + the restated decode for non-zero ones: (data, status, fixed, rc)."""
+        n, k, _ = self.rs_sizes(block_size, t)
+        raw = np.ascontiguousarray(raw, dtype=np.uint8)
+        nb = raw.size // n
+        data = np.zeros(nb * k, np.uint8)
+        status = np.zeros(nb, np.uint8)
+        fixed = np.zeros(nb * n, np.uint8)
+        rc = self.L.oracle_rs_decode_table(block_size, t, _p(raw), _p(data), _p(status), _p(fixed), nb)
+        return data, status, fixed, rc
 
     def rs_decode_one_full(self, block_size, t, raw):
         n, k, _ = self.rs_sizes(block_size, t)

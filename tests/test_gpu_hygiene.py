@@ -1,0 +1,161 @@
+"""GPU tests of the engine's boundary hygiene (round-2 fixes of the asynchronous-fault suspects):
+
+- the Python mirror rejects buffers shorter than a call touches, and buffers of the wrong kind,
+  before anything reaches the C ABI (an undersized host array would overflow the heap, an
+  undersized tensor would be written out of bounds in HBM);
+- a host buffer that is only partly page-locked is not DMA'd directly (api.cpp host_pinned checks
+  the whole range) and still gives the oracle's results;
+- destroying a context right after queueing device work on the caller's stream is safe: the
+  context's tables stay alive until that work is done (ppfs_ecc_destroy drains first);
+- the C++ adapter propagates engine errors as Disk_IOError (tests/cpp, EngineErrors).
+"""
+import numpy as np
+import pytest
+
+from tests.conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+if gpu_available():
+    import torch
+
+from paritypartyfs_amd import ECC_CRC, ECC_HAMMING, ECC_REED_SOLOMON, EccEngine, EccGroup, pinned, vote3, vote3_host
+
+
+def test_short_and_wrong_kind_buffers_rejected():
+    eng = EccEngine(ECC_REED_SOLOMON, 512, 3)
+    n, k = eng.raw_block_size, eng.data_size
+    nb = 100
+    d = torch.zeros(nb * k, dtype=torch.uint8, device="cuda")
+    r = torch.zeros(nb * n, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+    with pytest.raises(ValueError):
+        eng.encode(d, r[: nb * n - 1], nblocks=nb)
+    with pytest.raises(ValueError):
+        eng.encode(d[:-1], r, nblocks=nb)
+    with pytest.raises(ValueError):
+        eng.decode(r, d, st[:-1], nblocks=nb)
+    with pytest.raises(ValueError):
+        eng.decode(r, d[: nb * k - 5], st, nblocks=nb)
+    with pytest.raises(ValueError):
+        eng.write(d, r[:10], st, nblocks=nb)
+    with pytest.raises(ValueError):  # host array into a device entry point
+        eng.encode(np.zeros(nb * k, np.uint8), r, nblocks=nb)
+    hd, hr, hs = np.zeros(nb * k, np.uint8), np.zeros(nb * n, np.uint8), np.zeros(nb, np.uint8)
+    with pytest.raises(ValueError):
+        eng.encode_host(hd, hr[:-1])
+    with pytest.raises(ValueError):
+        eng.decode_host(hr, hd[:-1], hs)
+    with pytest.raises(ValueError):
+        eng.decode_host(hr, hd, hs[:-1])
+    with pytest.raises(ValueError):
+        eng.write_host(hd, hr, hs[:3])
+    with pytest.raises(ValueError):  # tensor into a host entry point
+        eng.encode_host(d, hr)
+    with pytest.raises(ValueError):
+        eng.scrub_host(hr, nblocks=nb + 1)
+    # right-sized calls still work
+    eng.encode(d, r, nblocks=nb)
+    eng.decode(r, d, st, nblocks=nb)
+    torch.cuda.synchronize()
+    assert int(st.max()) == 0
+    grp = EccGroup(ECC_REED_SOLOMON, 512, 3, devices=(0, 0))
+    with pytest.raises(ValueError):
+        grp.decode_host(hr, hd, hs[:-1])
+    grp.close()
+    eng.close()
+
+
+def test_vote3_rejects_bad_sizes():
+    a = np.zeros(49 * 3 + 5, np.uint8)
+    with pytest.raises(ValueError):  # ragged tail
+        vote3_host(a, a, a, 49)
+    ta = torch.zeros(49 * 4, dtype=torch.uint8, device="cuda")
+    out = torch.empty_like(ta)
+    with pytest.raises(ValueError):
+        vote3(ta, ta[:-1], ta, out, 49)
+    with pytest.raises(ValueError):
+        vote3(ta, ta, ta, out[:10], 49)
+    with pytest.raises(ValueError):
+        vote3(ta, ta, ta, out, 49, torch.zeros(3, dtype=torch.int32, device="cuda"))
+    dmg = torch.zeros(4, dtype=torch.int32, device="cuda")
+    vote3(ta, ta, ta, out, 49, dmg)
+    torch.cuda.synchronize()
+    assert int(dmg.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("codec", ["rs512", "ham1024"])
+def test_partly_registered_buffer_is_staged(oracle, codec):
+    """Only the first half of the codeword image is page-locked: the call must not take the direct
+    DMA path over the unlocked half, and its results equal the fully pageable and fully pinned
+    ones (and the oracle's for RS)."""
+    if codec == "rs512":
+        eng = EccEngine(ECC_REED_SOLOMON, 512, 3)
+    else:
+        eng = EccEngine(ECC_HAMMING, 1024)
+    n, k = eng.raw_block_size, eng.data_size
+    nb = 70001
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 256, nb * k, dtype=np.uint8)
+    results = []
+    for mode in ("pageable", "half", "full"):
+        raw = np.zeros(nb * n, np.uint8)
+        if mode == "half":
+            half = raw[: (nb // 2) * n]
+            with pinned(half, data):
+                eng.encode_host(data, raw)
+        elif mode == "full":
+            with pinned(raw, data):
+                eng.encode_host(data, raw)
+        else:
+            eng.encode_host(data, raw)
+        results.append(raw)
+    assert np.array_equal(results[0], results[1]) and np.array_equal(results[0], results[2])
+    if codec == "rs512":
+        assert np.array_equal(results[0], oracle.rs_encode(512, 3, data))
+    eng.close()
+
+
+def test_destroy_right_after_queued_work(oracle):
+    """close() immediately after queueing a large encode on the caller's stream: the kernels still
+    read the context's tables, so destroy must wait for them (results stay bit-exact)."""
+    rng = np.random.default_rng(8)
+    for typ, bs, t, poly in ((ECC_REED_SOLOMON, 512, 3, 0), (ECC_REED_SOLOMON, 4096, 16, 0),
+                             (ECC_CRC, 4096, 0, (0x9960034C << 1) + 1)):
+        eng = EccEngine(typ, bs, t, crc_polynomial_explicit=poly)
+        n, k = eng.raw_block_size, eng.data_size
+        nb = 1 << 16
+        data = rng.integers(0, 256, nb * k, dtype=np.uint8)
+        d = torch.from_numpy(data).cuda()
+        r = torch.zeros(nb * n, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        for _ in range(4):
+            eng.encode(d, r)
+        eng.close()  # work still in flight on the current stream
+        torch.cuda.synchronize()
+        got = r.cpu().numpy()
+        if typ == ECC_REED_SOLOMON:
+            want = oracle.rs_encode(bs, t, data[: 2048 * k])
+        else:
+            want = oracle.crc_encode(bs, poly, data[: 2048 * k], raw_old=np.zeros(2048 * n, np.uint8))
+        assert np.array_equal(got[: 2048 * n], want)
+
+
+def test_many_contexts_created_and_destroyed_across_threads(oracle):
+    """Contexts whose streams were first used on worker threads (group shards) and destroyed on
+    the main thread, interleaved with device work on torch's stream: no fault, same results."""
+    rng = np.random.default_rng(9)
+    data = rng.integers(0, 256, 20000 * 249, dtype=np.uint8)
+    want = oracle.rs_encode(512, 3, data)
+    for rep in range(6):
+        grp = EccGroup(ECC_REED_SOLOMON, 512, 3, devices=(0,) * (2 + rep % 3))
+        raw = np.zeros(20000 * 255, np.uint8)
+        grp.encode_host(data, raw)
+        d = torch.from_numpy(data).cuda()
+        r = torch.zeros(20000 * 255, dtype=torch.uint8, device="cuda")
+        eng = EccEngine(ECC_REED_SOLOMON, 512, 3)
+        eng.encode(d, r)
+        grp.close()
+        eng.close()
+        assert np.array_equal(raw, want)
+        assert np.array_equal(r.cpu().numpy(), want)

@@ -606,6 +606,7 @@ def test_group_host_path_matches_single_context(oracle, devices, codec):
         res.append((img, st))
     assert np.array_equal(res[0][0], res[1][0]) and np.array_equal(res[0][1], res[1][1])
     grp.close()
+    one.close()
 
 
 @pytest.mark.parametrize("nb", [1, 3, 31, 33, 129])

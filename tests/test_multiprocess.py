@@ -45,3 +45,31 @@ def test_gloo_world2_max_over_ranks():
     res = dict(q.get() for _ in range(world))
     assert abs(res[0] - res[1]) < 1e-9  # every rank reports the max
     assert res[0] >= 3 * 0.02 * world * 0.95
+
+
+def test_bench_gpus2_launches_two_ranks():
+    """The driver's command form `python bench.py --gpus 2` starts two ranks itself (torchrun as a
+    child process) and reports n_gpus 2 with the slowest rank's time.  The engine is replaced by
+    bench.py's CPU stand-in (--dry-run-cpu, gloo): this exercises the launcher, the barrier and the
+    max-over-ranks, not the kernels."""
+    import json
+    import subprocess
+
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "5",
+                        "--warmup", "1", "--dry-run-cpu"], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["dry_run"] and line["steps"] == 5
+    assert line["ms_per_step"] >= 2.0 * 0.95  # rank 1's stand-in sleeps 2 ms per step
+
+
+def test_bench_rejects_world_mismatch():
+    import subprocess
+
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--dry-run-cpu"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE" in r.stderr

@@ -44,6 +44,52 @@ def test_bits_msb_first():
     assert bits == [0] * u["zeros_then_ones"] + [1] * (64 - u["zeros_then_ones"])
 
 
+# ---------------- the reference's GF256 binary (oracle/_ref) ----------------
+GF_GOLD = os.path.join(os.path.dirname(__file__), "golden", "gf256_ref.npz")
+REF_GF_LIB = os.path.join(os.path.dirname(os.path.dirname(__file__)), "oracle", "_ref", "libppfs_ref_gf256.so")
+
+
+def test_gf256_matches_reference_binary_fixture(oracle):
+    """Every product, quotient (a/0 = 0), inverse (inv 0 = 0), log and power of the oracle's
+    GF(2^8) equals the reference's own GF256 (gf256.cpp:6-83, compiled unmodified into
+    oracle/_ref by oracle/Makefile; fixture written by tests/golden/gen_gf256_ref.py)."""
+    gold = np.load(GF_GOLD)  # plain arrays, allow_pickle=False
+    mine = oracle.gf_dump()
+    for k in ("mul", "div", "inv", "log", "pow"):
+        assert np.array_equal(mine[k], gold[k]), k
+    # spot facts of the reference field: alpha = 2 over 0x11D, EXP[255] = EXP[0] (gf256.cpp:16)
+    assert gold["pow"][8] == 0x1D and gold["pow"][255] == 1 and gold["div"][7, 0] == 0
+
+
+def test_gf256_matches_reference_binary_live(oracle):
+    """Same check against the reference binary itself, where it was built (this container)."""
+    if not os.path.exists(REF_GF_LIB):
+        pytest.skip("oracle/_ref not built (no /root/reference here): the committed fixture pins it")
+    from tests.golden.gen_gf256_ref import dump
+
+    ref = dump(REF_GF_LIB)
+    mine = oracle.gf_dump()
+    for k in ref:
+        assert np.array_equal(mine[k], ref[k]), k
+
+
+def test_rs_generator_from_reference_field():
+    """g(x) = prod_{i=1..2t} (x + alpha^i) (rs_block_device.cpp:195-208) multiplied out over the
+    reference binary's own product table gives the SURVEY-recorded generators."""
+    gold = np.load(GF_GOLD)
+    mul, pw = gold["mul"], gold["pow"]
+    for t, want in ((3, GOLD["survey_recorded"]["rs_generator"]["t3"]),
+                    (16, GOLD["survey_recorded"]["rs_generator"]["t16"])):
+        g = [1]
+        for i in range(1, 2 * t + 1):
+            ng = [0] * (len(g) + 1)
+            for k, c in enumerate(g):
+                ng[k] ^= int(mul[c, pw[i]])
+                ng[k + 1] ^= c
+            g = ng
+        assert bytes(g).hex() == want
+
+
 # ---------------- SURVEY-recorded reference outputs ----------------
 def test_rs_generator_kats(oracle):
     g = GOLD["survey_recorded"]["rs_generator"]
@@ -228,3 +274,26 @@ def test_hamming_oracle_layout():
     assert (bs, ds) == (4096, 4091)
     idx = RM.hamming_data_indices(bs, ds)
     assert idx[:5] == [3, 5, 6, 7, 9] and idx[-1] == 32743
+
+
+@pytest.mark.parametrize("bs,t", [(512, 3), (255, 1), (256, 4), (4096, 8), (4096, 16), (64, 3), (128, 10)])
+def test_table_codec_equals_long_division(oracle, bs, t):
+    """The CPU baseline's optimised column (LFSR encode, table syndromes) gives the restated
+    long-division encode's codewords and its decode's payloads / statuses / write-backs."""
+    n, k, tt = oracle.rs_sizes(bs, t)
+    rng = np.random.default_rng(bs * 100 + t)
+    nb = 400
+    data = rng.integers(0, 256, nb * k, dtype=np.uint8)
+    cw = oracle.rs_encode(bs, t, data)
+    assert np.array_equal(oracle.rs_encode_table(bs, t, data), cw)
+    bad = cw.reshape(nb, n).copy()
+    for b in range(nb):
+        ne = b % (tt + 3)
+        pos = rng.choice(n, ne, replace=False)
+        bad[b, pos] ^= rng.integers(1, 256, ne, dtype=np.uint8)
+    bad = bad.reshape(-1)
+    d1, s1, f1, _, rc1 = oracle.rs_decode(bs, t, bad)
+    d2, s2, f2, rc2 = oracle.rs_decode_table(bs, t, bad)
+    assert rc1 == rc2
+    if rc1 == 0:
+        assert np.array_equal(d1, d2) and np.array_equal(s1, s2) and np.array_equal(f1, f2)

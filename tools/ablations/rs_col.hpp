@@ -1,3 +1,4 @@
+// ABLATION ONLY (not built into libppfs_ecc.so): include with -I paritypartyfs_amd/csrc.
 #pragma once
 // rs_col.hpp -- workgroup RS(255, 255-2t) encode / decode for gfx950 with 8 < 2t <= 32
 // (cfg5: t = 16, RS(255, 223)).
@@ -36,8 +37,33 @@
 #include "rs_fast.hpp"
 #include "rs_layout.hpp"
 #include "rs_wg.hpp"
+#include "rs_emit.hpp"
 
 namespace ppfs {
+// Column-split RS path (rs_col.hpp), 8 < 2t <= 32: the remainder is a 32-byte top-aligned state
+// (coefficient q at byte 32 - 2t + q), four lanes per block each holding one 8-byte column.
+//   SL   slicing-by-4, byte-indexed: table k, value v -> v * x^(2t+k) mod g as a 32-byte entry
+//        (4 tables x 256 x 32 B); lane c reads bytes [8c, 8c+8) of an entry
+//   GF   the 1 KiB EXP2 / LOG / QS block of gf_common.hpp
+//   XP   decode only: row p (32 B, state layout) = LOG of each coefficient of x^(p+2t) mod g, 0xFF
+//        for a zero coefficient -- the remainder of a single error e at byte p is e * row p,
+//        which is how the decoder confirms the single-error case (see rs_col.hpp)
+template <int T2> struct RsColLayout {
+    static_assert(T2 > 8 && T2 <= 32 && (T2 % 2) == 0, "column RS path: 2t in (8, 32]");
+    static constexpr int N = 255, K = N - T2;
+    static constexpr int ES = 32;
+    static constexpr int TBL = 256 * ES;
+    static constexpr int OFF_SL = 0;
+    static constexpr int OFF_GF = OFF_SL + 4 * TBL;
+    static constexpr int OFF_XP = OFF_GF + GF_BYTES;
+    static constexpr int ENC_BYTES = OFF_GF;              // what encode loads
+    static constexpr int TABLE_BYTES = OFF_XP + 255 * 32; // what decode loads
+    static constexpr int POFF = 32 - T2; // state byte of parity / remainder coefficient 0
+};
+
+constexpr int rs_col_table_bytes() { return 4 * 256 * 32 + GF_BYTES + 255 * 32; }
+
+
 namespace col {
 
 using wg::barrier_lds;
@@ -49,10 +75,7 @@ using wg::st_bytes;
 using wg::st_nt;
 using wg::stage_bytes;
 
-constexpr int TB = 64;                   // blocks per tile
 constexpr int NTHR = 256;                // threads per workgroup
-constexpr int PAD = 48;                  // front pad of a tile buffer
-constexpr int BUF = PAD + TB * 255 + 96; // 16464: windows read up to 2t + 20 bytes past a piece
 
 // quad_perm DPP controls
 constexpr int QP_BCAST3 = 0xFF; // [3,3,3,3]: column 3 to every lane of the quad
@@ -112,82 +135,6 @@ __device__ __forceinline__ void col_remainder(uint32_t& lo_out, uint32_t& hi_out
     hi_out = hi;
 }
 
-// 16 bytes at any LDS byte address, from the two aligned 16-byte pieces that cover them.
-// Emission lanes read consecutive 16-byte pieces: as ds_read_b128 a 16-lane group then covers
-// the 64 banks exactly, where five ds_read_b32 per lane (lane stride 4 dwords) hit each bank
-// 4 times per 32-lane group.  The per-lane dword offset is selected with two v_bfi levels.
-__device__ __forceinline__ void win16(uint32_t (&X)[4], const uint8_t* lds, uint32_t addr)
-{
-    const uint32_t a16 = addr & ~15u;
-    const uint4 A = *(const uint4*)(lds + a16), B = *(const uint4*)(lds + a16 + 16);
-    const uint32_t D[8] = { A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w };
-    const uint32_t sh = (addr & 3u) * 8u;
-    // masks, not selects: LLVM folds a select between array elements into a dynamic index (scratch)
-    const uint32_t m2 = 0u - ((addr >> 3) & 1u), m1 = 0u - ((addr >> 2) & 1u);
-    uint32_t F[6], E[5];
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-        F[i] = bfi(m2, D[i + 2], D[i]);
-#pragma unroll
-    for (int i = 0; i < 5; ++i)
-        E[i] = bfi(m1, F[i + 1], F[i]);
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-        X[m] = __builtin_amdgcn_alignbit(E[m + 1], E[m], sh);
-}
-
-__device__ __forceinline__ uint32_t mword(const M128& mk, int m)
-{
-    return (uint32_t)((m < 2 ? mk.lo : mk.hi) >> ((m & 1) * 32));
-}
-
-// Encode emission: 16 bytes of the codeword tile at piece p.  Codeword byte j of block b = j / 255
-// (off = j % 255) is parity byte off (slot byte POFF + off) if off < 2t, else payload byte
-// K b + off - 2t; a piece may run into block b+1 (off > 239), whose parity and payload follow.
-template <int T2>
-__device__ __forceinline__ uint4 col_enc_piece(const uint8_t* lds, uint32_t buf, uint32_t par, uint32_t p)
-{
-    constexpr uint32_t K = 255 - T2, POFF = 32 - T2;
-    const uint32_t j0 = p * 16u, b = j0 / 255u, off = j0 - 255u * b;
-    const uint32_t S = buf + PAD + K * b + off - T2;   // payload source of output byte 0
-    const uint32_t kb = off > 239u ? 255u - off : 16u; // first byte of block b+1 in the piece
-    const uint32_t c0 = off < (uint32_t)T2 ? min((uint32_t)T2 - off, 16u) : 0u; // leading parity bytes
-    const uint32_t e1 = min(kb + (uint32_t)T2, 16u);   // end of block b+1's parity bytes
-    uint32_t X[4], Y[4], P0[4], P1[4];
-    win16(X, lds, S);
-    win16(Y, lds, S - T2); // block b+1 payload: 2t bytes behind
-    win16(P0, lds, par + 32u * b + POFF + (c0 ? off : 0u));
-    win16(P1, lds, par + 32u * (b + 1u) + POFF - kb);
-    const M128 mY = range_mask(e1, 16), mP1 = range_mask(kb, e1), mP0 = range_mask(0, c0);
-    uint32_t o[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        uint32_t v = bfi(mword(mY, m), Y[m], X[m]);
-        v = bfi(mword(mP1, m), P1[m], v);
-        o[m] = bfi(mword(mP0, m), P0[m], v);
-    }
-    return make_uint4(o[0], o[1], o[2], o[3]);
-}
-
-// Decode emission: 16 bytes of the payload tile at piece p: payload byte j of block b = j / K
-// (off = j % K) is codeword byte 255 b + 2t + off; past the block end the source skips block
-// b+1's 2t parity bytes.
-template <int T2> __device__ __forceinline__ uint4 col_dec_piece(const uint8_t* lds, uint32_t buf, uint32_t p)
-{
-    constexpr uint32_t K = 255 - T2;
-    const uint32_t j0 = p * 16u, b = j0 / K, off = j0 - K * b;
-    const uint32_t S = buf + PAD + 255u * b + T2 + off;
-    const uint32_t kb = off > K - 16u ? K - off : 16u;
-    uint32_t X[4], Z[4];
-    win16(X, lds, S);
-    win16(Z, lds, S + T2);
-    const M128 mZ = range_mask(kb, 16);
-    uint32_t o[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-        o[m] = bfi(mword(mZ, m), Z[m], X[m]);
-    return make_uint4(o[0], o[1], o[2], o[3]);
-}
 
 __device__ __forceinline__ uint32_t quad_xor(uint32_t v)
 {
@@ -202,17 +149,6 @@ __device__ __forceinline__ uint32_t quad_or(uint32_t v)
     return v;
 }
 
-// codeword byte `pos` of the LDS row ^= ev, and the same byte in HBM with write-back
-__device__ __forceinline__ void col_fix(uint8_t* lds, uint32_t row, uint8_t* __restrict__ raw_g, uint64_t gblk, bool wb,
-    uint32_t pos, uint32_t ev)
-{
-    if (ev == 0)
-        return;
-    const uint8_t fixed = (uint8_t)(lds[row + pos] ^ ev);
-    lds[row + pos] = fixed;
-    if (wb)
-        raw_g[gblk * 255u + pos] = fixed;
-}
 
 // General correction (2+ errors; out of line so its registers do not weigh on the streaming path).
 // Called by all four lanes of a quad whose block is not a single error: lane c computes S_i for

@@ -20,7 +20,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BENCH_ARGS = "bench.py --steps 50 --warmup 5 --prewarm-s 0.3 --no-cpu-baseline"
+BENCH_ARGS = "bench.py --steps 50 --warmup 5 --prewarm-s 0.3 --no-cpu-baseline --no-host-inclusive"
 
 
 def short(name):
@@ -78,7 +78,10 @@ def main():
     for k, v in latest.items():
         lines.append(f"- `{v['kernel_full']}`: " + ", ".join(f"{a}={b:.4g}" for a, b in sorted(v["counters"].items())))
     open(os.path.join(prof, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
-    json.dump({"tag": tag, "kernels": latest}, open(os.path.join(prof, "pmc_latest.json"), "w"), indent=1)
+    sha_path = os.path.join(d, "lib.sha256")  # the library build the counters were collected on
+    lib_sha = open(sha_path).read().strip() if os.path.exists(sha_path) else None
+    json.dump({"tag": tag, "lib_sha256": lib_sha, "kernels": latest},
+              open(os.path.join(prof, "pmc_latest.json"), "w"), indent=1)
     print("\n".join(lines))
 
 
