@@ -51,6 +51,13 @@ def _need(name: str, x, nbytes: int, kind: str) -> None:
         raise ValueError(f"{name}: {_size(x)} bytes < {nbytes} needed")
 
 
+def _host_blocks(x, per_block: int, name: str) -> int:
+    """Blocks a host array holds (the block count the *_host calls take from it)."""
+    if not isinstance(x, np.ndarray):
+        raise ValueError(f"{name}: host entry points take numpy arrays")
+    return x.size // per_block
+
+
 def _stream_handle(stream) -> Optional[int]:
     if stream is not None:
         return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
@@ -115,19 +122,19 @@ class EccEngine:
 
     # ---------------- host-memory batches (numpy uint8) ----------------
     def encode_host(self, data: np.ndarray, raw: np.ndarray) -> None:
-        n = data.size // self.data_size
+        n = _host_blocks(data, self.data_size, "data")
         self._check("host", n, data, raw)
         check(lib().ppfs_ecc_encode_host(self._h, _ptr(data), _ptr(raw), n))
 
     def decode_host(self, raw: np.ndarray, data: Optional[np.ndarray] = None, status: Optional[np.ndarray] = None,
                     write_back: bool = True, spill: Optional[np.ndarray] = None) -> None:
-        n = raw.size // self.raw_block_size
+        n = _host_blocks(raw, self.raw_block_size, "raw")
         self._check("host", n, data, raw, status, spill)
         check(lib().ppfs_ecc_decode_host(self._h, _ptr(raw), _ptr(data), _ptr(status), n, int(bool(write_back)),
                                          _ptr(spill)))
 
     def write_host(self, data: np.ndarray, raw: np.ndarray, status: Optional[np.ndarray] = None) -> None:
-        n = data.size // self.data_size
+        n = _host_blocks(data, self.data_size, "data")
         self._check("host", n, data, raw, status)
         check(lib().ppfs_ecc_write_host(self._h, _ptr(data), _ptr(raw), _ptr(status), n))
 
@@ -138,7 +145,7 @@ class EccEngine:
     def scrub_host(self, image: np.ndarray, nblocks: Optional[int] = None, status: Optional[np.ndarray] = None):
         """readBlock(i) for every block of a host image, in order, for its write-back effect only
         (include/ppfs_ecc.h ppfs_ecc_scrub_host).  Returns (ok, corrected, failed) block counts."""
-        n = nblocks if nblocks is not None else image.size // self.raw_block_size
+        n = nblocks if nblocks is not None else _host_blocks(image, self.raw_block_size, "image")
         self._check("host", n, raw=image, status=status)
         counts = (ctypes.c_size_t * 3)()
         check(lib().ppfs_ecc_scrub_host(self._h, _ptr(image), image.size, n, _ptr(status), counts))
@@ -187,19 +194,19 @@ class EccGroup:
         _need("spill", spill, n * (256 - min(self.raw_block_size, 255)), "host")
 
     def encode_host(self, data: np.ndarray, raw: np.ndarray) -> None:
-        n = data.size // self.data_size
+        n = _host_blocks(data, self.data_size, "data")
         self._check(n, data, raw)
         check(lib().ppfs_ecc_group_encode_host(self._h, _ptr(data), _ptr(raw), n))
 
     def decode_host(self, raw: np.ndarray, data: Optional[np.ndarray] = None, status: Optional[np.ndarray] = None,
                     write_back: bool = True, spill: Optional[np.ndarray] = None) -> None:
-        n = raw.size // self.raw_block_size
+        n = _host_blocks(raw, self.raw_block_size, "raw")
         self._check(n, data, raw, status, spill)
         check(lib().ppfs_ecc_group_decode_host(self._h, _ptr(raw), _ptr(data), _ptr(status), n,
                                                int(bool(write_back)), _ptr(spill)))
 
     def write_host(self, data: np.ndarray, raw: np.ndarray, status: Optional[np.ndarray] = None) -> None:
-        n = data.size // self.data_size
+        n = _host_blocks(data, self.data_size, "data")
         self._check(n, data, raw, status)
         check(lib().ppfs_ecc_group_write_host(self._h, _ptr(data), _ptr(raw), _ptr(status), n))
 
