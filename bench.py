@@ -408,30 +408,41 @@ def main(argv=None):
     he.close()
 
     # (2) standalone kernels: L back-to-back launches of one kernel, fence-free events between
-    # them (the north-star measurement: RS encode over the 1 M-block batch on its own)
+    # them (the north-star measurement: RS encode over the 1 M-block batch on its own).  "hot":
+    # every launch on the same buffers, so part of the 261 MB input can still sit in the 256 MB
+    # Infinity Cache from the previous launch; "cold": the launches rotate over R independent
+    # buffer sets (R x 0.5 GB), so every launch reads its input from HBM.
     L = max(3, args.standalone_launches)
+    R = 4
     hs = HipEvents(L + 1)
+
+    def time_launches(fn):
+        for i in range(3):
+            fn(i)
+        hs.record(0, stream)
+        for i in range(L):
+            fn(i)
+            hs.record(i + 1, stream)
+        torch.cuda.synchronize()
+        return [hs.ms(i, i + 1) for i in range(L)]
+
     rewarm(0.3)
-    for _ in range(3):
-        eng.encode(data, cw, nblocks=nb)
-    hs.record(0, stream)
-    for i in range(L):
-        eng.encode(data, cw, nblocks=nb)
-        hs.record(i + 1, stream)
-    torch.cuda.synchronize()
-    enc_sa = [hs.ms(i, i + 1) for i in range(L)]
+    enc_sa = time_launches(lambda i: eng.encode(data, cw, nblocks=nb))
     assert torch.equal(cw, clean_cw), "standalone encode output differs"
     # clean decode (status + write-back enabled, nothing to correct): the read path of a scrub
     rewarm(0.3)
     eng.encode(data, cw, nblocks=nb)
-    for _ in range(3):
-        eng.decode(cw, out, status, write_back=True, nblocks=nb)
-    hs.record(0, stream)
-    for i in range(L):
-        eng.decode(cw, out, status, write_back=True, nblocks=nb)
-        hs.record(i + 1, stream)
-    torch.cuda.synchronize()
-    dec_sa = [hs.ms(i, i + 1) for i in range(L)]
+    dec_sa = time_launches(lambda i: eng.decode(cw, out, status, write_back=True, nblocks=nb))
+    d_rot = [data] + [torch.randint(0, 256, (nb * k,), dtype=torch.uint8, device=dev, generator=gen)
+                      for _ in range(R - 1)]
+    c_rot = [torch.empty(nb * n, dtype=torch.uint8, device=dev) for _ in range(R)]
+    o_rot = [torch.empty(nb * k, dtype=torch.uint8, device=dev) for _ in range(R)]
+    rewarm(0.3)
+    enc_cold = time_launches(lambda i: eng.encode(d_rot[i % R], c_rot[i % R], nblocks=nb))
+    rewarm(0.3)
+    dec_cold = time_launches(lambda i: eng.decode(c_rot[i % R], o_rot[i % R], status, write_back=True, nblocks=nb))
+    assert torch.equal(o_rot[1], d_rot[1]), "standalone decode output differs"
+    del d_rot, c_rot, o_rot
     hs.close()
 
     # (3) device copy ceiling: the engine's full-grid 16-byte copy kernel over the bytes of one
@@ -449,8 +460,18 @@ def main(argv=None):
     torch.cuda.synchronize()
     copy_ms = float(np.median([hc.ms(i, i + 1) for i in range(20)]))
     copy_gbs = 2 * cp_src.numel() / (copy_ms * 1e-3) / 1e9
+    # the same copy rotating over 4 source / destination pairs (source bytes from HBM)
+    cps = [(torch.empty_like(cp_src), torch.empty_like(cp_src)) for _ in range(3)] + [(cp_src, cp_dst)]
+    for i in range(3):
+        device_copy(cps[i % 4][1], cps[i % 4][0], stream=stream)
+    hc.record(0, stream)
+    for i in range(20):
+        device_copy(cps[i % 4][1], cps[i % 4][0], stream=stream)
+        hc.record(i + 1, stream)
+    torch.cuda.synchronize()
+    copy_cold_gbs = 2 * cp_src.numel() / (float(np.median([hc.ms(i, i + 1) for i in range(20)])) * 1e-3) / 1e9
     hc.close()
-    del cp_src, cp_dst
+    del cp_src, cp_dst, cps
 
     alg_per_block = k + n  # 504 B for RS(255,249), both for encode and decode
     alg_launch = alg_per_block * nb
@@ -560,10 +581,17 @@ def main(argv=None):
                 "encode_frac": frac(float(np.median(enc_sa))),
                 "clean_decode_ms_median": round(float(np.median(dec_sa)), 5),
                 "clean_decode_frac": frac(float(np.median(dec_sa))),
+                "cold_encode_ms_median": round(float(np.median(enc_cold)), 5),
+                "cold_encode_frac": frac(float(np.median(enc_cold))),
+                "cold_clean_decode_ms_median": round(float(np.median(dec_cold)), 5),
+                "cold_clean_decode_frac": frac(float(np.median(dec_cold))),
                 "note": "back-to-back launches of one kernel, fence-free events between them, outside the "
-                        "timed region (north-star: >= 70 % on RS t=3 encode over 1 M blocks)",
+                        "timed region (north-star: >= 70 % on RS t=3 encode over 1 M blocks); hot = same "
+                        "buffers every launch (input partly Infinity-Cache resident), cold = launches rotate "
+                        f"over {R} buffer sets (input from HBM)",
             },
             "device_copy_GBps": round(copy_gbs, 1),
+            "device_copy_cold_GBps": round(copy_cold_gbs, 1),
             "device_copy_kernel": "ppfs_copy_device (full-grid 16-B copy, same bytes as one encode)",
             # payload rate beside the algorithmic one, and the dominant kernel
             # against the device-to-device copy measured above

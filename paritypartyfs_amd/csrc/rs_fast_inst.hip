@@ -47,8 +47,39 @@ static uint32_t rs_tile_grid(uint64_t nb, int wpc, int tb = 64)
 
 #if PPFS_T2 <= 8
 // segment workgroup path (2t <= 8): one 256-thread workgroup per 64-block tile, WPC resident per CU
-constexpr int ENC_NBUF = 2, ENC_WPC = (4 * wg::lds_bytes<PPFS_T2, false, 2>() <= 163840) ? 4 : 3;
-constexpr int DEC_NBUF = 2, DEC_WPC = 3;
+// PPFS_WG_FULL = N (ablation): one single-buffered workgroup per tile over a full grid, N per CU
+#ifndef PPFS_WG_FULL
+#define PPFS_WG_FULL 0
+#endif
+constexpr bool WG_FULL = PPFS_WG_FULL != 0;
+constexpr int fit_wpc(int bytes, int most) { return 163840 / bytes < most ? 163840 / bytes : most; }
+constexpr int ENC_NBUF = WG_FULL ? 0 : 2;
+constexpr int ENC_WPC = WG_FULL ? fit_wpc(wg::lds_bytes<PPFS_T2, false, 0>(), PPFS_WG_FULL) : ((4 * wg::lds_bytes<PPFS_T2, false, 2>() <= 163840) ? 4 : 3);
+// PPFS_WG_DEC_FULL = N (ablation): decode on a full grid, N workgroups per CU, one tile each.
+// Standalone from HBM ("cold") it is faster (2^20 blocks: 106-108 -> 91-99 us), but inside the
+// bench step slower (99.7 -> 103.7 us) and in the step is where the headline is measured,
+// so the persistent double-buffered grid (0) stays the default.
+#ifndef PPFS_WG_DEC_FULL
+#define PPFS_WG_DEC_FULL 0
+#endif
+constexpr bool DEC_FULL = PPFS_WG_DEC_FULL != 0;
+constexpr int DEC_NBUF = DEC_FULL ? 0 : 2, DEC_WPC = DEC_FULL ? fit_wpc(wg::lds_bytes<PPFS_T2, true, 0>(), PPFS_WG_DEC_FULL) : 3;
+// PPFS_WG_ENC_IMG = 1 (ablation): encode into a codeword image on a full grid
+// (rs_wg_encode_img_kernel).  A third fewer VALU instructions; standalone with the payload
+// cache-resident ("hot") 89-92 -> 83-85 us, but from HBM 108 -> 114 us and in the step 111 -> 114 us
+// (its DMA sources are byte-misaligned: 9 lines per 1 KiB wave read), so the default stays 0.
+#ifndef PPFS_WG_ENC_IMG
+#define PPFS_WG_ENC_IMG 0
+#endif
+#ifndef PPFS_WG_ENC_IMG_WPC
+#define PPFS_WG_ENC_IMG_WPC 6
+#endif
+#ifndef PPFS_ENC_MODE
+#define PPFS_ENC_MODE 3 // ablation builds only: rs_wg.hpp MODE bits (remainder / codeword emission)
+#endif
+#ifndef PPFS_DEC_MODE
+#define PPFS_DEC_MODE 7
+#endif
 #ifndef PPFS_ENC_NTST
 #define PPFS_ENC_NTST 1
 #endif
@@ -111,8 +142,12 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
     const uint8_t* tab, hipStream_t s)
 {
 #if PPFS_T2 <= 8
-    hipLaunchKernelGGL((wg::rs_wg_encode_kernel<PPFS_T2, ENC_NBUF, ENC_WPC, 3, PPFS_ENC_NTST>), dim3(rs_tile_grid(nb, ENC_WPC)), dim3(256),
-        0, s, d, r, nb, tab);
+    if constexpr (PPFS_WG_ENC_IMG)
+        hipLaunchKernelGGL((wg::rs_wg_encode_img_kernel<PPFS_T2, PPFS_WG_ENC_IMG_WPC, PPFS_ENC_NTST>),
+            dim3(rs_tile_grid(nb, 1 << 24)), dim3(256), 0, s, d, r, nb, tab);
+    else
+        hipLaunchKernelGGL((wg::rs_wg_encode_kernel<PPFS_T2, ENC_NBUF, ENC_WPC, PPFS_ENC_MODE, PPFS_ENC_NTST>), dim3(rs_tile_grid(nb, WG_FULL ? (1 << 24) : ENC_WPC)), dim3(256),
+            0, s, d, r, nb, tab);
 #elif PPFS_T2 > 16
     if constexpr (PAIR_IMG)
         hipLaunchKernelGGL((pair::rs_pair_encode_img_kernel<PPFS_T2, PPFS_PAIR_IMG_WPC, PPFS_PAIR_IMG_NW>),
@@ -134,7 +169,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
     const uint8_t* tab, int wb, hipStream_t s)
 {
 #if PPFS_T2 <= 8
-    hipLaunchKernelGGL((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC, 7, PPFS_DEC_NTST>), dim3(rs_tile_grid(nb, DEC_WPC)), dim3(256),
+    hipLaunchKernelGGL((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC, PPFS_DEC_MODE, PPFS_DEC_NTST>), dim3(rs_tile_grid(nb, DEC_FULL ? (1 << 24) : DEC_WPC)), dim3(256),
         0, s, r, d, st, nb, tab, wb);
 #elif PPFS_T2 > 16
     hipLaunchKernelGGL((pair::rs_pair_decode_kernel<PPFS_T2, PPFS_PAIR_DEC>),

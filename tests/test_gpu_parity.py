@@ -515,7 +515,7 @@ def test_host_decode_returns_only_changed_codewords(oracle, kind, codec):
     sets = [np.array([], np.int64), ch + rng.choice(ch, 100, replace=False), 2 * ch + np.arange(ch),
             3 * ch + rng.choice(ch, 5000, replace=False), 4 * ch + rng.choice(777, 9, replace=False)]
     hit = np.concatenate(sets)
-    if codec == "rs512":
+    if codec.startswith("rs"):
         bad[hit, rng.integers(0, n, hit.size)] ^= rng.integers(1, 256, hit.size, dtype=np.uint8)
     else:  # single bit flips (corrected, 1 byte written back); a few double flips (status 5, no write)
         pos = rng.integers(0, 8 * n, hit.size)
@@ -550,7 +550,7 @@ def test_host_decode_returns_only_changed_codewords(oracle, kind, codec):
 
 
 @pytest.mark.parametrize("devices", [(0, 0), (0, 0, 0)], ids=["g2", "g3"])
-@pytest.mark.parametrize("codec", ["rs512", "crc4096", "ham1024"])
+@pytest.mark.parametrize("codec", ["rs512", "rs4096t16", "crc4096", "ham1024"])
 def test_group_host_path_matches_single_context(oracle, devices, codec):
     """ppfs_ecc_group_* (SURVEY 8e host path): contiguous shards, one host thread per context
     (here several contexts on GPU 0).  Every shard boundary must leave results byte-identical to
@@ -559,6 +559,8 @@ def test_group_host_path_matches_single_context(oracle, devices, codec):
 
     if codec == "rs512":
         args = (ECC_REED_SOLOMON, 512, 3, 0)
+    elif codec == "rs4096t16":  # BASELINE configs[4]'s RS(255,223), sharded over the group
+        args = (ECC_REED_SOLOMON, 4096, 16, 0)
     elif codec == "crc4096":
         args = (ECC_CRC, 4096, 0, (0x9960034C << 1) + 1)
     else:
@@ -577,7 +579,7 @@ def test_group_host_path_matches_single_context(oracle, devices, codec):
     assert np.array_equal(raw_g, raw_1)
     bad = raw_g.reshape(nb, n).copy()
     hit = rng.choice(nb, nb // 3, replace=False)
-    if codec == "rs512":
+    if codec.startswith("rs"):
         bad[hit, rng.integers(0, n, hit.size)] ^= rng.integers(1, 256, hit.size, dtype=np.uint8)
     else:
         pos = rng.integers(0, 8 * n, hit.size)
@@ -592,8 +594,8 @@ def test_group_host_path_matches_single_context(oracle, devices, codec):
         outs.append((img, out, st))
     for a, b in zip(*outs):
         assert np.array_equal(a, b)
-    if codec == "rs512":
-        o_data, o_st, o_fixed, _, _ = oracle.rs_decode(512, 3, bad)
+    if codec.startswith("rs"):
+        o_data, o_st, o_fixed, _, _ = oracle.rs_decode(args[1], args[2], bad)
         assert np.array_equal(outs[0][2], o_st) and np.array_equal(outs[0][0], o_fixed)
         assert np.array_equal(outs[0][1], o_data)
     # read-modify-write of new payloads over the corrupted image
