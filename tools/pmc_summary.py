@@ -27,7 +27,7 @@ def short(name):
     # "void ppfs::rs255_encode_kernel<6, 0, 1, 1, 0>(unsigned char const*, ...)" -> rs255_encode_kernel<6, 0, 1, 1, 0>
     n = name.replace("void ", "")
     n = n.split("(")[0]
-    return n.replace("ppfs::", "").replace("wg::", "")
+    return n.replace("ppfs::", "").replace("wg::", "").replace("pair::", "").replace("bf::", "")
 
 
 def counters(path):
@@ -47,10 +47,16 @@ def main():
         blocks = int(sys.argv[sys.argv.index("--blocks") + 1])
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
-    stats = os.path.join(d, "trace", "trace_kernel_stats.csv")
+    stats = os.path.join(d, "trace_kernel_stats.csv")
+    if not os.path.exists(stats):
+        stats = os.path.join(d, "trace", "trace_kernel_stats.csv")
     shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
     rows = list(csv.DictReader(open(stats)))
     merged = defaultdict(dict)
+    red = os.path.join(d, "counters_median.json")  # tools/pmc_reduce.py, reduced on the box
+    if os.path.exists(red):
+        for k, cs in json.load(open(red)).items():
+            merged[k].update(cs)
     for sub in ("fetch", "write", "sq", "sq2"):
         for k, cs in counters(os.path.join(d, sub, f"{sub}_counter_collection.csv")).items():
             for c, v in cs.items():
@@ -62,7 +68,7 @@ def main():
     latest = {}
     for r in rows:
         k = short(r["Name"])
-        if not k.startswith(("rs255", "rs_wg", "crc", "ham", "parity", "rs_generic")):
+        if not k.startswith(("rs255", "rs_wg", "rs_pair", "rs_solo", "crc", "ham", "parity", "rs_generic")):
             continue
         c = merged.get(k, {})
         fetch = 2 * c.get("FETCH_SIZE", float("nan")) * 1024
