@@ -53,8 +53,23 @@ static uint32_t rs_tile_grid(uint64_t nb, int wpc, int tb = 64)
 #endif
 constexpr bool WG_FULL = PPFS_WG_FULL != 0;
 constexpr int fit_wpc(int bytes, int most) { return 163840 / bytes < most ? 163840 / bytes : most; }
-constexpr int ENC_NBUF = WG_FULL ? 0 : 2;
-constexpr int ENC_WPC = WG_FULL ? fit_wpc(wg::lds_bytes<PPFS_T2, false, 0>(), PPFS_WG_FULL) : ((4 * wg::lds_bytes<PPFS_T2, false, 2>() <= 163840) ? 4 : 3);
+// PPFS_WG_ENC_NBUF / PPFS_WG_DEC_NBUF = LDS tile buffers per workgroup: 2 = double buffer;
+// 3, 4 = a ring with the DMA NBUF - 1 tiles ahead and as many workgroups per CU as fit.
+// Encode ships with 3 (2 workgroups / CU, 2 tiles in flight each): in the bench step the encode
+// runs 110-112 -> 101-102 us (0.59 -> 0.65 of 8 TB/s) and from HBM 107-108 -> 102 us, while with
+// the payload cache-resident it is slower (89 -> 99 us: half the waves to hide LDS latency).
+// Decode stays at 2: its ring variants are 10 % slower in the step (profiles/r2_ablations/).
+#ifndef PPFS_WG_ENC_NBUF
+#define PPFS_WG_ENC_NBUF 3
+#endif
+#ifndef PPFS_WG_DEC_NBUF
+#define PPFS_WG_DEC_NBUF 2
+#endif
+static_assert(PPFS_WG_ENC_NBUF >= 2 && PPFS_WG_ENC_NBUF <= 4 && PPFS_WG_DEC_NBUF >= 2 && PPFS_WG_DEC_NBUF <= 4, "NBUF 2..4");
+constexpr int ENC_NBUF = WG_FULL ? 0 : PPFS_WG_ENC_NBUF;
+[[maybe_unused]] constexpr int ENC_WPC = WG_FULL ? fit_wpc(wg::lds_bytes<PPFS_T2, false, 0>(), PPFS_WG_FULL)
+    : ENC_NBUF >= 3          ? fit_wpc(wg::lds_bytes<PPFS_T2, false, ENC_NBUF>(), 4)
+                             : ((4 * wg::lds_bytes<PPFS_T2, false, 2>() <= 163840) ? 4 : 3);
 // PPFS_WG_DEC_FULL = N (ablation): decode on a full grid, N workgroups per CU, one tile each.
 // Standalone from HBM ("cold") it is faster (2^20 blocks: 106-108 -> 91-99 us), but inside the
 // bench step slower (99.7 -> 103.7 us) and in the step is where the headline is measured,
@@ -63,7 +78,10 @@ constexpr int ENC_WPC = WG_FULL ? fit_wpc(wg::lds_bytes<PPFS_T2, false, 0>(), PP
 #define PPFS_WG_DEC_FULL 0
 #endif
 constexpr bool DEC_FULL = PPFS_WG_DEC_FULL != 0;
-constexpr int DEC_NBUF = DEC_FULL ? 0 : 2, DEC_WPC = DEC_FULL ? fit_wpc(wg::lds_bytes<PPFS_T2, true, 0>(), PPFS_WG_DEC_FULL) : 3;
+constexpr int DEC_NBUF = DEC_FULL ? 0 : PPFS_WG_DEC_NBUF;
+[[maybe_unused]] constexpr int DEC_WPC = DEC_FULL ? fit_wpc(wg::lds_bytes<PPFS_T2, true, 0>(), PPFS_WG_DEC_FULL)
+    : DEC_NBUF >= 3          ? fit_wpc(wg::lds_bytes<PPFS_T2, true, DEC_NBUF>(), 3)
+                             : 3;
 // PPFS_WG_ENC_IMG = 1 (ablation): encode into a codeword image on a full grid
 // (rs_wg_encode_img_kernel).  A third fewer VALU instructions; standalone with the payload
 // cache-resident ("hot") 89-92 -> 83-85 us, but from HBM 108 -> 114 us and in the step 111 -> 114 us
@@ -73,6 +91,13 @@ constexpr int DEC_NBUF = DEC_FULL ? 0 : 2, DEC_WPC = DEC_FULL ? fit_wpc(wg::lds_
 #endif
 #ifndef PPFS_WG_ENC_IMG_WPC
 #define PPFS_WG_ENC_IMG_WPC 6
+#endif
+// PPFS_WG_RP = N: register-prefetch kernels (rs_wg_*_rp_kernel), N workgroups per CU; 0 = off
+#ifndef PPFS_WG_RP
+#define PPFS_WG_RP 0
+#endif
+#if PPFS_WG_RP
+#include "rs_wg_rp.hpp"
 #endif
 #ifndef PPFS_ENC_MODE
 #define PPFS_ENC_MODE 3 // ablation builds only: rs_wg.hpp MODE bits (remainder / codeword emission)
@@ -142,12 +167,17 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
     const uint8_t* tab, hipStream_t s)
 {
 #if PPFS_T2 <= 8
+#if PPFS_WG_RP
+    hipLaunchKernelGGL((wg::rs_wg_encode_rp_kernel<PPFS_T2, PPFS_WG_RP, PPFS_ENC_NTST>),
+        dim3(rs_tile_grid(nb, PPFS_WG_RP)), dim3(256), 0, s, d, r, nb, tab);
+#else
     if constexpr (PPFS_WG_ENC_IMG)
         hipLaunchKernelGGL((wg::rs_wg_encode_img_kernel<PPFS_T2, PPFS_WG_ENC_IMG_WPC, PPFS_ENC_NTST>),
             dim3(rs_tile_grid(nb, 1 << 24)), dim3(256), 0, s, d, r, nb, tab);
     else
         hipLaunchKernelGGL((wg::rs_wg_encode_kernel<PPFS_T2, ENC_NBUF, ENC_WPC, PPFS_ENC_MODE, PPFS_ENC_NTST>), dim3(rs_tile_grid(nb, WG_FULL ? (1 << 24) : ENC_WPC)), dim3(256),
             0, s, d, r, nb, tab);
+#endif
 #elif PPFS_T2 > 16
     if constexpr (PAIR_IMG)
         hipLaunchKernelGGL((pair::rs_pair_encode_img_kernel<PPFS_T2, PPFS_PAIR_IMG_WPC, PPFS_PAIR_IMG_NW>),
@@ -169,8 +199,17 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
     const uint8_t* tab, int wb, hipStream_t s)
 {
 #if PPFS_T2 <= 8
+#if PPFS_WG_RP
+    if (d)
+        hipLaunchKernelGGL((wg::rs_wg_decode_rp_kernel<PPFS_T2, PPFS_WG_RP, PPFS_DEC_NTST, true>),
+            dim3(rs_tile_grid(nb, PPFS_WG_RP)), dim3(256), 0, s, r, d, st, nb, tab, wb);
+    else
+        hipLaunchKernelGGL((wg::rs_wg_decode_rp_kernel<PPFS_T2, PPFS_WG_RP, PPFS_DEC_NTST, false>),
+            dim3(rs_tile_grid(nb, PPFS_WG_RP)), dim3(256), 0, s, r, d, st, nb, tab, wb);
+#else
     hipLaunchKernelGGL((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC, PPFS_DEC_MODE, PPFS_DEC_NTST>), dim3(rs_tile_grid(nb, DEC_FULL ? (1 << 24) : DEC_WPC)), dim3(256),
         0, s, r, d, st, nb, tab, wb);
+#endif
 #elif PPFS_T2 > 16
     hipLaunchKernelGGL((pair::rs_pair_decode_kernel<PPFS_T2, PPFS_PAIR_DEC>),
         dim3(rs_tile_grid(nb, PPFS_PAIR_DEC_FULL ? (1 << 24) : PAIR_DEC_WPC)),

@@ -434,12 +434,38 @@ __device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, ui
 // ------------------------------------------------------------------------------------
 // Kernels: persistent workgroups walk 64-block tiles t = blockIdx.x, += gridDim.x.
 // NBUF = LDS tile buffers: 2 = the next tile's DMA is issued at the top of an iteration (a whole
-// tile of compute ahead); 1 = it is issued after this tile's emission reads (cross-workgroup
+// tile of compute ahead); 3, 4 = a ring, the DMA NBUF - 1 tiles ahead (fewer workgroups per CU fit); 1 = it is issued after this tile's emission reads (cross-workgroup
 // overlap hides it); 0 = full grid: one tile per workgroup (the grid covers the batch, workgroups
 // dispatched in address order), emission pieces computed and stored one at a time (few live
 // registers, so WPC workgroups fit a CU without spills).  WPC = resident workgroups per CU (the
 // launch bound; persistent grids are WPC x CUs).
 // ------------------------------------------------------------------------------------
+// Ring of NBUF >= 3 tile buffers: the DMA of tile t + (NBUF-1) G is issued at the top of the
+// iteration of tile t.  Counted waits: the DMA and store instructions are 4 per wave per tile, and
+// a wave's vector-memory operations complete in issue order, so "tile t + G has landed" is
+// vmcnt(#operations issued after its DMA).  `hist` holds one bit per DMA slot (1 = issued; bit 0
+// the latest); a skipped DMA (past the last tile) means fewer newer operations and a lower count.
+__device__ __forceinline__ uint32_t ring_add(uint32_t c, uint32_t d, uint32_t n) { return c + d >= n ? c + d - n : c + d; }
+
+// s_waitcnt vmcnt(m) for the largest m in {0, 4, ..., 24} with m <= n (n wave-uniform)
+__device__ __forceinline__ void vm_wait_newer(uint32_t n)
+{
+    if (n >= 24)
+        asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if (n >= 20)
+        asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    else if (n >= 16)
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (n >= 12)
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (n >= 8)
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n >= 4)
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <int T2, bool DEC, int NBUF> struct Lds {
     using L = RsWgLayout<T2>;
     static constexpr int TBL = DEC ? L::TABLE_BYTES : L::OFF_SYN; // encode needs SL + MAP only
@@ -485,13 +511,32 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_kernel(const uint8_t* _
     uint32_t cur = 0, pc = 0; // tile buffer, parity-slot set
     if (t < nfull)
         dma_tile<IN_PIECES>(lds + D::OFF_BUF + PAD, data + t * (TB * K), tid);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t hist = 0, iter = 0;
+    if constexpr (NBUF >= 3) {
+#pragma unroll
+        for (int j = 1; j <= NBUF - 2; ++j) {
+            const bool go = t + j * gridDim.x < nfull;
+            if (go)
+                dma_tile<IN_PIECES>(lds + D::OFF_BUF + j * BUF + PAD, data + (t + j * gridDim.x) * (TB * K), tid);
+            hist = (hist << 1) | (go ? 1u : 0u);
+        }
+        vm_wait_newer(4u * __builtin_popcount(hist)); // tile t landed, the later ones may fly
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     for (; t < nfull; t += gridDim.x) {
         barrier_lds(); // A: tile t in LDS (every wave's pieces), last tile's emission reads done
         const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + pc * 512u;
         const uint64_t nx = t + gridDim.x;
         if (NBUF == 2 && nx < nfull)
             dma_tile<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, data + nx * (TB * K), tid);
+        if constexpr (NBUF >= 3) { // NBUF - 1 tiles ahead, into the buffer tile t - G used
+            const uint64_t ahead = t + (uint64_t)(NBUF - 1) * gridDim.x;
+            const bool go = ahead < nfull;
+            if (go)
+                dma_tile<IN_PIECES>(lds + D::OFF_BUF + ring_add(cur, NBUF - 1, NBUF) * BUF + PAD, data + ahead * (TB * K), tid);
+            hist = (hist << 1) | (go ? 1u : 0u);
+        }
         if (wave == 0)
             *(uint64_t*)(lds + D::OFF_PAR + (pc ^ 1u) * 512u + 8u * lane) = 0;
         if constexpr (MODE & 1)
@@ -524,8 +569,17 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_kernel(const uint8_t* _
                     st_nt<NTST>(dst + 16u * p, o[k]);
             }
         }
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); // next tile's DMA landed; stores may fly
-        cur ^= (NBUF == 2) ? 1u : 0u;
+        // next tile's DMA landed; this tile's stores (NBUF >= 3: and every store and DMA issued
+        // after that DMA) may fly
+        if constexpr (NBUF >= 3) {
+            ++iter;
+            const uint32_t st = 4u * (iter < (uint32_t)(NBUF - 1) ? iter : (uint32_t)(NBUF - 1));
+            vm_wait_newer(st + 4u * __builtin_popcount(hist & ((1u << (NBUF - 2)) - 1u)));
+            cur = ring_add(cur, 1, NBUF);
+        } else {
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            cur ^= (NBUF == 2) ? 1u : 0u;
+        }
         pc ^= 1u;
     }
     if (t == nfull && nfull < ntiles) {
@@ -711,13 +765,32 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_kernel(uint8_t* __restr
     uint32_t cur = 0, pc = 0;
     if (t < nfull)
         dma_tile<IN_PIECES>(lds + D::OFF_BUF + PAD, raw + t * (TB * 255), tid);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t hist = 0, iter = 0;
+    if constexpr (NBUF >= 3) {
+#pragma unroll
+        for (int j = 1; j <= NBUF - 2; ++j) {
+            const bool go = t + j * gridDim.x < nfull;
+            if (go)
+                dma_tile<IN_PIECES>(lds + D::OFF_BUF + j * BUF + PAD, raw + (t + j * gridDim.x) * (TB * 255), tid);
+            hist = (hist << 1) | (go ? 1u : 0u);
+        }
+        vm_wait_newer(4u * __builtin_popcount(hist));
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     for (; t < nfull; t += gridDim.x) {
         barrier_lds(); // A
         const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + pc * 512u;
         const uint64_t nx = t + gridDim.x;
         if (NBUF == 2 && nx < nfull)
             dma_tile<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, raw + nx * (TB * 255), tid);
+        if constexpr (NBUF >= 3) {
+            const uint64_t ahead = t + (uint64_t)(NBUF - 1) * gridDim.x;
+            const bool go = ahead < nfull;
+            if (go)
+                dma_tile<IN_PIECES>(lds + D::OFF_BUF + ring_add(cur, NBUF - 1, NBUF) * BUF + PAD, raw + ahead * (TB * 255), tid);
+            hist = (hist << 1) | (go ? 1u : 0u);
+        }
         if (wave == 0)
             *(uint64_t*)(lds + D::OFF_PAR + (pc ^ 1u) * 512u + 8u * lane) = 0;
         if constexpr (MODE & 1)
@@ -760,11 +833,20 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_kernel(uint8_t* __restr
                 }
             }
         }
-        if (want)
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        cur ^= (NBUF == 2) ? 1u : 0u;
+        // as in encode (no output stores without `data`); the wave-0 status / write-back stores
+        // only add newer operations, which keeps the count a lower bound
+        if constexpr (NBUF >= 3) {
+            ++iter;
+            const uint32_t st = want ? 4u * (iter < (uint32_t)(NBUF - 1) ? iter : (uint32_t)(NBUF - 1)) : 0u;
+            vm_wait_newer(st + 4u * __builtin_popcount(hist & ((1u << (NBUF - 2)) - 1u)));
+            cur = ring_add(cur, 1, NBUF);
+        } else {
+            if (want)
+                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            cur ^= (NBUF == 2) ? 1u : 0u;
+        }
         pc ^= 1u;
     }
     if (t == nfull && nfull < ntiles) {
