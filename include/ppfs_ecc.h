@@ -202,6 +202,14 @@ int ppfs_ecc_group_write_host(ppfs_ecc_group* group, const uint8_t* data, uint8_
 /* Last HIP error string recorded by this thread (diagnostics). */
 const char* ppfs_ecc_last_error(void);
 
+/* Diagnostics of PPFS_ECC_DEBUG builds (csrc/dbg.hpp): the number of out-of-bounds global
+ * accesses the kernels detected (and skipped) so far; -1 in normal builds.  Engine extension,
+ * no reference counterpart. */
+long long ppfs_ecc_debug_faults(void);
+/* PPFS_ECC_DEBUG builds: launches one deliberately out-of-range row gather and returns how many
+ * accesses the kernel reported (and skipped), >= 1 when the checks work; -1 in normal builds. */
+long long ppfs_ecc_debug_selftest(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_int, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
+from ctypes import POINTER, c_char_p, c_int, c_longlong, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # PPFS_ECC_LIB: an alternative build of the same library (ablation runs, tools/)
@@ -47,6 +47,8 @@ EXPORTED_SYMBOLS = (
     "ppfs_ecc_group_decode_host",
     "ppfs_ecc_group_write_host",
     "ppfs_ecc_last_error",
+    "ppfs_ecc_debug_faults",
+    "ppfs_ecc_debug_selftest",
 )
 
 
@@ -86,6 +88,10 @@ def lib() -> ctypes.CDLL:
         pass
     L = ctypes.CDLL(LIB_PATH)
     u8p = POINTER(c_uint8)
+    L.ppfs_ecc_debug_faults.restype = c_longlong
+    L.ppfs_ecc_debug_faults.argtypes = []
+    L.ppfs_ecc_debug_selftest.restype = c_longlong
+    L.ppfs_ecc_debug_selftest.argtypes = []
     L.ppfs_ecc_crc_implicit_to_explicit.restype = c_uint64
     L.ppfs_ecc_crc_implicit_to_explicit.argtypes = [c_uint64]
     L.ppfs_ecc_create.restype = c_int
@@ -155,3 +161,16 @@ class EccError(RuntimeError):
 def check(rc: int) -> None:
     if rc != 0:
         raise EccError(rc, lib().ppfs_ecc_last_error().decode(errors="replace"))
+
+
+def debug_faults() -> int | None:
+    """Out-of-bounds global accesses detected so far by a PPFS_ECC_DEBUG build of the library
+    (csrc/dbg.hpp); None when the loaded library is a normal build or is not loaded yet."""
+    if _lib is None:
+        return None
+    v = int(_lib.ppfs_ecc_debug_faults())
+    if v == -1:
+        return None
+    if v < 0:
+        raise RuntimeError(f"ppfs_ecc_debug_faults failed ({v})")
+    return v

@@ -50,7 +50,7 @@ hipError_t ppfs_ham_decode(uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, int
 hipError_t ppfs_parity_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs,
     hipStream_t s);
 hipError_t ppfs_parity_check(const uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, uint32_t bs, hipStream_t s);
-hipError_t ppfs_gather_rows_launch(const uint8_t* src, uint8_t* dst, const uint32_t* idx, uint32_t nrows,
+hipError_t ppfs_gather_rows_launch(const uint8_t* src, uint64_t src_rows, uint8_t* dst, const uint32_t* idx, uint32_t nrows,
     uint32_t row_bytes, hipStream_t s);
 hipError_t ppfs_vote3_launch(const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* out, uint64_t rec_bytes,
     uint64_t nrec, uint32_t* damaged, hipStream_t s);
@@ -598,6 +598,31 @@ extern "C" size_t ppfs_ecc_raw_block_size(const ppfs_ecc_ctx* c) { return c ? c-
 extern "C" size_t ppfs_ecc_data_size(const ppfs_ecc_ctx* c) { return c ? c->data : 0; }
 extern "C" const char* ppfs_ecc_kernel_name(const ppfs_ecc_ctx* c) { return c ? c->kname : ""; }
 
+// PPFS_ECC_DEBUG builds: out-of-bounds global accesses the kernels detected and skipped (dbg.hpp),
+// summed over the kernel translation units; -1 in normal builds
+#ifdef PPFS_ECC_DEBUG
+#define PPFS_DBG_UNITS(X) X(ppfs_dbg_faults_rs_t2) X(ppfs_dbg_faults_rs_t4) X(ppfs_dbg_faults_rs_t6) \
+    X(ppfs_dbg_faults_rs_t8) X(ppfs_dbg_faults_rs_t10) X(ppfs_dbg_faults_rs_t16) X(ppfs_dbg_faults_rs_t32)   \
+    X(ppfs_dbg_faults_rs_generic) X(ppfs_dbg_faults_bit) X(ppfs_dbg_faults_bitfast) X(ppfs_dbg_faults_vote)
+#define PPFS_DBG_DECL(f) extern "C" long long f(void);
+PPFS_DBG_UNITS(PPFS_DBG_DECL)
+extern "C" long long ppfs_ecc_debug_faults(void)
+{
+    long long sum = 0;
+#define PPFS_DBG_ADD(f)                                                                                                \
+    {                                                                                                                  \
+        const long long v = f();                                                                                       \
+        if (v < 0)                                                                                                     \
+            return v;                                                                                                  \
+        sum += v;                                                                                                      \
+    }
+    PPFS_DBG_UNITS(PPFS_DBG_ADD)
+    return sum;
+}
+#else
+extern "C" long long ppfs_ecc_debug_faults(void) { return -1; }
+#endif
+
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 static int check_hip(hipError_t e, const char* what)
@@ -1046,7 +1071,7 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
             return 0;
         }
         HIP_TRY(hipMemcpyAsync(d + L.idx, ix, nchg * sizeof(uint32_t), hipMemcpyHostToDevice, s), "H2D idx");
-        HIP_TRY(ppfs_gather_rows_launch(d + L.raw, d + L.gat, (const uint32_t*)(d + L.idx), (uint32_t)nchg,
+        HIP_TRY(ppfs_gather_rows_launch(d + L.raw, nb, d + L.gat, (const uint32_t*)(d + L.idx), (uint32_t)nchg,
                     (uint32_t)c->raw, s), "gather");
         HIP_TRY(hipMemcpyAsync(h + L.gat, d + L.gat, nchg * c->raw, hipMemcpyDeviceToHost, s), "D2H gather");
         HIP_TRY(hipStreamSynchronize(s), "sync");

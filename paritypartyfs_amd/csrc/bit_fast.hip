@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "dbg.hpp"
 #include "gf_common.hpp"
 
 namespace ppfs {
@@ -72,6 +73,13 @@ __device__ __forceinline__ void gst16_raw(uint8_t* p, uint4 v)
     } else {
         gst16(p, v);
     }
+}
+
+// PPFS_ECC_DEBUG (dbg.hpp): a load outside its buffer reads zeros (and is reported); normal
+// builds compile this to gld16
+__device__ __forceinline__ uint4 gld16c(const uint8_t* p, const uint8_t* base, uint64_t extent)
+{
+    return PPFS_DBG_OK(p, 16, base, extent) ? gld16(p) : make_uint4(0, 0, 0, 0);
 }
 
 constexpr int WAVES = 4;
@@ -156,7 +164,7 @@ __device__ __forceinline__ void ham_stage_load(HamEncStage<NP>& s, const uint8_t
         uint4 v = make_uint4(0, 0, 0, 0);
         if (p < npc) {
             if (g + 16 <= a.data_bytes) {
-                v = gld16(data + g);
+                v = gld16c(data + g, data, a.data_bytes);
             } else {
                 uint32_t w[4] = { 0, 0, 0, 0 };
                 for (uint32_t b = 0; b < 16 && g + b < a.data_bytes; ++b)
@@ -201,10 +209,10 @@ __global__ __launch_bounds__(256) void ham_fast_encode_kernel(const uint8_t* __r
             ham_stage_load<NP>(st, data, nx, a, lane); // lands while this block is computed
         const uint32_t m = (uint32_t)((blk * a.ds) & 15u); // payload byte 0 sits at LDS byte m
         uint8_t* rb = raw + blk * a.bs;
-        const bool skipped = skip && skip[blk] == 5;
+        const bool skipped = skip && PPFS_DBG_OK(skip + blk, 1, skip, nblocks_all) && skip[blk] == 5;
         // old raw tail word (bits past L keep their contents): the last word of the block
         uint32_t old_tail = 0;
-        if (lane == 63)
+        if (lane == 63 && PPFS_DBG_OK(rb + 4 * lastw, 4, raw, nblocks_all * a.bs))
             old_tail = bswap(*(const uint32_t*)(rb + 4 * lastw));
         uint32_t X[NP][4];
         uint32_t ax = 0, aw = 0;
@@ -264,8 +272,9 @@ __global__ __launch_bounds__(256) void ham_fast_encode_kernel(const uint8_t* __r
                     const uint32_t keep = ~top_bits(a.L - 32 * lastw + 1);
                     X[k][3] = (X[k][3] & ~keep) | (old_tail & keep);
                 }
-                gst16_raw(rb + 16u * (64u * k + lane),
-                    make_uint4(bswap(X[k][0]), bswap(X[k][1]), bswap(X[k][2]), bswap(X[k][3])));
+                if (PPFS_DBG_OK(rb + 16u * (64u * k + lane), 16, raw, nblocks_all * a.bs))
+                    gst16_raw(rb + 16u * (64u * k + lane),
+                        make_uint4(bswap(X[k][0]), bswap(X[k][1]), bswap(X[k][2]), bswap(X[k][3])));
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); // LDS reads done before the rewrite
@@ -380,7 +389,7 @@ __global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restric
     if (blk < nblocks) {
 #pragma unroll
         for (int k = 0; k < NP; ++k)
-            R[k] = gld16(raw + blk * a.bs + 16u * (64u * k + lane));
+            R[k] = gld16c(raw + blk * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
     }
     for (; blk < nblocks; blk += stride) {
         uint32_t X[NP][4];
@@ -395,7 +404,7 @@ __global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restric
         if (BF_PREFETCH && nx < nblocks) {
 #pragma unroll
             for (int k = 0; k < NP; ++k)
-                R[k] = gld16(raw + nx * a.bs + 16u * (64u * k + lane));
+                R[k] = gld16c(raw + nx * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
         }
         uint32_t ax = 0, aw = 0;
 #pragma unroll
@@ -425,11 +434,11 @@ __global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restric
                     for (int u = 0; u < 4; ++u)
                         if (256u * k + 4u * lane + u == ws)
                             X[k][u] ^= flip;
-                if (write_back)
+                if (write_back && PPFS_DBG_OK(rb + (S >> 3), 1, raw, nblocks_all * a.bs))
                     rb[S >> 3] = (uint8_t)(rb[S >> 3] ^ (0x80u >> (S & 7u)));
             }
         }
-        if (status && lane == 0)
+        if (status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
             status[blk] = (uint8_t)st;
         if (data && st != 5) {
 #pragma unroll
@@ -445,6 +454,9 @@ __global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restric
             const uint32_t npc = (m + a.ds + 15) >> 4;
             auto store = [&](uint32_t p, int32_t b0, const uint32_t (&o)[4]) {
                 uint8_t* dst = data + a0 + 16ull * p;
+                [[maybe_unused]] const int32_t lo = b0 < 0 ? -b0 : 0, hi = b0 + 16 > (int32_t)a.ds ? (int32_t)a.ds - b0 : 16;
+                if (!PPFS_DBG_OK(dst + lo, hi - lo, data, a.data_bytes))
+                    return;
                 if (b0 >= 0 && b0 + 16 <= (int32_t)a.ds)
                     gst16(dst, make_uint4(o[0], o[1], o[2], o[3]));
                 else
@@ -492,7 +504,7 @@ __global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restric
         if (!BF_PREFETCH && nx < nblocks) {
 #pragma unroll
             for (int k = 0; k < NP; ++k)
-                R[k] = gld16(raw + nx * a.bs + 16u * (64u * k + lane));
+                R[k] = gld16c(raw + nx * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
         }
     }
 }
@@ -559,7 +571,7 @@ __global__ __launch_bounds__(256) void parity_fast_encode_kernel(const uint8_t* 
             ham_stage_load<NP>(nxt, data, nx, ha, lane);
         const uint32_t m = (uint32_t)((blk * ds) & 15u);
         uint8_t* rb = raw + blk * a.bs;
-        const uint32_t old_last = (lane == 63) ? rb[a.bs - 1] : 0u;
+        const uint32_t old_last = (lane == 63 && PPFS_DBG_OK(rb + a.bs - 1, 1, raw, nblocks_all * a.bs)) ? rb[a.bs - 1] : 0u;
         uint4 O[NP];
         uint32_t ones = 0;
 #pragma unroll
@@ -576,13 +588,14 @@ __global__ __launch_bounds__(256) void parity_fast_encode_kernel(const uint8_t* 
             O[k] = o;
         }
         const uint32_t odd = wave_xor(ones & 1u);
-        if (!(skip && skip[blk] == 5)) {
+        if (!(skip && PPFS_DBG_OK(skip + blk, 1, skip, nblocks_all) && skip[blk] == 5)) {
 #pragma unroll
             for (int k = 0; k < NP; ++k) {
                 uint4 o = O[k];
                 if (k == NP - 1 && lane == 63)
                     o.w ^= odd << 24; // LSB of the last byte fixes the parity
-                gst16_raw(rb + 16u * (64u * k + lane), o);
+                if (PPFS_DBG_OK(rb + 16u * (64u * k + lane), 16, raw, nblocks_all * a.bs))
+                    gst16_raw(rb + 16u * (64u * k + lane), o);
             }
         }
         if (BF_PREFETCH)
@@ -606,20 +619,20 @@ __global__ __launch_bounds__(256) void parity_fast_check_kernel(const uint8_t* _
     if (blk < nblocks)
 #pragma unroll
         for (int k = 0; k < NP; ++k)
-            R[k] = gld16(raw + blk * a.bs + 16u * (64u * k + lane));
+            R[k] = gld16c(raw + blk * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
     for (; blk < nblocks; blk += stride) {
         const uint64_t nx = blk + stride;
         if (BF_PREFETCH && nx < nblocks)
 #pragma unroll
             for (int k = 0; k < NP; ++k)
-                N[k] = gld16(raw + nx * a.bs + 16u * (64u * k + lane));
+                N[k] = gld16c(raw + nx * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
         uint32_t ones = 0;
 #pragma unroll
         for (int k = 0; k < NP; ++k)
             ones += __builtin_popcount(R[k].x) + __builtin_popcount(R[k].y) + __builtin_popcount(R[k].z)
                 + __builtin_popcount(R[k].w);
         const uint32_t odd = wave_xor(ones & 1u);
-        if (status && lane == 0)
+        if (status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
             status[blk] = odd ? 5 : 0;
         if (data) {
             // payload byte x = raw byte x; output pieces on the payload's global 16-byte grid:
@@ -646,8 +659,11 @@ __global__ __launch_bounds__(256) void parity_fast_check_kernel(const uint8_t* _
                 const int32_t b0 = (int32_t)(16 * p) - (int32_t)m;
                 uint8_t* dst = data + a0 + 16ull * p;
                 if (b0 >= 0 && b0 + 16 <= (int32_t)ds) {
-                    gst16(dst, oo);
-                } else if (b0 < (int32_t)ds && b0 + 16 > 0) {
+                    if (PPFS_DBG_OK(dst, 16, data, nblocks_all * ds))
+                        gst16(dst, oo);
+                } else if (b0 < (int32_t)ds && b0 + 16 > 0
+                    && PPFS_DBG_OK(dst + (b0 < 0 ? -b0 : 0), (b0 + 16 > (int32_t)ds ? (int32_t)ds - b0 : 16) - (b0 < 0 ? -b0 : 0),
+                        data, nblocks_all * ds)) {
                     const uint32_t w[4] = { oo.x, oo.y, oo.z, oo.w };
                     store_piece_part(dst, w, b0 < 0 ? (uint32_t)(-b0) : 0u,
                         b0 + 16 > (int32_t)ds ? (uint32_t)((int32_t)ds - b0) : 16u);
@@ -661,7 +677,7 @@ __global__ __launch_bounds__(256) void parity_fast_check_kernel(const uint8_t* _
         } else if (nx < nblocks) {
 #pragma unroll
             for (int k = 0; k < NP; ++k)
-                R[k] = gld16(raw + nx * a.bs + 16u * (64u * k + lane));
+                R[k] = gld16c(raw + nx * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
         }
     }
 }
@@ -799,11 +815,11 @@ __global__ __launch_bounds__(256) void crc_fast_encode_kernel(const uint8_t* __r
         const uint32_t Vs = crc_lane_tree(tbl, acc);
         const uint32_t V = cmap(tbl + (CF_FENC + m) * CF_MAP, Vs);
         const uint32_t st = (V << 1) & a.mask;
-        if (!(skip && skip[blk] == 5)) {
+        if (!(skip && PPFS_DBG_OK(skip + blk, 1, skip, nblocks_all) && skip[blk] == 5)) {
             // raw bytes [ds, ds + nbc): the n CRC bits MSB first (a partial last byte keeps its old
             // low bits); all in the row's last raw piece (lane 63, k = NP - 1)
             uint32_t old_last = 0;
-            if (lane == 63 && (a.n & 7u))
+            if (lane == 63 && (a.n & 7u) && PPFS_DBG_OK(rb + a.ds + a.nbc - 1, 1, raw, nblocks_all * a.bs))
                 old_last = rb[a.ds + a.nbc - 1];
 #pragma unroll
             for (int k = 0; k < NP; ++k) {
@@ -831,7 +847,8 @@ __global__ __launch_bounds__(256) void crc_fast_encode_kernel(const uint8_t* __r
                     }
                     o = make_uint4(w[0], w[1], w[2], w[3]);
                 }
-                gst16_raw(rb + 16u * (64u * k + lane), o);
+                if (PPFS_DBG_OK(rb + 16u * (64u * k + lane), 16, raw, nblocks_all * a.bs))
+                    gst16_raw(rb + 16u * (64u * k + lane), o);
             }
         }
         if (BF_PREFETCH)
@@ -861,13 +878,13 @@ __global__ __launch_bounds__(256) void crc_fast_check_kernel(const uint8_t* __re
     if (blk < nblocks)
 #pragma unroll
         for (int k = 0; k < NP; ++k)
-            R[k] = gld16(raw + blk * a.bs + 16u * (64u * k + lane));
+            R[k] = gld16c(raw + blk * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
     for (; blk < nblocks; blk += stride) {
         const uint64_t nx = blk + stride;
         if (BF_PREFETCH && nx < nblocks)
 #pragma unroll
             for (int k = 0; k < NP; ++k)
-                N[k] = gld16(raw + nx * a.bs + 16u * (64u * k + lane));
+                N[k] = gld16c(raw + nx * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
         uint32_t acc = 0;
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
@@ -891,7 +908,7 @@ __global__ __launch_bounds__(256) void crc_fast_check_kernel(const uint8_t* __re
             f = (f << 8) | ((lw[b >> 2] >> (8 * (b & 3))) & 0xFFu);
         }
         const uint32_t field = (uint32_t)(f >> (8 * a.nbc - a.n));
-        if (status && lane == 0)
+        if (status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
             status[blk] = (st == field) ? 0 : 5;
         if (data) {
             const uint64_t start = blk * ds, a0 = start & ~15ull;
@@ -912,8 +929,11 @@ __global__ __launch_bounds__(256) void crc_fast_check_kernel(const uint8_t* __re
                 const int32_t b0 = (int32_t)(16 * p) - (int32_t)m;
                 uint8_t* dst = data + a0 + 16ull * p;
                 if (b0 >= 0 && b0 + 16 <= (int32_t)ds) {
-                    gst16(dst, oo);
-                } else if (b0 < (int32_t)ds && b0 + 16 > 0) {
+                    if (PPFS_DBG_OK(dst, 16, data, nblocks_all * ds))
+                        gst16(dst, oo);
+                } else if (b0 < (int32_t)ds && b0 + 16 > 0
+                    && PPFS_DBG_OK(dst + (b0 < 0 ? -b0 : 0), (b0 + 16 > (int32_t)ds ? (int32_t)ds - b0 : 16) - (b0 < 0 ? -b0 : 0),
+                        data, nblocks_all * ds)) {
                     const uint32_t w[4] = { oo.x, oo.y, oo.z, oo.w };
                     store_piece_part(dst, w, b0 < 0 ? (uint32_t)(-b0) : 0u,
                         b0 + 16 > (int32_t)ds ? (uint32_t)((int32_t)ds - b0) : 16u);
@@ -927,7 +947,7 @@ __global__ __launch_bounds__(256) void crc_fast_check_kernel(const uint8_t* __re
         } else if (nx < nblocks) {
 #pragma unroll
             for (int k = 0; k < NP; ++k)
-                R[k] = gld16(raw + nx * a.bs + 16u * (64u * k + lane));
+                R[k] = gld16c(raw + nx * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
         }
     }
 }
@@ -1022,3 +1042,5 @@ extern "C" hipError_t ppfs_parity_fast_check(const uint8_t* r, uint8_t* d, uint8
     PPFS_NP_DISPATCH(bs, bf::parity_fast_check_kernel, (nb + bf::BF_BPW - 1) / bf::BF_BPW, s, r, d, st, nb, a)
     return hipGetLastError();
 }
+
+PPFS_DBG_ACCESSOR(ppfs_dbg_faults_bitfast)

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "dbg.hpp"
 #include "gf_common.hpp"
 
 namespace ppfs {
@@ -206,6 +207,9 @@ __global__ __launch_bounds__(256) void crc_encode_kernel(const uint8_t* __restri
     const uint32_t lane = lane_id(), wave = wave_id();
     uint8_t* buf = lds + CRC_TBL_BYTES + wave * BK_BUF;
     for (uint64_t blk = (uint64_t)blockIdx.x * BK_WAVES + wave; blk < nblocks; blk += (uint64_t)gridDim.x * BK_WAVES) {
+        if (!PPFS_DBG_OK(data + blk * a.ds, a.ds, data, nblocks * a.ds) || !PPFS_DBG_OK(raw + blk * a.bs, a.bs, raw, nblocks * a.bs)
+            || (skip && !PPFS_DBG_OK(skip + blk, 1, skip, nblocks)))
+            continue; // PPFS_ECC_DEBUG: the block's rows (wave_g2l may also read the aligned dword holding a row's first byte)
         if (skip && skip[blk] == 5)
             continue;
         wave_g2l(buf, data + blk * a.ds, a.ds, lane);
@@ -245,6 +249,9 @@ __global__ __launch_bounds__(256) void crc_check_kernel(const uint8_t* __restric
     uint8_t* buf = lds + CRC_TBL_BYTES + wave * BK_BUF;
     for (uint64_t blk = (uint64_t)blockIdx.x * BK_WAVES + wave; blk < nblocks; blk += (uint64_t)gridDim.x * BK_WAVES) {
         const uint8_t* rb = raw + blk * a.bs;
+        if (!PPFS_DBG_OK(rb, a.bs, raw, nblocks * a.bs) || (data && !PPFS_DBG_OK(data + blk * a.ds, a.ds, data, nblocks * a.ds))
+            || (status && !PPFS_DBG_OK(status + blk, 1, status, nblocks)))
+            continue;
         wave_g2l(buf, rb, a.bs, lane);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         const uint64_t field = crc_read_field(buf, a);
@@ -359,6 +366,9 @@ __global__ __launch_bounds__(256) void ham_encode_kernel(const uint8_t* __restri
     uint8_t* buf = lds + wave * BK_BUF;
     const uint32_t nwords = a.bits / 32;
     for (uint64_t blk = (uint64_t)blockIdx.x * BK_WAVES + wave; blk < nblocks; blk += (uint64_t)gridDim.x * BK_WAVES) {
+        if (!PPFS_DBG_OK(data + blk * a.ds, a.ds, data, nblocks * a.ds) || !PPFS_DBG_OK(raw + blk * a.bs, a.bs, raw, nblocks * a.bs)
+            || (skip && !PPFS_DBG_OK(skip + blk, 1, skip, nblocks)))
+            continue;
         if (skip && skip[blk] == 5)
             continue;
         wave_g2l(buf, data + blk * a.ds, a.ds, lane);
@@ -433,6 +443,9 @@ __global__ __launch_bounds__(256) void ham_decode_kernel(uint8_t* __restrict__ r
     const uint32_t nwords = a.bits / 32;
     for (uint64_t blk = (uint64_t)blockIdx.x * BK_WAVES + wave; blk < nblocks; blk += (uint64_t)gridDim.x * BK_WAVES) {
         uint8_t* rb = raw + blk * a.bs;
+        if (!PPFS_DBG_OK(rb, a.bs, raw, nblocks * a.bs) || (data && !PPFS_DBG_OK(data + blk * a.ds, a.ds, data, nblocks * a.ds))
+            || (status && !PPFS_DBG_OK(status + blk, 1, status, nblocks)))
+            continue;
         uint32_t X[16];
         uint32_t syn = 0, par = 0;
 #pragma unroll
@@ -546,6 +559,9 @@ __global__ __launch_bounds__(256) void parity_encode_kernel(const uint8_t* __res
     uint8_t* buf = lds + wave * BK_BUF;
     const uint32_t ds = bs - 1;
     for (uint64_t blk = (uint64_t)blockIdx.x * BK_WAVES + wave; blk < nblocks; blk += (uint64_t)gridDim.x * BK_WAVES) {
+        if (!PPFS_DBG_OK(data + blk * ds, ds, data, nblocks * ds) || !PPFS_DBG_OK(raw + blk * bs, bs, raw, nblocks * bs)
+            || (skip && !PPFS_DBG_OK(skip + blk, 1, skip, nblocks)))
+            continue;
         if (skip && skip[blk] == 5)
             continue;
         uint8_t* rb = raw + blk * bs;
@@ -572,6 +588,9 @@ __global__ __launch_bounds__(256) void parity_check_kernel(const uint8_t* __rest
     uint8_t* buf = lds + wave * BK_BUF;
     for (uint64_t blk = (uint64_t)blockIdx.x * BK_WAVES + wave; blk < nblocks; blk += (uint64_t)gridDim.x * BK_WAVES) {
         const uint8_t* rb = raw + blk * bs;
+        if (!PPFS_DBG_OK(rb, bs, raw, nblocks * bs) || (data && !PPFS_DBG_OK(data + blk * (bs - 1), bs - 1, data, nblocks * (bs - 1)))
+            || (status && !PPFS_DBG_OK(status + blk, 1, status, nblocks)))
+            continue;
         wave_g2l(buf, rb, bs, lane);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         uint32_t ones = 0;
@@ -671,3 +690,5 @@ extern "C" hipError_t ppfs_parity_check(const uint8_t* r, uint8_t* d, uint8_t* s
     hipLaunchKernelGGL(parity_check_kernel, dim3(bk_grid(nb)), dim3(256), 0, s, r, d, st, nb, bs);
     return hipGetLastError();
 }
+
+PPFS_DBG_ACCESSOR(ppfs_dbg_faults_bit)

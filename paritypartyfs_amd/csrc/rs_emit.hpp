@@ -11,6 +11,8 @@
 // byte-indexed tables -- lost to the pair kernels and live on as an ablation in
 // tools/ablations/rs_col.hpp)
 #include <hip/hip_runtime.h>
+
+#include "dbg.hpp"
 #include <stdint.h>
 
 #include "gf_common.hpp"
@@ -105,14 +107,15 @@ template <int T2> __device__ __forceinline__ uint4 col_dec_piece(const uint8_t* 
 }
 
 // codeword byte `pos` of the LDS row ^= ev, and the same byte in HBM with write-back
+// (raw_bytes: extent of raw_g, PPFS_ECC_DEBUG bounds checks)
 __device__ __forceinline__ void col_fix(uint8_t* lds, uint32_t row, uint8_t* __restrict__ raw_g, uint64_t gblk, bool wb,
-    uint32_t pos, uint32_t ev)
+    uint32_t pos, uint32_t ev, [[maybe_unused]] uint64_t raw_bytes)
 {
     if (ev == 0)
         return;
     const uint8_t fixed = (uint8_t)(lds[row + pos] ^ ev);
     lds[row + pos] = fixed;
-    if (wb)
+    if (wb && PPFS_DBG_OK(raw_g + gblk * 255u + pos, 1, raw_g, raw_bytes))
         raw_g[gblk * 255u + pos] = fixed;
 }
 

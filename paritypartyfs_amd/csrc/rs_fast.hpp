@@ -27,6 +27,8 @@
 //   - Output rows are rebuilt in place in the same LDS buffer (interior dwords + byte-wise
 //     row ends) and streamed out with 16-byte stores.
 #include <hip/hip_runtime.h>
+
+#include "dbg.hpp"
 #include <stdint.h>
 
 #include "gf_common.hpp"
@@ -698,7 +700,8 @@ __device__ __forceinline__ void emit_payload_direct(uint8_t* tile, uint32_t l, u
 
 template <int T2, int NS, typename Pre>
 __device__ __forceinline__ void rs_decode_lane(uint8_t* tile, const uint8_t* lds, uint32_t l, bool valid,
-    uint8_t* __restrict__ raw_g, size_t blk, bool write_back, bool want_data, uint8_t* status_lds, Pre&& prefetch)
+    uint8_t* __restrict__ raw_g, size_t blk, bool write_back, bool want_data, uint8_t* status_lds, Pre&& prefetch,
+    [[maybe_unused]] uint64_t raw_bytes)
 {
     using Cf = RsCfg<T2, NS>;
     constexpr int K = Cf::K, W = Cf::W;
@@ -744,7 +747,7 @@ __device__ __forceinline__ void rs_decode_lane(uint8_t* tile, const uint8_t* lds
                     return;
                 const uint8_t fixed = (uint8_t)(tile[ib + pos] ^ e);
                 tile[ib + pos] = fixed;
-                if (write_back)
+                if (write_back && PPFS_DBG_OK(raw_g + blk * RS_N + pos, 1, raw_g, raw_bytes))
                     raw_g[blk * RS_N + pos] = fixed;
             };
             if (err) {
@@ -759,7 +762,7 @@ __device__ __forceinline__ void rs_decode_lane(uint8_t* tile, const uint8_t* lds
         } else if (geo && ge != 0) {
             // single-error lanes only: R stays as read; the byte is patched after emission
             const uint8_t fixed = (uint8_t)(tile[ib + gpos] ^ ge);
-            if (write_back)
+            if (write_back && PPFS_DBG_OK(raw_g + blk * RS_N + gpos, 1, raw_g, raw_bytes))
                 raw_g[blk * RS_N + gpos] = fixed;
             fpos = gpos;
             fval = fixed;
@@ -938,7 +941,8 @@ __global__ __launch_bounds__(256, 2) void rs255_encode_kernel(const uint8_t* __r
     // PF = 2: one-shot (grid covers every tile, no prefetch: other waves hide the latency)
     uint4 L[(IN_PIECES + 63) / 64];
     if (PF != 2)
-        load_regs_if<IN_PIECES, NT>(wt < nfull, L, data + wt * RS_WT * K, lane, tables);
+        load_regs_if<IN_PIECES, NT>(wt < nfull && PPFS_DBG_OK(data + wt * RS_WT * K, RS_WT * K, data, nblocks * K), L,
+            data + wt * RS_WT * K, lane, tables);
     for (; wt < nfull; wt += stride) {
         const uint64_t b0 = wt * RS_WT;
         if (PF == 2)
@@ -950,24 +954,30 @@ __global__ __launch_bounds__(256, 2) void rs255_encode_kernel(const uint8_t* __r
             rs_encode_lane<T2, NS>(tile, lds, lane, [&]() {
                 // block is in registers: prefetch the next tile now, its latency hides under compute
                 if (PF == 1)
-                    load_regs_if<IN_PIECES, NT>(nx < nfull, L, data + nx * RS_WT * K, lane, tables);
+                    load_regs_if<IN_PIECES, NT>(nx < nfull && PPFS_DBG_OK(data + nx * RS_WT * K, RS_WT * K, data, nblocks * K), L,
+                        data + nx * RS_WT * K, lane, tables);
             });
         } else {
             if (PF == 1)
-                load_regs_if<IN_PIECES, NT>(nx < nfull, L, data + nx * RS_WT * K, lane, tables);
+                load_regs_if<IN_PIECES, NT>(nx < nfull && PPFS_DBG_OK(data + nx * RS_WT * K, RS_WT * K, data, nblocks * K), L,
+                        data + nx * RS_WT * K, lane, tables);
         }
         wave_fence();
         uint4 o[(OUT_PIECES + 63) / 64];
         read_tile<OUT_PIECES>(o, tile, lane);
         if (PF == 0)
-            load_regs_if<IN_PIECES, NT>(nx < nfull, L, data + nx * RS_WT * K, lane, tables);
-        store_tile<OUT_PIECES, NT>(raw + b0 * RS_N, o, lane);
+            load_regs_if<IN_PIECES, NT>(nx < nfull && PPFS_DBG_OK(data + nx * RS_WT * K, RS_WT * K, data, nblocks * K), L,
+                        data + nx * RS_WT * K, lane, tables);
+        if (PPFS_DBG_OK(raw + b0 * RS_N, RS_WT * RS_N, raw, nblocks * RS_N))
+            store_tile<OUT_PIECES, NT>(raw + b0 * RS_N, o, lane);
         wave_fence();
     }
     // the one partial tile (nblocks % 64 blocks), by the wave whose walk reaches it
     if (wt == nfull && nfull < ntiles) {
         const uint64_t b0 = wt * RS_WT;
         const uint32_t nb = (uint32_t)(nblocks - b0);
+        if (!PPFS_DBG_OK(data + b0 * K, nb * K, data, nblocks * K) || !PPFS_DBG_OK(raw + b0 * RS_N, nb * RS_N, raw, nblocks * RS_N))
+            return;
         wave_stage_in(tile, data + b0 * K, nb * K, lane);
         wave_fence();
         rs_encode_lane<T2, NS>(tile, lds, lane, []() {});
@@ -1009,7 +1019,8 @@ __global__ __launch_bounds__(256, 2) void rs255_decode_kernel(uint8_t* __restric
     if constexpr (STAGE == 4) {
         // one-shot: loaded at the loop top
     } else if constexpr (REGS) {
-        load_regs_if<IN_PIECES, NT & 1>(wt < nfull, L, raw + wt * RS_WT * RS_N, lane, tables);
+        load_regs_if<IN_PIECES, NT & 1>(wt < nfull && PPFS_DBG_OK(raw + wt * RS_WT * RS_N, RS_WT * RS_N, raw, nblocks * RS_N),
+            L, raw + wt * RS_WT * RS_N, lane, tables);
     } else if (wt < nfull) {
         wave_dma_issue(tile, raw + wt * RS_WT * RS_N, IN_PIECES, lane);
     }
@@ -1024,23 +1035,28 @@ __global__ __launch_bounds__(256, 2) void rs255_decode_kernel(uint8_t* __restric
         wave_fence();
         const uint64_t nx = wt + stride;
         const bool nfullx = nx < nfull;
-        rs_decode_lane<T2, NS>(tile, lds, lane, true, raw, b0 + lane, wb, want, st_lds, [&]() {
+        rs_decode_lane<T2, NS>(tile, lds, lane, true, raw, b0 + lane, wb, want, st_lds,
+            [&]() {
             if constexpr (STAGE == 2)
-                load_regs_if<IN_PIECES, NT & 1>(nfullx, L, raw + nx * RS_WT * RS_N, lane, tables);
-        });
+                load_regs_if<IN_PIECES, NT & 1>(nfullx && PPFS_DBG_OK(raw + nx * RS_WT * RS_N, RS_WT * RS_N, raw, nblocks * RS_N),
+                L, raw + nx * RS_WT * RS_N, lane, tables);
+            },
+            nblocks * RS_N);
         wave_fence();
         uint4 o[(OUT_PIECES + 63) / 64];
         if (want)
             read_tile<OUT_PIECES>(o, tile, lane);
         const uint4 sv = (lane < 4) ? *(const uint4*)(st_lds + 16 * lane) : make_uint4(0, 0, 0, 0);
         if constexpr (STAGE == 0)
-            load_regs_if<IN_PIECES, NT & 1>(nfullx, L, raw + nx * RS_WT * RS_N, lane, tables);
-        if (want)
+            load_regs_if<IN_PIECES, NT & 1>(nfullx && PPFS_DBG_OK(raw + nx * RS_WT * RS_N, RS_WT * RS_N, raw, nblocks * RS_N),
+                L, raw + nx * RS_WT * RS_N, lane, tables);
+        if (want && PPFS_DBG_OK(data + b0 * K, RS_WT * K, data, nblocks * K))
             store_tile<OUT_PIECES, (NT >> 1) & 1>(data + b0 * K, o, lane);
-        if (status && lane < 4)
+        if (status && lane < 4 && PPFS_DBG_OK(status + b0 + 16 * lane, 16, status, nblocks))
             *(uint4*)(status + b0 + 16 * lane) = sv;
         if constexpr (STAGE == 1)
-            load_regs_if<IN_PIECES, NT & 1>(nfullx, L, raw + nx * RS_WT * RS_N, lane, tables);
+            load_regs_if<IN_PIECES, NT & 1>(nfullx && PPFS_DBG_OK(raw + nx * RS_WT * RS_N, RS_WT * RS_N, raw, nblocks * RS_N),
+                L, raw + nx * RS_WT * RS_N, lane, tables);
         wave_fence();
         if constexpr (STAGE == 3)
             if (nfullx)
@@ -1049,9 +1065,12 @@ __global__ __launch_bounds__(256, 2) void rs255_decode_kernel(uint8_t* __restric
     if (wt == nfull && nfull < ntiles) {
         const uint64_t b0 = wt * RS_WT;
         const uint32_t nb = (uint32_t)(nblocks - b0);
+        if (!PPFS_DBG_OK(raw + b0 * RS_N, nb * RS_N, raw, nblocks * RS_N) || (want && !PPFS_DBG_OK(data + b0 * K, nb * K, data, nblocks * K))
+            || (status && !PPFS_DBG_OK(status + b0, nb, status, nblocks)))
+            return;
         wave_stage_in(tile, raw + b0 * RS_N, nb * RS_N, lane);
         wave_fence();
-        rs_decode_lane<T2, NS>(tile, lds, lane, lane < nb, raw, b0 + lane, wb, want, st_lds, []() {});
+        rs_decode_lane<T2, NS>(tile, lds, lane, lane < nb, raw, b0 + lane, wb, want, st_lds, []() {}, nblocks * RS_N);
         wave_fence();
         if (want)
             wave_stage_out(data + b0 * K, tile, nb * K, lane);

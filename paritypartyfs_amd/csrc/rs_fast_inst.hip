@@ -219,3 +219,4 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
 #endif
     return hipGetLastError();
 }
+PPFS_DBG_ACCESSOR(PPFS_CAT(ppfs_dbg_faults_rs_t, PPFS_T2))

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "dbg.hpp"
 #include "gf_common.hpp"
 #include "rs_layout.hpp"
 
@@ -39,6 +40,8 @@ __global__ __launch_bounds__(256) void rs_generic_encode_kernel(const uint8_t* _
     const int k = n - t2;
     const uint8_t* d = data + blk * (uint64_t)k;
     uint8_t* o = raw + blk * (uint64_t)n;
+    if (!PPFS_DBG_OK(d, k, data, nblocks * k) || !PPFS_DBG_OK(o, n, raw, nblocks * n))
+        return;
     uint8_t r[256];
     for (int q = 0; q < t2; ++q)
         r[q] = 0;
@@ -65,6 +68,10 @@ __global__ __launch_bounds__(64) void rs_generic_decode_kernel(uint8_t* __restri
     const GfG gf { tables };
     const int k = n - t2;
     uint8_t* c = raw + blk * (uint64_t)n;
+    if (!PPFS_DBG_OK(c, n, raw, nblocks * n) || (data && !PPFS_DBG_OK(data + blk * (uint64_t)k, k, data, nblocks * k))
+        || (status && !PPFS_DBG_OK(status + blk, 1, status, nblocks))
+        || (spill && !PPFS_DBG_OK(spill + blk * (uint64_t)(256 - n), 256 - n, spill, nblocks * (256 - n))))
+        return;
     uint8_t cw[256];
     for (int i = 0; i < n; ++i)
         cw[i] = c[i];
@@ -250,3 +257,5 @@ extern "C" hipError_t ppfs_rs_generic_decode(uint8_t* r, uint8_t* d, uint8_t* st
     hipLaunchKernelGGL(rs_generic_decode_kernel, dim3(grid), dim3(64), 0, s, r, d, st, spill, nb, n, t2, wb, tab);
     return hipGetLastError();
 }
+
+PPFS_DBG_ACCESSOR(ppfs_dbg_faults_rs_generic)

@@ -197,7 +197,7 @@ __device__ __forceinline__ uint32_t pair_or(uint32_t v) { return v | pair_xchg(v
 // RM: the state is c mod g (coefficient q has exponent i q in S_i) instead of x^2t c mod g
 template <int T2, bool RM = false>
 __device__ __noinline__ void pair_correct_general(uint8_t* lds, uint32_t goff, uint32_t row, uint32_t slot, uint32_t c,
-    uint8_t* __restrict__ raw_g, uint64_t gblk, bool wb)
+    uint8_t* __restrict__ raw_g, uint64_t gblk, bool wb, uint64_t raw_bytes)
 {
     const Gf gf { lds + goff };
     const uint4 r0 = *(const uint4*)(lds + slot), r1 = *(const uint4*)(lds + slot + 16);
@@ -229,7 +229,7 @@ __device__ __noinline__ void pair_correct_general(uint8_t* lds, uint32_t goff, u
 #pragma unroll
         for (int i = 0; i < T2; ++i)
             S[i] = (sw8[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-        rs_correct_general<T2>(S, gf, [&](uint32_t pos, uint32_t ev) { col_fix(lds, row, raw_g, gblk, wb, pos, ev); });
+        rs_correct_general<T2>(S, gf, [&](uint32_t pos, uint32_t ev) { col_fix(lds, row, raw_g, gblk, wb, pos, ev, raw_bytes); });
     }
 }
 
@@ -238,7 +238,7 @@ __device__ __noinline__ void pair_correct_general(uint8_t* lds, uint32_t goff, u
 template <int T2, bool RM = false>
 __device__ __forceinline__ uint32_t pair_correct(uint8_t* lds, uint32_t goff, const uint8_t* __restrict__ xp, uint32_t row,
     uint32_t slot,
-    uint32_t c, const uint32_t (&s)[4], bool valid, uint8_t* __restrict__ raw_g, uint64_t gblk, bool wb)
+    uint32_t c, const uint32_t (&s)[4], bool valid, uint8_t* __restrict__ raw_g, uint64_t gblk, bool wb, uint64_t raw_bytes)
 {
     const bool err = valid && pair_or(s[0] | s[1] | s[2] | s[3]) != 0u;
     if (!__builtin_amdgcn_ballot_w64(err))
@@ -274,9 +274,9 @@ __device__ __forceinline__ uint32_t pair_correct(uint8_t* lds, uint32_t goff, co
     }
     const bool geo = err && pair_or(bad) == 0u;
     if (geo && c == 0)
-        col_fix(lds, row, raw_g, gblk, wb, lx, gf.exp(le));
+        col_fix(lds, row, raw_g, gblk, wb, lx, gf.exp(le), raw_bytes);
     if (err && !geo)
-        pair_correct_general<T2, RM>(lds, goff, row, slot, c, raw_g, gblk, wb);
+        pair_correct_general<T2, RM>(lds, goff, row, slot, c, raw_g, gblk, wb, raw_bytes);
     return err ? 1u : 0u;
 }
 
@@ -311,14 +311,15 @@ template <int T2> __device__ __forceinline__ uint4 dec_piece(const uint8_t* lds,
 
 // LDS-DMA of a tile by 128 threads: piece p = tid + 128 k lands at dst + 16 p.
 template <int NPIECE>
-__device__ __forceinline__ void dma_tile128(uint8_t* dst, const uint8_t* __restrict__ src, uint32_t tid)
+__device__ __forceinline__ void dma_tile128(uint8_t* dst, const uint8_t* __restrict__ src, uint32_t tid,
+    [[maybe_unused]] const uint8_t* gbase, [[maybe_unused]] uint64_t extent)
 {
     constexpr int K = (NPIECE + NTHR - 1) / NTHR;
     const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(dst) + (tid & ~63u) * 16u);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const uint32_t p = tid + (uint32_t)NTHR * k;
-        if ((k + 1) * NTHR <= NPIECE || p < (uint32_t)NPIECE)
+        if (((k + 1) * NTHR <= NPIECE || p < (uint32_t)NPIECE) && PPFS_DBG_OK(src + (size_t)p * 16, 16, gbase, extent))
             dma16(src + (size_t)p * 16, base + 16u * NTHR * k);
     }
 }
@@ -365,14 +366,14 @@ __global__ __launch_bounds__(NTHR, 2) void rs_pair_encode_kernel(const uint8_t* 
     uint64_t t = blockIdx.x;
     uint32_t cur = 0;
     if (t < nfull)
-        dma_tile128<IN_PIECES>(lds + D::OFF_BUF + PAD, data + t * (TB * K), tid);
+        dma_tile128<IN_PIECES>(lds + D::OFF_BUF + PAD, data + t * (TB * K), tid, data, nblocks * K);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (; t < nfull; t += gridDim.x) {
         barrier_lds(); // A: tile t in LDS, the last tile's emission reads done
         const uint32_t buf = D::OFF_BUF + cur * BUF;
         const uint64_t nx = t + gridDim.x;
         if (NBUF == 2 && nx < nfull)
-            dma_tile128<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, data + nx * (TB * K), tid);
+            dma_tile128<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, data + nx * (TB * K), tid, data, nblocks * K);
         uint32_t s[4];
         pair_remainder<K>(s, lds, buf + PAD + (uint32_t)K * blk, tb, c);
         *(uint4*)(lds + D::OFF_PAR + 32u * blk + 16u * c) = make_uint4(s[0], s[1], s[2], s[3]);
@@ -392,7 +393,7 @@ __global__ __launch_bounds__(NTHR, 2) void rs_pair_encode_kernel(const uint8_t* 
         if constexpr (NBUF == 1) {
             barrier_lds(); // every wave's emission reads done: the buffer is free
             if (nx < nfull)
-                dma_tile128<IN_PIECES>(lds + D::OFF_BUF + PAD, data + nx * (TB * K), tid);
+                dma_tile128<IN_PIECES>(lds + D::OFF_BUF + PAD, data + nx * (TB * K), tid, data, nblocks * K);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // other workgroups overlap this wait
         } else {
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); // next tile's DMA landed; stores may fly
@@ -474,7 +475,7 @@ __global__ __launch_bounds__(64 * NW, 2) void rs_pair_encode_img_kernel(const ui
         for (int k = 0; k < KP; ++k) {
             const uint32_t i = tid + (uint32_t)NT * k;
             const int so = img_src<T2>(i);
-            if (((k + 1) * NT <= PIECES || i < (uint32_t)PIECES) && so >= 0)
+            if (((k + 1) * NT <= PIECES || i < (uint32_t)PIECES) && so >= 0 && PPFS_DBG_OK(src + so, 16, data, nblocks * K))
                 dma16(src + so, img_base + 16u * NT * k);
         }
     };
@@ -497,7 +498,7 @@ __global__ __launch_bounds__(64 * NW, 2) void rs_pair_encode_img_kernel(const ui
 #pragma unroll
         for (int k = 0; k < KP; ++k) {
             const uint32_t i = tid + (uint32_t)NT * k;
-            if ((k + 1) * NT <= PIECES || i < (uint32_t)PIECES)
+            if (((k + 1) * NT <= PIECES || i < (uint32_t)PIECES) && PPFS_DBG_OK(dst + 16u * i, 16, raw, nblocks * 255u))
                 st_nt<NTST>(dst + 16u * i, ld16(lds, IMG + 16u * i));
         }
         barrier_lds(); // C: the image is free
@@ -511,6 +512,8 @@ __global__ __launch_bounds__(64 * NW, 2) void rs_pair_encode_img_kernel(const ui
         barrier_lds();
         const uint32_t nb = (uint32_t)(nblocks - t * TBK);
         const uint8_t* src = data + t * (TBK * K);
+        if (!PPFS_DBG_OK(src, nb * (uint32_t)K, data, nblocks * K))
+            return;
         for (uint32_t j = tid; j < nb * (uint32_t)K; j += NT) {
             const uint32_t b = j / (uint32_t)K;
             lds[row - 255u * blk + 255u * b + (j - (uint32_t)K * b)] = src[j];
@@ -526,6 +529,8 @@ __global__ __launch_bounds__(64 * NW, 2) void rs_pair_encode_img_kernel(const ui
         const uint32_t nout = nb * 255u;
         for (uint32_t i = tid; 16u * i < nout; i += NT) {
             const uint4 v = ld16(lds, IMG + 16u * i);
+            if (!PPFS_DBG_OK(dst + 16u * i, min(16u, nout - 16u * i), raw, nblocks * 255u))
+                continue;
             if (16u * i + 16u <= nout)
                 *(uint4*)(dst + 16u * i) = v;
             else
@@ -584,7 +589,7 @@ __global__ __launch_bounds__(64 * NW, 2) void rs_solo_encode_img_kernel(const ui
         for (int k = 0; k < KP; ++k) {
             const uint32_t i = tid + (uint32_t)NT * k;
             const int so = img_src<T2>(i);
-            if (((k + 1) * NT <= PIECES || i < (uint32_t)PIECES) && so >= 0)
+            if (((k + 1) * NT <= PIECES || i < (uint32_t)PIECES) && so >= 0 && PPFS_DBG_OK(src + so, 16, data, nblocks * K))
                 dma16(src + so, img_base + 16u * NT * k);
         }
     };
@@ -607,7 +612,7 @@ __global__ __launch_bounds__(64 * NW, 2) void rs_solo_encode_img_kernel(const ui
 #pragma unroll
         for (int k = 0; k < KP; ++k) {
             const uint32_t i = tid + (uint32_t)NT * k;
-            if ((k + 1) * NT <= PIECES || i < (uint32_t)PIECES)
+            if (((k + 1) * NT <= PIECES || i < (uint32_t)PIECES) && PPFS_DBG_OK(dst + 16u * i, 16, raw, nblocks * 255u))
                 st_nt<NTST>(dst + 16u * i, ld16(lds, IMG + 16u * i));
         }
         barrier_lds(); // C: the image is free
@@ -620,6 +625,8 @@ __global__ __launch_bounds__(64 * NW, 2) void rs_solo_encode_img_kernel(const ui
         barrier_lds();
         const uint32_t nb = (uint32_t)(nblocks - t * TBK);
         const uint8_t* src = data + t * (TBK * K);
+        if (!PPFS_DBG_OK(src, nb * (uint32_t)K, data, nblocks * K))
+            return;
         for (uint32_t j = tid; j < nb * (uint32_t)K; j += NT) {
             const uint32_t b = j / (uint32_t)K;
             lds[IMG + T2 + 255u * b + (j - (uint32_t)K * b)] = src[j];
@@ -635,6 +642,8 @@ __global__ __launch_bounds__(64 * NW, 2) void rs_solo_encode_img_kernel(const ui
         const uint32_t nout = nb * 255u;
         for (uint32_t i = tid; 16u * i < nout; i += NT) {
             const uint4 v = ld16(lds, IMG + 16u * i);
+            if (!PPFS_DBG_OK(dst + 16u * i, min(16u, nout - 16u * i), raw, nblocks * 255u))
+                continue;
             if (16u * i + 16u <= nout)
                 *(uint4*)(dst + 16u * i) = v;
             else
@@ -668,14 +677,14 @@ __global__ __launch_bounds__(NTHR, (WPC >= 5 ? 3 : 2)) void rs_pair_decode_kerne
     uint64_t t = blockIdx.x;
     uint32_t cur = 0;
     if (t < nfull)
-        dma_tile128<IN_PIECES>(lds + D::OFF_BUF + PAD, raw + t * (TB * 255), tid);
+        dma_tile128<IN_PIECES>(lds + D::OFF_BUF + PAD, raw + t * (TB * 255), tid, raw, nblocks * 255u);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     for (; t < nfull; t += gridDim.x) {
         barrier_lds(); // A
         const uint32_t buf = D::OFF_BUF + cur * BUF;
         const uint64_t nx = t + gridDim.x;
         if (NBUF == 2 && nx < nfull)
-            dma_tile128<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, raw + nx * (TB * 255), tid);
+            dma_tile128<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, raw + nx * (TB * 255), tid, raw, nblocks * 255u);
         const uint32_t row = buf + PAD + 255u * blk;
         uint32_t s[4];
         if constexpr (RM)
@@ -685,8 +694,8 @@ __global__ __launch_bounds__(NTHR, (WPC >= 5 ? 3 : 2)) void rs_pair_decode_kerne
         *(uint4*)(lds + slot + 16u * c) = make_uint4(s[0], s[1], s[2], s[3]); // read by the general path
         wave_fence();
         const uint32_t st = pair_correct<T2, RM>(
-            lds, L::OFF_GF, tables + (RM ? L::OFF_XPM : L::OFF_XP), row, slot, c, s, true, raw, t * TB + blk, wb);
-        if (status && c == 0)
+            lds, L::OFF_GF, tables + (RM ? L::OFF_XPM : L::OFF_XP), row, slot, c, s, true, raw, t * TB + blk, wb, nblocks * 255u);
+        if (status && c == 0 && PPFS_DBG_OK(status + t * TB + blk, 1, status, nblocks))
             status[t * TB + blk] = (uint8_t)st;
         barrier_lds(); // C: corrections patched into the LDS rows
         uint8_t* dst = want ? data + t * (TB * K) : nullptr;
@@ -697,14 +706,14 @@ __global__ __launch_bounds__(NTHR, (WPC >= 5 ? 3 : 2)) void rs_pair_decode_kerne
             for (int k = 0; k < KOUT; ++k) {
                 const uint32_t p = tid_o + (uint32_t)NTHR * k;
                 const uint4 o = dec_piece<T2>(lds, buf, p);
-                if ((k + 1) * NTHR <= OUT_PIECES || p < (uint32_t)OUT_PIECES)
+                if (((k + 1) * NTHR <= OUT_PIECES || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, data, nblocks * K))
                     st_nt<NTST>(dst + 16u * p, o);
             }
         }
         if constexpr (NBUF == 1) {
             barrier_lds(); // emission reads done: the buffer is free
             if (nx < nfull)
-                dma_tile128<IN_PIECES>(lds + D::OFF_BUF + PAD, raw + nx * (TB * 255), tid);
+                dma_tile128<IN_PIECES>(lds + D::OFF_BUF + PAD, raw + nx * (TB * 255), tid, raw, nblocks * 255u);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // other workgroups overlap this wait
         } else if (want) {
             asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
@@ -718,7 +727,8 @@ __global__ __launch_bounds__(NTHR, (WPC >= 5 ? 3 : 2)) void rs_pair_decode_kerne
         barrier_lds();
         const uint32_t nb = (uint32_t)(nblocks - t * TB);
         const uint32_t buf = D::OFF_BUF + cur * BUF;
-        stage_bytes128(lds + buf + PAD, raw + t * (TB * 255), nb * 255u, tid);
+        if (PPFS_DBG_OK(raw + t * (TB * 255), nb * 255u, raw, nblocks * 255u))
+            stage_bytes128(lds + buf + PAD, raw + t * (TB * 255), nb * 255u, tid);
         barrier_lds();
         const uint32_t row = buf + PAD + 255u * blk;
         uint32_t s[4];
@@ -730,8 +740,8 @@ __global__ __launch_bounds__(NTHR, (WPC >= 5 ? 3 : 2)) void rs_pair_decode_kerne
         wave_fence();
         const bool valid = blk < nb;
         const uint32_t st = pair_correct<T2, RM>(
-            lds, L::OFF_GF, tables + (RM ? L::OFF_XPM : L::OFF_XP), row, slot, c, s, valid, raw, t * TB + blk, wb);
-        if (status && valid && c == 0)
+            lds, L::OFF_GF, tables + (RM ? L::OFF_XPM : L::OFF_XP), row, slot, c, s, valid, raw, t * TB + blk, wb, nblocks * 255u);
+        if (status && valid && c == 0 && PPFS_DBG_OK(status + t * TB + blk, 1, status, nblocks))
             status[t * TB + blk] = (uint8_t)st;
         barrier_lds();
         if (want) {
@@ -739,6 +749,8 @@ __global__ __launch_bounds__(NTHR, (WPC >= 5 ? 3 : 2)) void rs_pair_decode_kerne
             const uint32_t nout = nb * (uint32_t)K;
             for (uint32_t p = tid; 16u * p < nout; p += NTHR) {
                 const uint4 v = dec_piece<T2>(lds, buf, p);
+                if (!PPFS_DBG_OK(dst + 16u * p, min(16u, nout - 16u * p), data, nblocks * K))
+                    continue;
                 if (16u * p + 16u <= nout)
                     *(uint4*)(dst + 16u * p) = v;
                 else

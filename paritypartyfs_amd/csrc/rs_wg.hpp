@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "dbg.hpp"
 #include "gf_common.hpp"
 #include "rs_fast.hpp"
 #include "rs_layout.hpp"
@@ -69,16 +70,18 @@ __device__ __forceinline__ uint32_t lds_addr(const uint8_t* p)
 
 // LDS-DMA of NPIECE 16-byte pieces: piece p = tid + 256k lands at dst + 16p (wave-uniform base
 // dst + 1024 * (4k + wave), + 16 * lane implicit).  Exactly 4 instructions per wave.
+// (base, extent): the global buffer the tile lies in (PPFS_ECC_DEBUG bounds checks, dbg.hpp)
 template <int NPIECE>
-__device__ __forceinline__ void dma_tile(uint8_t* dst, const uint8_t* __restrict__ src, uint32_t tid)
+__device__ __forceinline__ void dma_tile(uint8_t* dst, const uint8_t* __restrict__ src, uint32_t tid,
+    [[maybe_unused]] const uint8_t* base, [[maybe_unused]] uint64_t extent)
 {
     static_assert(NPIECE > 768 && NPIECE <= 1024, "4 pieces per thread, every wave active in each");
-    const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(dst) + (tid & ~63u) * 16u);
+    const uint32_t lbase = __builtin_amdgcn_readfirstlane(lds_addr(dst) + (tid & ~63u) * 16u);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const uint32_t p = tid + 256u * k;
-        if (k < 3 || p < (uint32_t)NPIECE)
-            dma16(src + (size_t)p * 16, base + 4096u * k);
+        if ((k < 3 || p < (uint32_t)NPIECE) && PPFS_DBG_OK(src + (size_t)p * 16, 16, base, extent))
+            dma16(src + (size_t)p * 16, lbase + 4096u * k);
     }
 }
 
@@ -379,7 +382,7 @@ __device__ __forceinline__ void stage_bytes(uint8_t* dst, const uint8_t* __restr
 // fix(pos, e) patches codeword byte pos of the lane's row (LDS) and, with write-back, in HBM.
 template <int T2>
 __device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, uint32_t par, uint32_t r, bool valid,
-    uint8_t* __restrict__ raw_g, uint64_t blk, bool wb)
+    uint8_t* __restrict__ raw_g, uint64_t blk, bool wb, [[maybe_unused]] uint64_t raw_bytes)
 {
     using L = RsWgLayout<T2>;
     const uint64_t rem = *(const uint64_t*)(lds + par + 8u * r);
@@ -414,7 +417,7 @@ __device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, ui
                 return;
             const uint8_t fixed = (uint8_t)(lds[row + pos] ^ e);
             lds[row + pos] = fixed;
-            if (wb)
+            if (wb && PPFS_DBG_OK(raw_g + blk * 255u + pos, 1, raw_g, raw_bytes))
                 raw_g[blk * 255u + pos] = fixed;
         };
         if (__builtin_amdgcn_ballot_w64(err && !geo)) {
@@ -510,14 +513,14 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_kernel(const uint8_t* _
     uint64_t t = blockIdx.x;
     uint32_t cur = 0, pc = 0; // tile buffer, parity-slot set
     if (t < nfull)
-        dma_tile<IN_PIECES>(lds + D::OFF_BUF + PAD, data + t * (TB * K), tid);
+        dma_tile<IN_PIECES>(lds + D::OFF_BUF + PAD, data + t * (TB * K), tid, data, nblocks * K);
     uint32_t hist = 0, iter = 0;
     if constexpr (NBUF >= 3) {
 #pragma unroll
         for (int j = 1; j <= NBUF - 2; ++j) {
             const bool go = t + j * gridDim.x < nfull;
             if (go)
-                dma_tile<IN_PIECES>(lds + D::OFF_BUF + j * BUF + PAD, data + (t + j * gridDim.x) * (TB * K), tid);
+                dma_tile<IN_PIECES>(lds + D::OFF_BUF + j * BUF + PAD, data + (t + j * gridDim.x) * (TB * K), tid, data, nblocks * K);
             hist = (hist << 1) | (go ? 1u : 0u);
         }
         vm_wait_newer(4u * __builtin_popcount(hist)); // tile t landed, the later ones may fly
@@ -529,12 +532,12 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_kernel(const uint8_t* _
         const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + pc * 512u;
         const uint64_t nx = t + gridDim.x;
         if (NBUF == 2 && nx < nfull)
-            dma_tile<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, data + nx * (TB * K), tid);
+            dma_tile<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, data + nx * (TB * K), tid, data, nblocks * K);
         if constexpr (NBUF >= 3) { // NBUF - 1 tiles ahead, into the buffer tile t - G used
             const uint64_t ahead = t + (uint64_t)(NBUF - 1) * gridDim.x;
             const bool go = ahead < nfull;
             if (go)
-                dma_tile<IN_PIECES>(lds + D::OFF_BUF + ring_add(cur, NBUF - 1, NBUF) * BUF + PAD, data + ahead * (TB * K), tid);
+                dma_tile<IN_PIECES>(lds + D::OFF_BUF + ring_add(cur, NBUF - 1, NBUF) * BUF + PAD, data + ahead * (TB * K), tid, data, nblocks * K);
             hist = (hist << 1) | (go ? 1u : 0u);
         }
         if (wave == 0)
@@ -553,7 +556,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_kernel(const uint8_t* _
                 o[k] = enc_piece<T2>(lds, buf, par, p);
             else
                 o[k] = *(const uint4*)(lds + buf + PAD + 16u * (p < 996u ? p : p - 64u));
-            if (NBUF != 1 && (k < 3 || p < (uint32_t)OUT_PIECES))
+            if (NBUF != 1 && (k < 3 || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, raw, nblocks * 255u))
                 st_nt<NTST>(dst + 16u * p, o[k]); // store as soon as the piece is assembled
             if constexpr (NBUF == 0)
                 asm volatile("" ::: "memory"); // one piece live at a time
@@ -561,11 +564,11 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_kernel(const uint8_t* _
         if (NBUF == 1) {
             barrier_lds(); // every wave's emission reads done: the buffer is free
             if (nx < nfull)
-                dma_tile<IN_PIECES>(lds + D::OFF_BUF + PAD, data + nx * (TB * K), tid);
+                dma_tile<IN_PIECES>(lds + D::OFF_BUF + PAD, data + nx * (TB * K), tid, data, nblocks * K);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const uint32_t p = tid + 256u * k;
-                if (k < 3 || p < (uint32_t)OUT_PIECES)
+                if ((k < 3 || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, raw, nblocks * 255u))
                     st_nt<NTST>(dst + 16u * p, o[k]);
             }
         }
@@ -588,7 +591,8 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_kernel(const uint8_t* _
         barrier_lds();
         const uint32_t nb = (uint32_t)(nblocks - t * TB);
         const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + pc * 512u;
-        stage_bytes(lds + buf + PAD, data + t * (TB * K), nb * K, tid);
+        if (PPFS_DBG_OK(data + t * (TB * K), nb * K, data, nblocks * K))
+            stage_bytes(lds + buf + PAD, data + t * (TB * K), nb * K, tid);
         barrier_lds();
         phase_remainder<T2, K>(lds, buf, par, wave, row);
         barrier_lds();
@@ -596,6 +600,8 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_kernel(const uint8_t* _
         const uint32_t nout = nb * 255u;
         for (uint32_t p = tid; 16u * p < nout; p += NTHR) {
             const uint4 v = enc_piece<T2>(lds, buf, par, p);
+            if (!PPFS_DBG_OK(dst + 16u * p, min(16u, nout - 16u * p), raw, nblocks * 255u))
+                continue;
             if (16u * p + 16u <= nout)
                 *(uint4*)(dst + 16u * p) = v;
             else
@@ -764,14 +770,14 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_kernel(uint8_t* __restr
     uint64_t t = blockIdx.x;
     uint32_t cur = 0, pc = 0;
     if (t < nfull)
-        dma_tile<IN_PIECES>(lds + D::OFF_BUF + PAD, raw + t * (TB * 255), tid);
+        dma_tile<IN_PIECES>(lds + D::OFF_BUF + PAD, raw + t * (TB * 255), tid, raw, nblocks * 255u);
     uint32_t hist = 0, iter = 0;
     if constexpr (NBUF >= 3) {
 #pragma unroll
         for (int j = 1; j <= NBUF - 2; ++j) {
             const bool go = t + j * gridDim.x < nfull;
             if (go)
-                dma_tile<IN_PIECES>(lds + D::OFF_BUF + j * BUF + PAD, raw + (t + j * gridDim.x) * (TB * 255), tid);
+                dma_tile<IN_PIECES>(lds + D::OFF_BUF + j * BUF + PAD, raw + (t + j * gridDim.x) * (TB * 255), tid, raw, nblocks * 255u);
             hist = (hist << 1) | (go ? 1u : 0u);
         }
         vm_wait_newer(4u * __builtin_popcount(hist));
@@ -783,12 +789,12 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_kernel(uint8_t* __restr
         const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + pc * 512u;
         const uint64_t nx = t + gridDim.x;
         if (NBUF == 2 && nx < nfull)
-            dma_tile<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, raw + nx * (TB * 255), tid);
+            dma_tile<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, raw + nx * (TB * 255), tid, raw, nblocks * 255u);
         if constexpr (NBUF >= 3) {
             const uint64_t ahead = t + (uint64_t)(NBUF - 1) * gridDim.x;
             const bool go = ahead < nfull;
             if (go)
-                dma_tile<IN_PIECES>(lds + D::OFF_BUF + ring_add(cur, NBUF - 1, NBUF) * BUF + PAD, raw + ahead * (TB * 255), tid);
+                dma_tile<IN_PIECES>(lds + D::OFF_BUF + ring_add(cur, NBUF - 1, NBUF) * BUF + PAD, raw + ahead * (TB * 255), tid, raw, nblocks * 255u);
             hist = (hist << 1) | (go ? 1u : 0u);
         }
         if (wave == 0)
@@ -797,8 +803,8 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_kernel(uint8_t* __restr
             phase_remainder<T2, 255>(lds, buf, par, wave, row);
         barrier_lds(); // B: remainders complete
         if ((MODE & 4) && wave == 0) {
-            const uint32_t st = phase_correct<T2>(lds, buf, par, row, true, raw, t * TB + row, wb);
-            if (status)
+            const uint32_t st = phase_correct<T2>(lds, buf, par, row, true, raw, t * TB + row, wb, nblocks * 255u);
+            if (status && PPFS_DBG_OK(status + t * TB + row, 1, status, nblocks))
                 status[t * TB + row] = (uint8_t)st;
         }
         barrier_lds(); // C: corrections patched into the LDS rows
@@ -814,7 +820,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_kernel(uint8_t* __restr
                     o[k] = dec_piece<T2>(lds, buf, p);
                 else
                     o[k] = *(const uint4*)(lds + buf + PAD + 16u * p);
-                if (NBUF != 1 && (k < 3 || p < (uint32_t)OUT_PIECES))
+                if (NBUF != 1 && (k < 3 || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, data, nblocks * K))
                     st_nt<NTST>(dst + 16u * p, o[k]);
                 if constexpr (NBUF == 0)
                     asm volatile("" ::: "memory");
@@ -823,12 +829,12 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_kernel(uint8_t* __restr
         if (NBUF == 1) {
             barrier_lds();
             if (nx < nfull)
-                dma_tile<IN_PIECES>(lds + D::OFF_BUF + PAD, raw + nx * (TB * 255), tid);
+                dma_tile<IN_PIECES>(lds + D::OFF_BUF + PAD, raw + nx * (TB * 255), tid, raw, nblocks * 255u);
             if (want) {
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const uint32_t p = tid + 256u * k;
-                    if (k < 3 || p < (uint32_t)OUT_PIECES)
+                    if ((k < 3 || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, data, nblocks * K))
                         st_nt<NTST>(dst + 16u * p, o[k]);
                 }
             }
@@ -854,14 +860,15 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_kernel(uint8_t* __restr
         barrier_lds();
         const uint32_t nb = (uint32_t)(nblocks - t * TB);
         const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + pc * 512u;
-        stage_bytes(lds + buf + PAD, raw + t * (TB * 255), nb * 255u, tid);
+        if (PPFS_DBG_OK(raw + t * (TB * 255), nb * 255u, raw, nblocks * 255u))
+            stage_bytes(lds + buf + PAD, raw + t * (TB * 255), nb * 255u, tid);
         barrier_lds();
         phase_remainder<T2, 255>(lds, buf, par, wave, row);
         barrier_lds();
         if (wave == 0) {
             const bool valid = row < nb;
-            const uint32_t st = phase_correct<T2>(lds, buf, par, row, valid, raw, t * TB + row, wb);
-            if (status && valid)
+            const uint32_t st = phase_correct<T2>(lds, buf, par, row, valid, raw, t * TB + row, wb, nblocks * 255u);
+            if (status && valid && PPFS_DBG_OK(status + t * TB + row, 1, status, nblocks))
                 status[t * TB + row] = (uint8_t)st;
         }
         barrier_lds();
@@ -870,6 +877,8 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_kernel(uint8_t* __restr
             const uint32_t nout = nb * (uint32_t)K;
             for (uint32_t p = tid; 16u * p < nout; p += NTHR) {
                 const uint4 v = dec_piece<T2>(lds, buf, p);
+                if (!PPFS_DBG_OK(dst + 16u * p, min(16u, nout - 16u * p), data, nblocks * K))
+                    continue;
                 if (16u * p + 16u <= nout)
                     *(uint4*)(dst + 16u * p) = v;
                 else

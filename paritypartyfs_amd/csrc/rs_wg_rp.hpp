@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_rp_kernel(uint8_t* __re
         phase_remainder<T2, 255>(lds, buf, par, wave, row);
         barrier_lds(); // B: remainders complete
         if (wave == 0) {
-            const uint32_t st = phase_correct<T2>(lds, buf, par, row, true, raw, t * TB + row, wb);
+            const uint32_t st = phase_correct<T2>(lds, buf, par, row, true, raw, t * TB + row, wb, nblocks * 255u);
             if (status)
                 status[t * TB + row] = (uint8_t)st;
         }
@@ -214,7 +214,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_rp_kernel(uint8_t* __re
         barrier_lds();
         if (wave == 0) {
             const bool valid = row < nb;
-            const uint32_t st = phase_correct<T2>(lds, buf, par, row, valid, raw, t * TB + row, wb);
+            const uint32_t st = phase_correct<T2>(lds, buf, par, row, valid, raw, t * TB + row, wb, nblocks * 255u);
             if (status && valid)
                 status[t * TB + row] = (uint8_t)st;
         }

@@ -7,6 +7,8 @@
 // one thread per byte: out = (a & b) | (a & c) | (b & c) as one v_bitop3, and a record's damage
 // bits are set with one atomic OR only where a byte disagrees.
 #include <hip/hip_runtime.h>
+
+#include "dbg.hpp"
 #include <stdint.h>
 
 namespace ppfs {
@@ -50,12 +52,14 @@ extern "C" hipError_t ppfs_vote3_launch(const uint8_t* a, const uint8_t* b, cons
 // (status 1), packed for one D2H copy when they are few.  One workgroup per row, 16-byte pieces
 // where source and destination are 16-byte aligned, else bytes.
 namespace ppfs {
-__global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-    const uint32_t* __restrict__ idx, uint32_t nrows, uint32_t row_bytes)
+__global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* __restrict__ src, [[maybe_unused]] uint64_t src_rows,
+    uint8_t* __restrict__ dst, const uint32_t* __restrict__ idx, uint32_t nrows, uint32_t row_bytes)
 {
     for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
         const uint8_t* s = src + (uint64_t)idx[r] * row_bytes;
         uint8_t* d = dst + (uint64_t)r * row_bytes;
+        if (!PPFS_DBG_OK(s, row_bytes, src, src_rows * row_bytes) || !PPFS_DBG_OK(d, row_bytes, dst, (uint64_t)nrows * row_bytes))
+            continue;
         if ((((uintptr_t)s | (uintptr_t)d | row_bytes) & 15u) == 0) {
             for (uint32_t p = threadIdx.x; 16u * p < row_bytes; p += blockDim.x)
                 *(uint4*)(d + 16u * p) = *(const uint4*)(s + 16u * p);
@@ -104,12 +108,42 @@ extern "C" hipError_t ppfs_copy_launch(uint8_t* dst, const uint8_t* src, uint64_
     return hipGetLastError();
 }
 
-extern "C" hipError_t ppfs_gather_rows_launch(const uint8_t* src, uint8_t* dst, const uint32_t* idx, uint32_t nrows,
-    uint32_t row_bytes, hipStream_t s)
+// src holds src_rows rows; idx[i] < src_rows
+extern "C" hipError_t ppfs_gather_rows_launch(const uint8_t* src, uint64_t src_rows, uint8_t* dst, const uint32_t* idx,
+    uint32_t nrows, uint32_t row_bytes, hipStream_t s)
 {
     if (nrows == 0)
         return hipSuccess;
     const uint32_t grid = nrows < 4096u ? nrows : 4096u;
-    hipLaunchKernelGGL(ppfs::gather_rows_kernel, dim3(grid), dim3(256), 0, s, src, dst, idx, nrows, row_bytes);
+    hipLaunchKernelGGL(ppfs::gather_rows_kernel, dim3(grid), dim3(256), 0, s, src, src_rows, dst, idx, nrows, row_bytes);
     return hipGetLastError();
 }
+
+PPFS_DBG_ACCESSOR(ppfs_dbg_faults_vote)
+
+// Positive control of the PPFS_ECC_DEBUG checks (tests/test_gpu_hygiene.py): a gather of row 5
+// from a 4-row source must be reported and skipped.  Returns the number of reports (the counter is
+// restored afterwards, so the suite's per-test accounting is unaffected); -1 in normal builds.
+#ifdef PPFS_ECC_DEBUG
+extern "C" long long ppfs_ecc_debug_selftest(void)
+{
+    uint8_t *src = nullptr, *dst = nullptr;
+    uint32_t* idx = nullptr;
+    const uint32_t bad = 5;
+    unsigned long long before = 0, after = 0;
+    long long r = -2;
+    if (hipMalloc(&src, 4 * 16) == hipSuccess && hipMalloc(&dst, 16) == hipSuccess && hipMalloc(&idx, 4) == hipSuccess
+        && hipMemcpy(idx, &bad, 4, hipMemcpyHostToDevice) == hipSuccess
+        && hipMemcpyFromSymbol(&before, HIP_SYMBOL(ppfs::dbg::g_faults), sizeof(before)) == hipSuccess
+        && ppfs_gather_rows_launch(src, 4, dst, idx, 1, 16, nullptr) == hipSuccess && hipDeviceSynchronize() == hipSuccess
+        && hipMemcpyFromSymbol(&after, HIP_SYMBOL(ppfs::dbg::g_faults), sizeof(after)) == hipSuccess
+        && hipMemcpyToSymbol(HIP_SYMBOL(ppfs::dbg::g_faults), &before, sizeof(before)) == hipSuccess)
+        r = (long long)(after - before);
+    (void)hipFree(src);
+    (void)hipFree(dst);
+    (void)hipFree(idx);
+    return r;
+}
+#else
+extern "C" long long ppfs_ecc_debug_selftest(void) { return -1; }
+#endif

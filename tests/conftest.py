@@ -31,6 +31,9 @@ def _gpu_fault_guard(request):
     """After every GPU test: collect the test's garbage (engine contexts destroyed here, not at some
     later test's GC point), then drain the device.  A fault of work a test queued asynchronously
     is then reported against that test, not at the next unrelated torch call."""
+    from paritypartyfs_amd import _native
+
+    before = _native.debug_faults() if request.node.get_closest_marker("gpu") is not None else None
     yield
     if request.node.get_closest_marker("gpu") is None:
         return
@@ -44,3 +47,9 @@ def _gpu_fault_guard(request):
             torch.cuda.synchronize()
         except RuntimeError as e:  # sticky asynchronous error: name the test that queued it
             pytest.fail(f"asynchronous GPU fault after {request.node.nodeid}: {e}", pytrace=False)
+    # PPFS_ECC_DEBUG builds (PPFS_ECC_LIB=.../libppfs_ecc_debug.so): kernels count the global
+    # accesses outside the extents their launch implies (csrc/dbg.hpp)
+    after = _native.debug_faults()
+    if after is not None and after != (before or 0):
+        pytest.fail(f"{after - (before or 0)} out-of-bounds kernel accesses in {request.node.nodeid} "
+                    "(PPFS_ECC_DEBUG; details on stdout)", pytrace=False)

@@ -159,3 +159,17 @@ def test_many_contexts_created_and_destroyed_across_threads(oracle):
         eng.close()
         assert np.array_equal(raw, want)
         assert np.array_equal(r.cpu().numpy(), want)
+
+
+def test_debug_bounds_checks_positive_control():
+    """PPFS_ECC_DEBUG builds (tools/gpu_debug_suite.sh): a deliberately out-of-range row gather is
+    reported and skipped by the kernel, so a green debug suite means the checks ran and found
+    nothing.  Normal builds have no checks (-1)."""
+    from paritypartyfs_amd import _native
+
+    L = _native.lib()
+    n = L.ppfs_ecc_debug_selftest()
+    if _native.debug_faults() is None:
+        assert n == -1
+    else:
+        assert n >= 1, n

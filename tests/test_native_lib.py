@@ -64,3 +64,19 @@ def test_param_validation_without_gpu(lib):
 
 def test_crc_implicit_to_explicit(lib):
     assert lib.ppfs_ecc_crc_implicit_to_explicit(0xad0424f3) == 0x15a0849e7
+
+
+def test_normal_build_has_no_debug_checks(lib):
+    # PPFS_ECC_DEBUG instrumentation (csrc/dbg.hpp) is compiled out of the product library
+    assert lib.ppfs_ecc_debug_faults() == -1
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True).stdout
+    assert "ppfs_dbg_faults_" not in out
+
+
+def test_debug_build_exports_its_counters():
+    dbg = os.path.join(ROOT, "paritypartyfs_amd", "_lib", "alt", "libppfs_ecc_debug.so")
+    if not os.path.exists(dbg):
+        pytest.skip("no PPFS_ECC_DEBUG build (tools/build_alt.sh debug -DPPFS_ECC_DEBUG=1)")
+    out = subprocess.run(["nm", "-D", "--defined-only", dbg], capture_output=True, text=True).stdout
+    units = re.findall(r"\bT (ppfs_dbg_faults_\w+)$", out, flags=re.M)
+    assert len(units) == 11, units  # 7 RS instantiations, generic RS, bit, bit-fast, vote
