@@ -66,10 +66,18 @@ constexpr int fit_wpc(int bytes, int most) { return 163840 / bytes < most ? 1638
 #define PPFS_WG_DEC_NBUF 2
 #endif
 static_assert(PPFS_WG_ENC_NBUF >= 2 && PPFS_WG_ENC_NBUF <= 4 && PPFS_WG_DEC_NBUF >= 2 && PPFS_WG_DEC_NBUF <= 4, "NBUF 2..4");
+// PPFS_WG_ENC_COMPACT = 1 (ablation): the compact encode LDS layout (rs_wg.hpp Lds: 2 maps,
+// payload-sized tile buffers), so a ring of 3 buffers fits 3 workgroups per CU.  Slower: 2^20
+// blocks hot / from HBM 101 / 104 -> 108 / 111 us (3 ring buffers) and 103 / 106 us (4 buffers,
+// 2 workgroups) (profiles/r2_ablations/compact_enc_kablate.jsonl)
+#ifndef PPFS_WG_ENC_COMPACT
+#define PPFS_WG_ENC_COMPACT 0
+#endif
+constexpr bool ENC_COMPACT = PPFS_WG_ENC_COMPACT != 0 && !WG_FULL;
 constexpr int ENC_NBUF = WG_FULL ? 0 : PPFS_WG_ENC_NBUF;
 [[maybe_unused]] constexpr int ENC_WPC = WG_FULL ? fit_wpc(wg::lds_bytes<PPFS_T2, false, 0>(), PPFS_WG_FULL)
-    : ENC_NBUF >= 3          ? fit_wpc(wg::lds_bytes<PPFS_T2, false, ENC_NBUF>(), 4)
-                             : ((4 * wg::lds_bytes<PPFS_T2, false, 2>() <= 163840) ? 4 : 3);
+    : ENC_NBUF >= 3          ? fit_wpc(wg::lds_bytes<PPFS_T2, false, ENC_NBUF, ENC_COMPACT>(), 4)
+                             : ((4 * wg::lds_bytes<PPFS_T2, false, 2, ENC_COMPACT>() <= 163840) ? 4 : 3);
 // PPFS_WG_DEC_FULL = N (ablation): decode on a full grid, N workgroups per CU, one tile each.
 // Standalone from HBM ("cold") it is faster (2^20 blocks: 106-108 -> 91-99 us), but inside the
 // bench step slower (99.7 -> 103.7 us) and in the step is where the headline is measured,
@@ -175,7 +183,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
         hipLaunchKernelGGL((wg::rs_wg_encode_img_kernel<PPFS_T2, PPFS_WG_ENC_IMG_WPC, PPFS_ENC_NTST>),
             dim3(rs_tile_grid(nb, 1 << 24)), dim3(256), 0, s, d, r, nb, tab);
     else
-        hipLaunchKernelGGL((wg::rs_wg_encode_kernel<PPFS_T2, ENC_NBUF, ENC_WPC, PPFS_ENC_MODE, PPFS_ENC_NTST>), dim3(rs_tile_grid(nb, WG_FULL ? (1 << 24) : ENC_WPC)), dim3(256),
+        hipLaunchKernelGGL((wg::rs_wg_encode_kernel<PPFS_T2, ENC_NBUF, ENC_WPC, PPFS_ENC_MODE, PPFS_ENC_NTST, ENC_COMPACT>), dim3(rs_tile_grid(nb, WG_FULL ? (1 << 24) : ENC_WPC)), dim3(256),
             0, s, d, r, nb, tab);
 #endif
 #elif PPFS_T2 > 16

@@ -213,19 +213,22 @@ template <int T2, int S> __device__ __forceinline__ void seg_map(uint32_t (&s)[2
 __device__ __forceinline__ uint32_t lane_row(uint32_t lane) { return ((lane & 31u) << 1) | (lane >> 5); }
 
 // Phase 1 for this wave's segment of block `blk`: XOR its remainder into the block's slot
-template <int T2, int LEN>
+template <int T2, int LEN, int NMAP = 3>
 __device__ __forceinline__ void phase_remainder_row(uint8_t* lds, uint32_t row, uint32_t par, uint32_t wave, uint32_t blk);
 
-template <int T2, int LEN>
+// NMAP = x^(64 s) maps in LDS: 3 (one per segment), or 2 (x^64, x^128; segment 3 applies both,
+// which frees 2t x 256 B of LDS for the compact encode layout)
+template <int T2, int LEN, int NMAP = 3>
 __device__ __forceinline__ void phase_remainder(uint8_t* lds, uint32_t buf, uint32_t par, uint32_t wave, uint32_t blk)
 {
-    phase_remainder_row<T2, LEN>(lds, buf + PAD + (uint32_t)LEN * blk, par, wave, blk);
+    phase_remainder_row<T2, LEN, NMAP>(lds, buf + PAD + (uint32_t)LEN * blk, par, wave, blk);
 }
 
 // the same for a LEN-byte row at LDS byte `row` (any row layout)
-template <int T2, int LEN>
+template <int T2, int LEN, int NMAP>
 __device__ __forceinline__ void phase_remainder_row(uint8_t* lds, uint32_t row, uint32_t par, uint32_t wave, uint32_t blk)
 {
+    static_assert(NMAP == 2 || NMAP == 3, "x^(64 s) maps");
     uint32_t s[2];
     switch (wave) {
     case 0:
@@ -241,7 +244,12 @@ __device__ __forceinline__ void phase_remainder_row(uint8_t* lds, uint32_t row, 
         break;
     default:
         seg_remainder<T2, LEN, 3>(s, lds, row);
-        seg_map<T2, 3>(s, lds);
+        if constexpr (NMAP == 3) {
+            seg_map<T2, 3>(s, lds);
+        } else {
+            seg_map<T2, 1>(s, lds); // x^192 = x^64 x^128
+            seg_map<T2, 2>(s, lds);
+        }
         break;
     }
     const uint64_t v = ((uint64_t)s[1] << 32) | s[0];
@@ -469,16 +477,21 @@ __device__ __forceinline__ void vm_wait_newer(uint32_t n)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int T2, bool DEC, int NBUF> struct Lds {
+// COMPACT (encode only): 2 maps (phase_remainder NMAP = 2) and tile buffers sized for the 64
+// payload rows (PAD + 64 K + 32) instead of 64 codewords, so 3 ring buffers fit 3 workgroups / CU
+template <int T2, bool DEC, int NBUF, bool COMPACT = false> struct Lds {
     using L = RsWgLayout<T2>;
-    static constexpr int TBL = DEC ? L::TABLE_BYTES : L::OFF_SYN; // encode needs SL + MAP only
+    static_assert(!(DEC && COMPACT), "compact layout: encode only");
+    static constexpr int NMAP = COMPACT ? 2 : 3;
+    static constexpr int TBL = DEC ? L::TABLE_BYTES : L::OFF_MAP + NMAP * L::MAP_STRIDE; // encode: SL + MAP only
     static constexpr int OFF_PAR = TBL;                              // 2 x 64 x 8 B remainder slots
     static constexpr int OFF_BUF = OFF_PAR + 1024 + 64;             // + slack: par[b+1] over-read
-    static constexpr int BYTES = OFF_BUF + (NBUF ? NBUF : 1) * BUF;
+    static constexpr int BUFB = COMPACT ? (PAD + TB * L::K + 32 + 15) / 16 * 16 : BUF; // one tile buffer
+    static constexpr int BYTES = OFF_BUF + (NBUF ? NBUF : 1) * BUFB;
     static_assert(OFF_BUF % 16 == 0 && TBL % 16 == 0, "aligned buffers");
 };
 
-template <int T2, bool DEC, int NBUF> constexpr int lds_bytes() { return Lds<T2, DEC, NBUF>::BYTES; }
+template <int T2, bool DEC, int NBUF, bool COMPACT = false> constexpr int lds_bytes() { return Lds<T2, DEC, NBUF, COMPACT>::BYTES; }
 
 // LDS declared per workgroup: at least the layout, and more than 1/(WPC+1) of the CU's 160 KiB, so
 // exactly WPC workgroups are resident per CU -- a WPC x CUs persistent grid is then balanced
@@ -491,12 +504,13 @@ template <int BYTES, int WPC> constexpr int lds_alloc()
 
 // MODE (ablation builds only; the engine uses 3): bit 0 = remainder phase, bit 1 = codeword
 // emission (else a plain 16-byte copy out of the LDS tile, same bytes moved)
-template <int T2, int NBUF = 2, int WPC = 4, int MODE = 3, int NTST = 1>
+template <int T2, int NBUF = 2, int WPC = 4, int MODE = 3, int NTST = 1, bool COMPACT = false>
 __global__ __launch_bounds__(256, WPC) void rs_wg_encode_kernel(const uint8_t* __restrict__ data,
     uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables)
 {
     using L = RsWgLayout<T2>;
-    using D = Lds<T2, false, NBUF>;
+    using D = Lds<T2, false, NBUF, COMPACT>;
+    constexpr int BUF = D::BUFB;
     constexpr int LDS_ALLOC = lds_alloc<D::BYTES, WPC>();
     static_assert(WPC * LDS_ALLOC <= 163840, "LDS for WPC workgroups per CU");
     constexpr int K = L::K;
@@ -543,7 +557,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_kernel(const uint8_t* _
         if (wave == 0)
             *(uint64_t*)(lds + D::OFF_PAR + (pc ^ 1u) * 512u + 8u * lane) = 0;
         if constexpr (MODE & 1)
-            phase_remainder<T2, K>(lds, buf, par, wave, row);
+            phase_remainder<T2, K, D::NMAP>(lds, buf, par, wave, row);
         barrier_lds(); // B: parity slots complete
         uint8_t* dst = raw + t * (TB * 255);
         uint4 o[4];
@@ -594,7 +608,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_kernel(const uint8_t* _
         if (PPFS_DBG_OK(data + t * (TB * K), nb * K, data, nblocks * K))
             stage_bytes(lds + buf + PAD, data + t * (TB * K), nb * K, tid);
         barrier_lds();
-        phase_remainder<T2, K>(lds, buf, par, wave, row);
+        phase_remainder<T2, K, D::NMAP>(lds, buf, par, wave, row);
         barrier_lds();
         uint8_t* dst = raw + t * (TB * 255);
         const uint32_t nout = nb * 255u;
