@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <functional>
 #include <cstdio>
 #include <cstdlib>
@@ -23,12 +24,15 @@
 
 #include "../../include/ppfs_ecc.h"
 #include "rs_layout.hpp"
+#include "server_box.hpp"
 
 // kernels (rs_kernels.hip / bit_kernels.hip)
 extern "C" {
 int ppfs_rs_fast_supported(int n, int t2);
 int ppfs_rs_fast_tables_bytes(int t2);
 hipError_t ppfs_rs_fast_encode(int t2, const uint8_t* d, uint8_t* r, uint64_t nb, const uint8_t* tab, hipStream_t s);
+hipError_t ppfs_rs_server_launch(int t2, ppfs::SrvBox* box, uint8_t* zc, uint64_t zc_bytes, const uint8_t* tab,
+    uint32_t gen, uint32_t idle_us, hipStream_t s);
 hipError_t ppfs_rs_fast_decode(int t2, uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, const uint8_t* tab, int wb,
     hipStream_t s);
 hipError_t ppfs_rs_generic_encode(const uint8_t* d, uint8_t* r, uint64_t nb, int n, int t2, const uint8_t* tab,
@@ -442,6 +446,14 @@ struct ppfs_ecc_ctx {
     uint8_t* h_zc = nullptr;
     uint8_t* d_zc = nullptr;
     size_t zc_bytes = 0;
+    // resident small-batch server (RS 2t <= 8, server_box.hpp): mailbox, its stream, the current
+    // launch generation, the last request number; srv_ok = -1 undecided, 0 off, 1 on
+    ppfs::SrvBox* h_box = nullptr;
+    ppfs::SrvBox* d_box = nullptr;
+    hipStream_t srv_stream = nullptr;
+    uint32_t srv_gen = 0, srv_seq = 0;
+    bool srv_launched = false;
+    int srv_ok = -1;
 };
 
 extern "C" uint64_t ppfs_ecc_crc_implicit_to_explicit(uint64_t implicit_poly) { return (implicit_poly << 1) + 1; }
@@ -567,6 +579,16 @@ extern "C" void ppfs_ecc_destroy(ppfs_ecc_ctx* c)
     if (!c)
         return;
     DeviceGuard guard(c->device);
+    // the resident server leaves at `stop` (it polls every few microseconds) before anything it
+    // reads is freed
+    if (c->srv_launched) {
+        __atomic_store_n(&c->h_box->stop, 1u, __ATOMIC_RELEASE);
+        (void)hipStreamSynchronize(c->srv_stream);
+    }
+    if (c->srv_stream)
+        (void)hipStreamDestroy(c->srv_stream);
+    if (c->h_box)
+        (void)hipHostFree(c->h_box);
     // Nothing the context queued may outlive it: its own streams drain before they are destroyed
     // and before the staging buffers their copies and kernels use are freed.  Work the caller
     // queued on its own streams (device entry points) is the caller's to order; the device-wide
@@ -939,6 +961,90 @@ static int device_op(ppfs_ecc_ctx* c, HostOp op, uint8_t* d, const Layout& L, si
 
 constexpr size_t kSmallBlocks = 64; // one tile: the per-block IBlockDevice calls
 
+// ---- resident small-batch server (server_box.hpp, rs_wg.hpp rs_wg_server_kernel) ----
+// RS with 2t <= 8 (the segment-layout tables): a per-block call posts its request to the resident
+// workgroup instead of launching kernels and synchronizing a stream (measured on the box, RS(255,249),
+// one block: launch + stream synchronize alone 10.3 us, a whole decode_host call 16.2 us).
+// PPFS_ECC_SERVER=0 turns it off (the launch path below).
+constexpr uint32_t kSrvIdleUs = 20000; // a launch leaves after 20 ms without a request
+
+static bool server_eligible(ppfs_ecc_ctx* c)
+{
+    if (c->srv_ok < 0) {
+        const char* e = std::getenv("PPFS_ECC_SERVER");
+        const bool off = e && e[0] == '0';
+        c->srv_ok = (!off && c->p.ecc_type == PPFS_ECC_REED_SOLOMON && c->rs_fast && c->rs_t2 <= 8) ? 1 : 0;
+    }
+    return c->srv_ok == 1;
+}
+
+// stop the resident launch (if any) and wait until it has returned
+static void server_stop(ppfs_ecc_ctx* c)
+{
+    if (!c->srv_launched)
+        return;
+    __atomic_store_n(&c->h_box->stop, 1u, __ATOMIC_RELEASE);
+    (void)hipStreamSynchronize(c->srv_stream);
+    (void)hipGetLastError();
+    c->srv_launched = false;
+}
+
+static int server_launch(ppfs_ecc_ctx* c)
+{
+    const uint32_t gen = (++c->srv_gen) & ~ppfs::SRV_EXITED;
+    c->srv_gen = gen;
+    __atomic_store_n(&c->h_box->stop, 0u, __ATOMIC_RELEASE);
+    HIP_TRY(ppfs_rs_server_launch(c->rs_t2, c->d_box, c->d_zc, c->zc_bytes, c->d_tables, gen, kSrvIdleUs, c->srv_stream),
+        "server launch");
+    c->srv_launched = true;
+    return 0;
+}
+
+static int server_call(ppfs_ecc_ctx* c, HostOp op, const Layout& L, size_t nb, int write_back, bool want_data)
+{
+    using namespace ppfs;
+    if (!c->h_box) {
+        HIP_TRY(hipHostMalloc((void**)&c->h_box, sizeof(SrvBox), hipHostMallocMapped | hipHostMallocCoherent),
+            "server mailbox");
+        std::memset((void*)c->h_box, 0, sizeof(SrvBox));
+        HIP_TRY(hipHostGetDevicePointer((void**)&c->d_box, c->h_box, 0), "server mailbox map");
+        HIP_TRY(hipStreamCreateWithFlags(&c->srv_stream, hipStreamNonBlocking), "server stream");
+    }
+    SrvBox* b = c->h_box;
+    const SrvLayout sl = srv_layout((uint32_t)nb, c->data, c->raw);
+    if (nb < 1 || nb > SRV_MAX_BLOCKS || sl.data != L.data || sl.raw != L.raw || sl.status != L.status)
+        return fail(PPFS_ECC_EINVAL, "small-batch server: layout mismatch");
+    const SrvCmd sc { (uint32_t)nb, op == OP_ENCODE ? SRV_ENCODE : (op == OP_DECODE ? SRV_DECODE : SRV_WRITE),
+        write_back != 0, want_data };
+    c->srv_seq = (c->srv_seq + 1) & 0xFFFFu;
+    const uint32_t seq = srv_cmd_pack(c->srv_seq, sc);
+    __atomic_store_n(&b->cmd, seq, __ATOMIC_RELEASE); // publishes the request and its input bytes
+    auto exited = [&]() { return __atomic_load_n(&b->alive, __ATOMIC_ACQUIRE) == (c->srv_gen | SRV_EXITED); };
+    if (!c->srv_launched || exited()) {
+        const int r = server_launch(c);
+        if (r)
+            return r;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 1;; ++spin) {
+        if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq)
+            return 0;
+        if ((spin & 255u) == 0) {
+            if (exited()) { // the launch left (idle / lifetime) without seeing this request
+                const int r = server_launch(c);
+                if (r)
+                    return r;
+            } else if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+                server_stop(c);
+                c->srv_ok = 0; // this context uses the launch path from now on
+                if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq)
+                    return 0;
+                return fail(PPFS_ECC_EHIP, "small-batch server: no answer within 10 s");
+            }
+        }
+    }
+}
+
 // Small batches run the kernels on coherent host memory in place: no H2D / D2H copies on the
 // critical path of a per-block readBlock / writeBlock (each async copy costs microseconds).
 static int host_run_small(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t* data_out, uint8_t* raw,
@@ -946,6 +1052,7 @@ static int host_run_small(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, ui
 {
     const Layout L = layout_for(c, nb);
     if (c->zc_bytes < L.total) {
+        server_stop(c); // it holds the buffer's address
         if (c->h_zc && c->hs[0])
             HIP_TRY(hipStreamSynchronize(c->hs[0]), "zero-copy sync");
         if (c->h_zc)
@@ -965,10 +1072,16 @@ static int host_run_small(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, ui
         std::memcpy(h + L.data, data_in, nb * c->data);
     if (op != OP_ENCODE || raw_is_rmw(c))
         std::memcpy(h + L.raw, raw, nb * c->raw);
-    int r = device_op(c, op, c->d_zc, L, nb, write_back, data_out != nullptr, spill != nullptr, c->hs[0]);
-    if (r)
-        return r;
-    HIP_TRY(hipStreamSynchronize(c->hs[0]), "sync");
+    if (server_eligible(c) && !spill) {
+        const int r = server_call(c, op, L, nb, write_back, data_out != nullptr);
+        if (r)
+            return r;
+    } else {
+        const int r = device_op(c, op, c->d_zc, L, nb, write_back, data_out != nullptr, spill != nullptr, c->hs[0]);
+        if (r)
+            return r;
+        HIP_TRY(hipStreamSynchronize(c->hs[0]), "sync");
+    }
     if (op == OP_ENCODE || op == OP_WRITE)
         std::memcpy(raw, h + L.raw, nb * c->raw);
     else if (write_back) // only the codewords the decode changed (status 1)

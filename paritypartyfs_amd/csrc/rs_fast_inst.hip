@@ -228,3 +228,13 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
     return hipGetLastError();
 }
 PPFS_DBG_ACCESSOR(PPFS_CAT(ppfs_dbg_faults_rs_t, PPFS_T2))
+
+// resident small-batch server (2t <= 8; rs_wg.hpp rs_wg_server_kernel, api.cpp host_run_server)
+#if PPFS_T2 <= 8
+extern "C" hipError_t PPFS_CAT(ppfs_rs_server_launch_t, PPFS_T2)(ppfs::SrvBox* box, uint8_t* zc, uint64_t zc_bytes,
+    const uint8_t* tab, uint32_t gen, uint32_t idle_us, hipStream_t s)
+{
+    hipLaunchKernelGGL((wg::rs_wg_server_kernel<PPFS_T2>), dim3(1), dim3(256), 0, s, box, zc, zc_bytes, tab, gen, idle_us);
+    return hipGetLastError();
+}
+#endif

@@ -6,6 +6,7 @@
 #include "dbg.hpp"
 #include "gf_common.hpp"
 #include "rs_layout.hpp"
+#include "server_box.hpp"
 
 namespace ppfs {
 
@@ -236,6 +237,27 @@ extern "C" hipError_t ppfs_rs_fast_decode(int t2, uint8_t* r, uint8_t* d, uint8_
     case T:                                                                                                            \
         return ppfs_rs_fast_decode_t##T(r, d, st, nb, tab, wb, s);
         PPFS_RS_CASES(X)
+#undef X
+    default:
+        return hipErrorInvalidValue;
+    }
+}
+
+// resident small-batch server (2t <= 8: the segment-layout tables)
+#define PPFS_RS_SERVER_CASES(X) X(2) X(4) X(6) X(8)
+#define X(T)                                                                                                           \
+    extern "C" hipError_t ppfs_rs_server_launch_t##T(ppfs::SrvBox*, uint8_t*, uint64_t, const uint8_t*, uint32_t,      \
+        uint32_t, hipStream_t);
+PPFS_RS_SERVER_CASES(X)
+#undef X
+extern "C" hipError_t ppfs_rs_server_launch(int t2, ppfs::SrvBox* box, uint8_t* zc, uint64_t zc_bytes, const uint8_t* tab,
+    uint32_t gen, uint32_t idle_us, hipStream_t s)
+{
+    switch (t2) {
+#define X(T)                                                                                                           \
+    case T:                                                                                                            \
+        return ppfs_rs_server_launch_t##T(box, zc, zc_bytes, tab, gen, idle_us, s);
+        PPFS_RS_SERVER_CASES(X)
 #undef X
     default:
         return hipErrorInvalidValue;
