@@ -31,6 +31,7 @@ extern "C" {
 int ppfs_rs_fast_supported(int n, int t2);
 int ppfs_rs_fast_tables_bytes(int t2);
 hipError_t ppfs_rs_fast_encode(int t2, const uint8_t* d, uint8_t* r, uint64_t nb, const uint8_t* tab, hipStream_t s);
+hipError_t ppfs_flag_launch(uint32_t* flag, uint32_t v, hipStream_t s);
 hipError_t ppfs_rs_server_launch(int t2, ppfs::SrvBox* box, uint8_t* zc, uint64_t zc_bytes, const uint8_t* tab,
     uint32_t gen, uint32_t idle_us, hipStream_t s);
 hipError_t ppfs_rs_fast_decode(int t2, uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, const uint8_t* tab, int wb,
@@ -451,7 +452,7 @@ struct ppfs_ecc_ctx {
     ppfs::SrvBox* h_box = nullptr;
     ppfs::SrvBox* d_box = nullptr;
     hipStream_t srv_stream = nullptr;
-    uint32_t srv_gen = 0, srv_seq = 0;
+    uint32_t srv_gen = 0, srv_seq = 0, flag_seq = 0;
     bool srv_launched = false;
     int srv_ok = -1;
 };
@@ -587,8 +588,6 @@ extern "C" void ppfs_ecc_destroy(ppfs_ecc_ctx* c)
     }
     if (c->srv_stream)
         (void)hipStreamDestroy(c->srv_stream);
-    if (c->h_box)
-        (void)hipHostFree(c->h_box);
     // Nothing the context queued may outlive it: its own streams drain before they are destroyed
     // and before the staging buffers their copies and kernels use are freed.  Work the caller
     // queued on its own streams (device entry points) is the caller's to order; the device-wide
@@ -613,6 +612,8 @@ extern "C" void ppfs_ecc_destroy(ppfs_ecc_ctx* c)
         (void)hipFree(c->d_scratch);
     if (c->h_zc)
         (void)hipHostFree(c->h_zc);
+    if (c->h_box) // after the streams drained: the launch path's flag kernels write it
+        (void)hipHostFree(c->h_box);
     delete c;
 }
 
@@ -1000,14 +1001,49 @@ static int server_launch(ppfs_ecc_ctx* c)
     return 0;
 }
 
+// the context's mailbox (server requests, completion flag of the launch path)
+static int ensure_box(ppfs_ecc_ctx* c)
+{
+    if (c->h_box)
+        return 0;
+    HIP_TRY(hipHostMalloc((void**)&c->h_box, sizeof(ppfs::SrvBox), hipHostMallocMapped | hipHostMallocCoherent),
+        "mailbox");
+    std::memset((void*)c->h_box, 0, sizeof(ppfs::SrvBox));
+    HIP_TRY(hipHostGetDevicePointer((void**)&c->d_box, c->h_box, 0), "mailbox map");
+    return 0;
+}
+
+// Wait for the small-batch launch path's work on stream s: a flag kernel after it stores a fresh
+// number into the mailbox and the host spins on it (hipStreamSynchronize's completion signal
+// costs ~4 us more per call).  A faulting kernel never lets the flag arrive: the stream is queried
+// every few thousand spins and its error returned.
+static int wait_flag(ppfs_ecc_ctx* c, hipStream_t s)
+{
+    int r = ensure_box(c);
+    if (r)
+        return r;
+    const uint32_t v = ++c->flag_seq;
+    HIP_TRY(ppfs_flag_launch(&c->d_box->flag, v, s), "flag launch");
+    for (uint32_t spin = 1;; ++spin) {
+        if (__atomic_load_n(&c->h_box->flag, __ATOMIC_ACQUIRE) == v)
+            return 0;
+        if ((spin & 4095u) == 0) {
+            const hipError_t e = hipStreamQuery(s);
+            if (e != hipErrorNotReady && e != hipSuccess)
+                return check_hip(e, "small-batch kernels");
+            if (e == hipSuccess && __atomic_load_n(&c->h_box->flag, __ATOMIC_ACQUIRE) != v)
+                return fail(PPFS_ECC_EHIP, "small-batch completion flag missing");
+        }
+    }
+}
+
 static int server_call(ppfs_ecc_ctx* c, HostOp op, const Layout& L, size_t nb, int write_back, bool want_data)
 {
     using namespace ppfs;
-    if (!c->h_box) {
-        HIP_TRY(hipHostMalloc((void**)&c->h_box, sizeof(SrvBox), hipHostMallocMapped | hipHostMallocCoherent),
-            "server mailbox");
-        std::memset((void*)c->h_box, 0, sizeof(SrvBox));
-        HIP_TRY(hipHostGetDevicePointer((void**)&c->d_box, c->h_box, 0), "server mailbox map");
+    if (!c->srv_stream) {
+        const int r = ensure_box(c);
+        if (r)
+            return r;
         HIP_TRY(hipStreamCreateWithFlags(&c->srv_stream, hipStreamNonBlocking), "server stream");
     }
     SrvBox* b = c->h_box;
@@ -1077,10 +1113,11 @@ static int host_run_small(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, ui
         if (r)
             return r;
     } else {
-        const int r = device_op(c, op, c->d_zc, L, nb, write_back, data_out != nullptr, spill != nullptr, c->hs[0]);
+        int r = device_op(c, op, c->d_zc, L, nb, write_back, data_out != nullptr, spill != nullptr, c->hs[0]);
+        if (!r)
+            r = wait_flag(c, c->hs[0]);
         if (r)
             return r;
-        HIP_TRY(hipStreamSynchronize(c->hs[0]), "sync");
     }
     if (op == OP_ENCODE || op == OP_WRITE)
         std::memcpy(raw, h + L.raw, nb * c->raw);

@@ -53,7 +53,8 @@ struct alignas(64) SrvBox {
     uint32_t done;   // device -> host: the last cmd served
     uint32_t alive;  // device -> host: generation (| SRV_EXITED after return)
     uint64_t served; // requests served by this launch (diagnostics)
-    uint32_t pad1[12];
+    uint32_t flag;   // device -> host: completion of the launch path (api.cpp wait_flag)
+    uint32_t pad1[11];
 };
 static_assert(sizeof(SrvBox) == 128, "mailbox layout: one request line, one reply line");
 
