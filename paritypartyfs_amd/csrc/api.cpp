@@ -963,7 +963,7 @@ static int device_op(ppfs_ecc_ctx* c, HostOp op, uint8_t* d, const Layout& L, si
 constexpr size_t kSmallBlocks = 64; // one tile: the per-block IBlockDevice calls
 
 // ---- resident small-batch server (server_box.hpp, rs_wg.hpp rs_wg_server_kernel) ----
-// RS with 2t <= 8 (the segment-layout tables): a per-block call posts its request to the resident
+// RS with 2t <= 8 or 2t = 32 (rs_wg / rs_pair servers): a per-block call posts its request to the resident
 // workgroup instead of launching kernels and synchronizing a stream (measured on the box, RS(255,249),
 // one block: launch + stream synchronize alone 10.3 us, a whole decode_host call 16.2 us).
 // PPFS_ECC_SERVER=0 turns it off (the launch path below).
@@ -974,7 +974,9 @@ static bool server_eligible(ppfs_ecc_ctx* c)
     if (c->srv_ok < 0) {
         const char* e = std::getenv("PPFS_ECC_SERVER");
         const bool off = e && e[0] == '0';
-        c->srv_ok = (!off && c->p.ecc_type == PPFS_ECC_REED_SOLOMON && c->rs_fast && c->rs_t2 <= 8) ? 1 : 0;
+        c->srv_ok = (!off && c->p.ecc_type == PPFS_ECC_REED_SOLOMON && c->rs_fast && (c->rs_t2 <= 8 || c->rs_t2 == 32))
+            ? 1
+            : 0;
     }
     return c->srv_ok == 1;
 }

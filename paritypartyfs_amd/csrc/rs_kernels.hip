@@ -243,8 +243,8 @@ extern "C" hipError_t ppfs_rs_fast_decode(int t2, uint8_t* r, uint8_t* d, uint8_
     }
 }
 
-// resident small-batch server (2t <= 8: the segment-layout tables)
-#define PPFS_RS_SERVER_CASES(X) X(2) X(4) X(6) X(8)
+// resident small-batch servers (2t <= 8: segment-layout tables; 2t = 32: pair layout)
+#define PPFS_RS_SERVER_CASES(X) X(2) X(4) X(6) X(8) X(32)
 #define X(T)                                                                                                           \
     extern "C" hipError_t ppfs_rs_server_launch_t##T(ppfs::SrvBox*, uint8_t*, uint64_t, const uint8_t*, uint32_t,      \
         uint32_t, hipStream_t);

@@ -29,6 +29,7 @@
 
 #include "gf_common.hpp"
 #include "rs_emit.hpp"
+#include "srv_device.hpp"
 #include "rs_fast.hpp"
 #include "rs_layout.hpp"
 #include "rs_wg.hpp"
@@ -195,7 +196,9 @@ __device__ __forceinline__ uint32_t pair_or(uint32_t v) { return v | pair_xchg(v
 // i = 16c+1 .. 16c+16 into the block's slot (over r', which both lanes have read), then lane 0
 // runs BM / roots / Forney (rs_fast.hpp).
 // RM: the state is c mod g (coefficient q has exponent i q in S_i) instead of x^2t c mod g
-template <int T2, bool RM = false>
+// TAG: a separate instance per calling kernel (the server's looser register budget must not
+// become the decode kernel's: an out-of-line function is compiled once for all its callers)
+template <int T2, bool RM = false, int TAG = 0>
 __device__ __noinline__ void pair_correct_general(uint8_t* lds, uint32_t goff, uint32_t row, uint32_t slot, uint32_t c,
     uint8_t* __restrict__ raw_g, uint64_t gblk, bool wb, uint64_t raw_bytes)
 {
@@ -235,7 +238,7 @@ __device__ __noinline__ void pair_correct_general(uint8_t* lds, uint32_t goff, u
 
 // Decode correction for the pair's block; s = the lane's column of r' = x^2t c(x) mod g.  Single
 // error: S_1, S_2 -> X = S_2/S_1, e = S_1/X, confirmed iff r' == e * XP row LOG X.
-template <int T2, bool RM = false>
+template <int T2, bool RM = false, int TAG = 0>
 __device__ __forceinline__ uint32_t pair_correct(uint8_t* lds, uint32_t goff, const uint8_t* __restrict__ xp, uint32_t row,
     uint32_t slot,
     uint32_t c, const uint32_t (&s)[4], bool valid, uint8_t* __restrict__ raw_g, uint64_t gblk, bool wb, uint64_t raw_bytes)
@@ -276,7 +279,7 @@ __device__ __forceinline__ uint32_t pair_correct(uint8_t* lds, uint32_t goff, co
     if (geo && c == 0)
         col_fix(lds, row, raw_g, gblk, wb, lx, gf.exp(le), raw_bytes);
     if (err && !geo)
-        pair_correct_general<T2, RM>(lds, goff, row, slot, c, raw_g, gblk, wb, raw_bytes);
+        pair_correct_general<T2, RM, TAG>(lds, goff, row, slot, c, raw_g, gblk, wb, raw_bytes);
     return err ? 1u : 0u;
 }
 
@@ -758,6 +761,110 @@ __global__ __launch_bounds__(NTHR, (WPC >= 5 ? 3 : 2)) void rs_pair_decode_kerne
             }
         }
     }
+}
+
+// Resident small-batch server for 16 < 2t <= 32 (server_box.hpp; the 2t <= 8 twin is
+// rs_wg_server_kernel): one 128-thread workgroup, the decode tables in LDS (the XP rows stay in
+// global memory as in the decode kernel), requests of <= 64 blocks from the context's zero-copy
+// buffer.  Decode is the partial-tile path of rs_pair_decode_kernel; encode stages the payloads
+// contiguously (one round trip) and copies them into the codeword image of
+// rs_pair_encode_img_kernel inside LDS.
+template <int T2, bool RM>
+__global__ __launch_bounds__(NTHR, 1) void rs_pair_server_kernel(SrvBox* box, uint8_t* zc, uint64_t zc_bytes,
+    const uint8_t* __restrict__ tables, uint32_t gen, uint32_t idle_us)
+{
+    static_assert(T2 % 16 == 0, "codeword image pieces need 16 | 2t");
+    using L = RsPairLayout<T2>;
+    using D = Lds<T2, true, 1>;
+    constexpr int K = L::K;
+    constexpr int IMG = D::OFF_BUF;           // encode: the codeword image (64 x 255 + 64 <= BUF)
+    constexpr int STG = D::BYTES;             // encode: the payloads as read (64 K bytes)
+    static_assert(img_bytes<TB>() <= BUF && IMG % 16 == 0, "image in the tile buffer");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[STG + TB * K + 16];
+    __shared__ uint32_t s_cmd[2];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
+    const uint32_t c = lane_col(lane), blk = spread_blk<NTHR / 32>(wave, lane);
+    const uint32_t tb = L::OFF_SL + 256u * c;
+    const uint32_t slot = D::OFF_PAR + 32u * blk;
+    for (uint32_t p = tid; p < (uint32_t)D::TBL / 16; p += NTHR)
+        *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t last = t0;
+    uint32_t seen = srv::ld_sys(&box->done), served = 0;
+    if (tid == 0)
+        srv::st_sys(&box->alive, gen);
+    for (;;) {
+        const uint32_t r = srv::next_request(box, seen, last, t0, idle_us, s_cmd);
+        if (r == 0)
+            break;
+        const SrvCmd cmd = srv_cmd_unpack(r);
+        const uint32_t op = cmd.op, nb = cmd.nb;
+        const SrvLayout lay = srv_layout(nb, (uint32_t)K, 255u);
+        uint8_t* data = zc + lay.data;
+        uint8_t* raw = zc + lay.raw;
+        uint8_t* status = zc + lay.status;
+        const bool ok = nb >= 1 && nb <= (uint32_t)TB && PPFS_DBG_OK(data, nb * K, zc, zc_bytes)
+            && PPFS_DBG_OK(raw, nb * 255u, zc, zc_bytes) && PPFS_DBG_OK(status, nb, zc, zc_bytes);
+        if (ok && (op == SRV_DECODE || op == SRV_WRITE)) {
+            const uint32_t buf = D::OFF_BUF;
+            srv::stage_host<NTHR, TB * 255>(lds + buf + PAD, raw, nb * 255u, tid);
+            barrier_lds();
+            const uint32_t row = buf + PAD + 255u * blk;
+            uint32_t s[4];
+            if constexpr (RM)
+                pair_cmodg<T2>(s, lds, row, tb, c);
+            else
+                pair_remainder<255>(s, lds, row, tb, c);
+            *(uint4*)(lds + slot + 16u * c) = make_uint4(s[0], s[1], s[2], s[3]);
+            wave_fence();
+            const bool valid = blk < nb;
+            const uint32_t st = pair_correct<T2, RM, 1>(lds, L::OFF_GF, tables + (RM ? L::OFF_XPM : L::OFF_XP), row,
+                slot, c, s, valid, raw, blk, op == SRV_DECODE && cmd.write_back, nb * 255u);
+            if (valid && c == 0)
+                status[blk] = (uint8_t)st;
+            barrier_lds();
+            if (op == SRV_DECODE && cmd.want_data) {
+                const uint32_t nout = nb * (uint32_t)K;
+                for (uint32_t p = tid; 16u * p < nout; p += NTHR) {
+                    const uint4 v = dec_piece<T2>(lds, buf, p);
+                    if (16u * p + 16u <= nout)
+                        *(uint4*)(data + 16u * p) = v;
+                    else
+                        st_bytes(data + 16u * p, v, nout - 16u * p);
+                }
+            }
+            barrier_lds();
+        }
+        if (ok && (op == SRV_ENCODE || op == SRV_WRITE)) {
+            srv::stage_host<NTHR, TB * K + 16>(lds + STG, data, nb * (uint32_t)K, tid);
+            barrier_lds();
+            for (uint32_t j = tid; j < nb * (uint32_t)K; j += NTHR) { // payload b -> image row b
+                const uint32_t b = j / (uint32_t)K;
+                lds[IMG + 255u * b + (uint32_t)T2 + (j - (uint32_t)K * b)] = lds[STG + j];
+            }
+            barrier_lds();
+            uint32_t s[4];
+            pair_remainder<K>(s, lds, IMG + 255u * blk + (uint32_t)T2, tb, c);
+            uint8_t* const gap = lds + IMG + 255u * blk + 16u * c; // this lane's 16 parity bytes
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                gap[k] = (uint8_t)(s[k >> 2] >> (8 * (k & 3)));
+            barrier_lds();
+            const uint32_t nout = nb * 255u;
+            for (uint32_t i = tid; 16u * i < nout; i += NTHR) {
+                const uint4 v = ld16(lds, IMG + 16u * i);
+                if (16u * i + 16u <= nout)
+                    *(uint4*)(raw + 16u * i) = v;
+                else
+                    st_bytes(raw + 16u * i, v, nout - 16u * i);
+            }
+            barrier_lds();
+        }
+        seen = r;
+        srv::finish_request(box, r, ++served);
+    }
+    if (tid == 0)
+        srv::st_sys(&box->alive, gen | SRV_EXITED);
 }
 
 } // namespace pair

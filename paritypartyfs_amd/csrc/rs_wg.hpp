@@ -30,7 +30,7 @@
 #include "gf_common.hpp"
 #include "rs_fast.hpp"
 #include "rs_layout.hpp"
-#include "server_box.hpp"
+#include "srv_device.hpp"
 
 namespace ppfs {
 namespace wg {
@@ -910,44 +910,6 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_kernel(uint8_t* __restr
 // zero-copy buffer.  A request costs two PCIe round trips instead of a kernel launch and a stream
 // synchronize.  The tile work is the partial-tile path of the kernels above.
 // ------------------------------------------------------------------------------------
-// relaxed system-scope loads bypass the caches without invalidating them (an acquire load would
-// invalidate the L2 on every poll, under whatever else runs on the XCD); one acquire fence follows
-// a new request
-__device__ __forceinline__ uint32_t ld_sys(const uint32_t* p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ uint64_t ld_sys64(const void* p)
-{
-    return __hip_atomic_load((const uint64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// nbytes (<= one tile of codewords) from host-coherent memory (16-byte aligned src, readable up to
-// the next 16 bytes) into LDS: every thread's loads are issued before any is waited for, so the
-// tile costs one PCIe round trip
-__device__ __forceinline__ void stage_host(uint8_t* dst, const uint8_t* __restrict__ src, uint32_t nbytes, uint32_t tid)
-{
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4))); // (a uint4 array went to scratch)
-    constexpr int KP = (TB * 255 / 16 + NTHR - 1) / NTHR; // 4
-    u32x4 v[KP];
-    const uint32_t plast = (nbytes - 1u) / 16u; // loads are unconditional (a branch per load made the
-#pragma unroll                                  // compiler wait for each one): past the end, re-read the last piece
-    for (int k = 0; k < KP; ++k) {
-        const uint32_t p = tid + (uint32_t)NTHR * k;
-        v[k] = *(const u32x4*)(src + 16u * min(p, plast));
-    }
-#pragma unroll
-    for (int k = 0; k < KP; ++k) {
-        const uint32_t p = tid + (uint32_t)NTHR * k;
-        if (16u * p < nbytes)
-            *(u32x4*)(dst + 16u * p) = v[k];
-    }
-}
-
 template <int T2>
 __global__ __launch_bounds__(256, 1) void rs_wg_server_kernel(SrvBox* box, uint8_t* zc, uint64_t zc_bytes,
     const uint8_t* __restrict__ tables, uint32_t gen, uint32_t idle_us)
@@ -962,42 +924,17 @@ __global__ __launch_bounds__(256, 1) void rs_wg_server_kernel(SrvBox* box, uint8
     const uint32_t buf = D::OFF_BUF, par = D::OFF_PAR;
     for (uint32_t p = tid; p < (uint32_t)D::TBL / 16; p += NTHR)
         *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime(); // 100 MHz (lane 0's timers)
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint64_t last = t0;
-    uint32_t seen = ld_sys(&box->done), served = 0;
+    uint32_t seen = srv::ld_sys(&box->done), served = 0;
     if (tid == 0)
-        st_sys(&box->alive, gen);
+        srv::st_sys(&box->alive, gen);
     for (;;) {
-        if (tid == 0) {
-            // poll ~50 us (s_sleep 2: ~128 clocks) between timer checks; cmd and stop in one load
-            uint64_t w = 0;
-            bool take = false, stop = false;
-            for (int spin = 0; spin < 512; ++spin) {
-                w = ld_sys64(box);
-                take = (uint32_t)w != seen;
-                stop = (w >> 32) != 0;
-                if (take || stop)
-                    break;
-                __builtin_amdgcn_s_sleep(2);
-            }
-            const uint64_t now = __builtin_amdgcn_s_memrealtime();
-            if (take)
-                last = now;
-            s_cmd[0] = take ? (uint32_t)w : seen;
-            s_cmd[1] = stop || (!take && (now - last > 100ull * idle_us || now - t0 > 100ull * SRV_LIFETIME_US));
-        }
-        __syncthreads();
-        const uint32_t r = s_cmd[0];
-        if (s_cmd[1])
+        const uint32_t r = srv::next_request(box, seen, last, t0, idle_us, s_cmd);
+        if (r == 0)
             break;
-        if (r == seen) {
-            __syncthreads(); // s_cmd is rewritten only after every wave has read it
-            continue;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // the request's input bytes, written before cmd
         const SrvCmd cmd = srv_cmd_unpack(r);
         const uint32_t op = cmd.op, nb = cmd.nb;
-        const bool wb = cmd.write_back;
         const SrvLayout lay = srv_layout(nb, (uint32_t)K, 255u);
         uint8_t* data = zc + lay.data;
         uint8_t* raw = zc + lay.raw;
@@ -1007,13 +944,14 @@ __global__ __launch_bounds__(256, 1) void rs_wg_server_kernel(SrvBox* box, uint8
         if (ok && (op == SRV_DECODE || op == SRV_WRITE)) {
             if (wave == 0)
                 *(uint64_t*)(lds + par + 8u * lane) = 0;
-            stage_host(lds + buf + PAD, raw, nb * 255u, tid);
+            srv::stage_host<NTHR, TB * 255>(lds + buf + PAD, raw, nb * 255u, tid);
             barrier_lds();
             phase_remainder<T2, 255>(lds, buf, par, wave, row);
             barrier_lds();
             if (wave == 0) {
                 const bool valid = row < nb;
-                const uint32_t st = phase_correct<T2>(lds, buf, par, row, valid, raw, row, op == SRV_DECODE && wb, nb * 255u);
+                const uint32_t st = phase_correct<T2>(lds, buf, par, row, valid, raw, row, op == SRV_DECODE && cmd.write_back,
+                    nb * 255u);
                 if (valid)
                     status[row] = (uint8_t)st;
             }
@@ -1033,7 +971,7 @@ __global__ __launch_bounds__(256, 1) void rs_wg_server_kernel(SrvBox* box, uint8
         if (ok && (op == SRV_ENCODE || op == SRV_WRITE)) {
             if (wave == 0)
                 *(uint64_t*)(lds + par + 8u * lane) = 0;
-            stage_host(lds + buf + PAD, data, nb * (uint32_t)K, tid);
+            srv::stage_host<NTHR, TB * 255>(lds + buf + PAD, data, nb * (uint32_t)K, tid);
             barrier_lds();
             phase_remainder<T2, K>(lds, buf, par, wave, row);
             barrier_lds();
@@ -1047,17 +985,11 @@ __global__ __launch_bounds__(256, 1) void rs_wg_server_kernel(SrvBox* box, uint8
             }
             barrier_lds();
         }
-        __threadfence_system(); // this thread's outputs are visible to the host
-        __syncthreads();
         seen = r;
-        ++served;
-        if (tid == 0) {
-            __hip_atomic_store(&box->served, (uint64_t)served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            st_sys(&box->done, r);
-        }
+        srv::finish_request(box, r, ++served);
     }
     if (tid == 0)
-        st_sys(&box->alive, gen | SRV_EXITED);
+        srv::st_sys(&box->alive, gen | SRV_EXITED);
 }
 
 } // namespace wg

@@ -1,5 +1,5 @@
 """GPU tests of the resident small-batch server (api.cpp server_call, rs_wg.hpp rs_wg_server_kernel):
-the per-block readBlock / writeBlock calls of RS with 2t <= 8 (batches of <= 64 blocks through
+the per-block readBlock / writeBlock calls of RS with 2t <= 8 or 2t = 32 (batches of <= 64 blocks through
 the host entry points) are served by one resident workgroup polling a mailbox in host-coherent
 memory.  Every result is compared with the oracle (rs_block_device.cpp semantics: payload,
 status, written-back codeword bytes) and with the launch path (PPFS_ECC_SERVER=0); the server is
@@ -19,7 +19,8 @@ pytestmark = pytest.mark.gpu
 
 from paritypartyfs_amd import ECC_REED_SOLOMON, EccEngine
 
-SERVER_CASES = [(512, 3), (255, 1), (255, 2), (256, 4)]  # the 2t <= 8 fast path (n = 255)
+# the 2t <= 8 segment path and the 2t = 32 pair path (n = 255)
+SERVER_CASES = [(512, 3), (255, 1), (255, 2), (256, 4), (256, 16), (4096, 16)]
 
 
 def rng_for(*k):
@@ -82,8 +83,9 @@ def test_server_encode_decode_write_match_oracle(oracle, bs, t, nb):
     eng.close()
 
 
-def test_server_equals_launch_path(oracle):
-    bs, t, nb = 512, 3, 40
+@pytest.mark.parametrize("bs,t", [(512, 3), (256, 16)], ids=lambda x: str(x))
+def test_server_equals_launch_path(oracle, bs, t):
+    nb = 40
     a, b = engine(bs, t, server=True), engine(bs, t, server=False)
     n, k, _ = oracle.rs_sizes(bs, t)
     rng = rng_for("srv-vs-launch")
