@@ -18,6 +18,7 @@
 #include <stdint.h>
 
 #include "dbg.hpp"
+#include "srv_device.hpp"
 #include "gf_common.hpp"
 
 namespace ppfs {
@@ -197,16 +198,14 @@ __device__ __forceinline__ uint64_t crc_read_field(const uint8_t* blk, const Crc
 }
 
 // encode: raw[i] <- data[i] ++ CRC bits (+ old tail bits); skip blocks whose status is 5
-__global__ __launch_bounds__(256) void crc_encode_kernel(const uint8_t* __restrict__ data, uint8_t* __restrict__ raw,
-    const uint8_t* __restrict__ skip, uint64_t nblocks, CrcArgs a, const uint8_t* __restrict__ tables)
+// per-wave body of crc_encode_kernel (also run by bit_server_kernel): blocks first, first + stride, ...
+__device__ __forceinline__ void crc_encode_blocks(const uint8_t* __restrict__ data, uint8_t* __restrict__ raw,
+    const uint8_t* __restrict__ skip, uint64_t nblocks, CrcArgs a, const uint8_t* __restrict__ tables,
+    uint8_t* lds, uint64_t first, uint64_t stride)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[CRC_TBL_BYTES + BK_WAVES * BK_BUF];
-    for (uint32_t p = threadIdx.x; p < CRC_TBL_BYTES / 16; p += 256)
-        *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
-    __syncthreads();
     const uint32_t lane = lane_id(), wave = wave_id();
     uint8_t* buf = lds + CRC_TBL_BYTES + wave * BK_BUF;
-    for (uint64_t blk = (uint64_t)blockIdx.x * BK_WAVES + wave; blk < nblocks; blk += (uint64_t)gridDim.x * BK_WAVES) {
+    for (uint64_t blk = first; blk < nblocks; blk += stride) {
         if (!PPFS_DBG_OK(data + blk * a.ds, a.ds, data, nblocks * a.ds) || !PPFS_DBG_OK(raw + blk * a.bs, a.bs, raw, nblocks * a.bs)
             || (skip && !PPFS_DBG_OK(skip + blk, 1, skip, nblocks)))
             continue; // PPFS_ECC_DEBUG: the block's rows (wave_g2l may also read the aligned dword holding a row's first byte)
@@ -237,17 +236,26 @@ __global__ __launch_bounds__(256) void crc_encode_kernel(const uint8_t* __restri
     }
 }
 
-// check: status 0 / 5; optional payload copy
-__global__ __launch_bounds__(256) void crc_check_kernel(const uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
-    uint8_t* __restrict__ status, uint64_t nblocks, CrcArgs a, const uint8_t* __restrict__ tables)
+__global__ __launch_bounds__(256) void crc_encode_kernel(const uint8_t* __restrict__ data, uint8_t* __restrict__ raw,
+    const uint8_t* __restrict__ skip, uint64_t nblocks, CrcArgs a, const uint8_t* __restrict__ tables)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[CRC_TBL_BYTES + BK_WAVES * BK_BUF];
     for (uint32_t p = threadIdx.x; p < CRC_TBL_BYTES / 16; p += 256)
         *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
     __syncthreads();
+    crc_encode_blocks(data, raw, skip, nblocks, a, tables, lds, (uint64_t)blockIdx.x * BK_WAVES + wave_id(),
+        (uint64_t)gridDim.x * BK_WAVES);
+}
+
+// check: status 0 / 5; optional payload copy
+// per-wave body of crc_check_kernel (also run by bit_server_kernel): blocks first, first + stride, ...
+__device__ __forceinline__ void crc_check_blocks(const uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
+    uint8_t* __restrict__ status, uint64_t nblocks, CrcArgs a, const uint8_t* __restrict__ tables,
+    uint8_t* lds, uint64_t first, uint64_t stride)
+{
     const uint32_t lane = lane_id(), wave = wave_id();
     uint8_t* buf = lds + CRC_TBL_BYTES + wave * BK_BUF;
-    for (uint64_t blk = (uint64_t)blockIdx.x * BK_WAVES + wave; blk < nblocks; blk += (uint64_t)gridDim.x * BK_WAVES) {
+    for (uint64_t blk = first; blk < nblocks; blk += stride) {
         const uint8_t* rb = raw + blk * a.bs;
         if (!PPFS_DBG_OK(rb, a.bs, raw, nblocks * a.bs) || (data && !PPFS_DBG_OK(data + blk * a.ds, a.ds, data, nblocks * a.ds))
             || (status && !PPFS_DBG_OK(status + blk, 1, status, nblocks)))
@@ -266,6 +274,17 @@ __global__ __launch_bounds__(256) void crc_check_kernel(const uint8_t* __restric
             status[blk] = (st == field) ? 0 : 5;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
+}
+
+__global__ __launch_bounds__(256) void crc_check_kernel(const uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
+    uint8_t* __restrict__ status, uint64_t nblocks, CrcArgs a, const uint8_t* __restrict__ tables)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[CRC_TBL_BYTES + BK_WAVES * BK_BUF];
+    for (uint32_t p = threadIdx.x; p < CRC_TBL_BYTES / 16; p += 256)
+        *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
+    __syncthreads();
+    crc_check_blocks(raw, data, status, nblocks, a, tables, lds, (uint64_t)blockIdx.x * BK_WAVES + wave_id(),
+        (uint64_t)gridDim.x * BK_WAVES);
 }
 
 // ------------------------------------------------------------------------------------
@@ -358,14 +377,15 @@ __device__ __forceinline__ uint32_t ham_place_word(const uint8_t* dbuf, uint32_t
 }
 
 // encode: per lane 16 raw words (64 B); tail bits from the old raw block
-__global__ __launch_bounds__(256) void ham_encode_kernel(const uint8_t* __restrict__ data, uint8_t* __restrict__ raw,
-    const uint8_t* __restrict__ skip, uint64_t nblocks, HamArgs a)
+// per-wave body of ham_encode_kernel (also run by bit_server_kernel): blocks first, first + stride, ...
+__device__ __forceinline__ void ham_encode_blocks(const uint8_t* __restrict__ data, uint8_t* __restrict__ raw,
+    const uint8_t* __restrict__ skip, uint64_t nblocks, HamArgs a,
+    uint8_t* lds, uint64_t first, uint64_t stride)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[BK_WAVES * BK_BUF];
     const uint32_t lane = lane_id(), wave = wave_id();
     uint8_t* buf = lds + wave * BK_BUF;
     const uint32_t nwords = a.bits / 32;
-    for (uint64_t blk = (uint64_t)blockIdx.x * BK_WAVES + wave; blk < nblocks; blk += (uint64_t)gridDim.x * BK_WAVES) {
+    for (uint64_t blk = first; blk < nblocks; blk += stride) {
         if (!PPFS_DBG_OK(data + blk * a.ds, a.ds, data, nblocks * a.ds) || !PPFS_DBG_OK(raw + blk * a.bs, a.bs, raw, nblocks * a.bs)
             || (skip && !PPFS_DBG_OK(skip + blk, 1, skip, nblocks)))
             continue;
@@ -433,15 +453,24 @@ __global__ __launch_bounds__(256) void ham_encode_kernel(const uint8_t* __restri
     }
 }
 
-// decode: status 0/1/5, one-byte write-back, payload extraction
-__global__ __launch_bounds__(256) void ham_decode_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
-    uint8_t* __restrict__ status, uint64_t nblocks, int write_back, HamArgs a)
+__global__ __launch_bounds__(256) void ham_encode_kernel(const uint8_t* __restrict__ data, uint8_t* __restrict__ raw,
+    const uint8_t* __restrict__ skip, uint64_t nblocks, HamArgs a)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[BK_WAVES * BK_BUF];
+    ham_encode_blocks(data, raw, skip, nblocks, a, lds, (uint64_t)blockIdx.x * BK_WAVES + wave_id(),
+        (uint64_t)gridDim.x * BK_WAVES);
+}
+
+// decode: status 0/1/5, one-byte write-back, payload extraction
+// per-wave body of ham_decode_kernel (also run by bit_server_kernel): blocks first, first + stride, ...
+__device__ __forceinline__ void ham_decode_blocks(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
+    uint8_t* __restrict__ status, uint64_t nblocks, int write_back, HamArgs a,
+    uint8_t* lds, uint64_t first, uint64_t stride)
+{
     const uint32_t lane = lane_id(), wave = wave_id();
     uint8_t* buf = lds + wave * BK_BUF;
     const uint32_t nwords = a.bits / 32;
-    for (uint64_t blk = (uint64_t)blockIdx.x * BK_WAVES + wave; blk < nblocks; blk += (uint64_t)gridDim.x * BK_WAVES) {
+    for (uint64_t blk = first; blk < nblocks; blk += stride) {
         uint8_t* rb = raw + blk * a.bs;
         if (!PPFS_DBG_OK(rb, a.bs, raw, nblocks * a.bs) || (data && !PPFS_DBG_OK(data + blk * a.ds, a.ds, data, nblocks * a.ds))
             || (status && !PPFS_DBG_OK(status + blk, 1, status, nblocks)))
@@ -548,17 +577,26 @@ __global__ __launch_bounds__(256) void ham_decode_kernel(uint8_t* __restrict__ r
     }
 }
 
+__global__ __launch_bounds__(256) void ham_decode_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
+    uint8_t* __restrict__ status, uint64_t nblocks, int write_back, HamArgs a)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[BK_WAVES * BK_BUF];
+    ham_decode_blocks(raw, data, status, nblocks, write_back, a, lds, (uint64_t)blockIdx.x * BK_WAVES + wave_id(),
+        (uint64_t)gridDim.x * BK_WAVES);
+}
+
 // ------------------------------------------------------------------------------------
 // Parity (even parity over the whole raw block; the LSB of the last byte is the fix bit)
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void parity_encode_kernel(const uint8_t* __restrict__ data, uint8_t* __restrict__ raw,
-    const uint8_t* __restrict__ skip, uint64_t nblocks, uint32_t bs)
+// per-wave body of parity_encode_kernel (also run by bit_server_kernel): blocks first, first + stride, ...
+__device__ __forceinline__ void parity_encode_blocks(const uint8_t* __restrict__ data, uint8_t* __restrict__ raw,
+    const uint8_t* __restrict__ skip, uint64_t nblocks, uint32_t bs,
+    uint8_t* lds, uint64_t first, uint64_t stride)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[BK_WAVES * BK_BUF];
     const uint32_t lane = lane_id(), wave = wave_id();
     uint8_t* buf = lds + wave * BK_BUF;
     const uint32_t ds = bs - 1;
-    for (uint64_t blk = (uint64_t)blockIdx.x * BK_WAVES + wave; blk < nblocks; blk += (uint64_t)gridDim.x * BK_WAVES) {
+    for (uint64_t blk = first; blk < nblocks; blk += stride) {
         if (!PPFS_DBG_OK(data + blk * ds, ds, data, nblocks * ds) || !PPFS_DBG_OK(raw + blk * bs, bs, raw, nblocks * bs)
             || (skip && !PPFS_DBG_OK(skip + blk, 1, skip, nblocks)))
             continue;
@@ -580,13 +618,22 @@ __global__ __launch_bounds__(256) void parity_encode_kernel(const uint8_t* __res
     }
 }
 
-__global__ __launch_bounds__(256) void parity_check_kernel(const uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
-    uint8_t* __restrict__ status, uint64_t nblocks, uint32_t bs)
+__global__ __launch_bounds__(256) void parity_encode_kernel(const uint8_t* __restrict__ data, uint8_t* __restrict__ raw,
+    const uint8_t* __restrict__ skip, uint64_t nblocks, uint32_t bs)
 {
     __shared__ __attribute__((aligned(16))) uint8_t lds[BK_WAVES * BK_BUF];
+    parity_encode_blocks(data, raw, skip, nblocks, bs, lds, (uint64_t)blockIdx.x * BK_WAVES + wave_id(),
+        (uint64_t)gridDim.x * BK_WAVES);
+}
+
+// per-wave body of parity_check_kernel (also run by bit_server_kernel): blocks first, first + stride, ...
+__device__ __forceinline__ void parity_check_blocks(const uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
+    uint8_t* __restrict__ status, uint64_t nblocks, uint32_t bs,
+    uint8_t* lds, uint64_t first, uint64_t stride)
+{
     const uint32_t lane = lane_id(), wave = wave_id();
     uint8_t* buf = lds + wave * BK_BUF;
-    for (uint64_t blk = (uint64_t)blockIdx.x * BK_WAVES + wave; blk < nblocks; blk += (uint64_t)gridDim.x * BK_WAVES) {
+    for (uint64_t blk = first; blk < nblocks; blk += stride) {
         const uint8_t* rb = raw + blk * bs;
         if (!PPFS_DBG_OK(rb, bs, raw, nblocks * bs) || (data && !PPFS_DBG_OK(data + blk * (bs - 1), bs - 1, data, nblocks * (bs - 1)))
             || (status && !PPFS_DBG_OK(status + blk, 1, status, nblocks)))
@@ -603,6 +650,90 @@ __global__ __launch_bounds__(256) void parity_check_kernel(const uint8_t* __rest
             wave_l2g(data + blk * (bs - 1), buf, bs - 1, lane);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
+}
+
+__global__ __launch_bounds__(256) void parity_check_kernel(const uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
+    uint8_t* __restrict__ status, uint64_t nblocks, uint32_t bs)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t lds[BK_WAVES * BK_BUF];
+    parity_check_blocks(raw, data, status, nblocks, bs, lds, (uint64_t)blockIdx.x * BK_WAVES + wave_id(),
+        (uint64_t)gridDim.x * BK_WAVES);
+}
+
+// ------------------------------------------------------------------------------------
+// Resident small-batch server for CRC / Hamming / parity (server_box.hpp protocol; the RS twins
+// are rs_wg_server_kernel and rs_pair_server_kernel): one 256-thread workgroup, wave w takes the
+// request's blocks w, w + 4, ... through the per-wave bodies above (every block size: the CRC
+// context always carries these generic tables, the fast ones follow them).  A write is the check
+// (Hamming: decode with write-back) then the encode that skips status-5 blocks, as
+// ppfs_ecc_write_device queues them.
+// ------------------------------------------------------------------------------------
+struct BitSrv {
+    CrcArgs crc;
+    HamArgs ham;
+    uint32_t bs, ds;
+};
+
+template <int CODEC> // PPFS_ECC_CRC 1, PPFS_ECC_HAMMING 2, PPFS_ECC_PARITY 3
+__global__ __launch_bounds__(256, 1) void bit_server_kernel(SrvBox* box, uint8_t* zc, uint64_t zc_bytes, BitSrv a,
+    const uint8_t* __restrict__ tables, uint32_t gen, uint32_t idle_us)
+{
+    constexpr int TBL = CODEC == 1 ? CRC_TBL_BYTES : 0;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[TBL + BK_WAVES * BK_BUF];
+    __shared__ uint32_t s_cmd[2];
+    for (uint32_t p = threadIdx.x; p < (uint32_t)TBL / 16; p += 256)
+        *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
+    const uint64_t w0 = wave_id(), W = BK_WAVES;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t last = t0;
+    uint32_t seen = srv::ld_sys(&box->done), served = 0;
+    if (threadIdx.x == 0)
+        srv::st_sys(&box->alive, gen);
+    for (;;) {
+        const uint32_t r = srv::next_request(box, seen, last, t0, idle_us, s_cmd);
+        if (r == 0)
+            break;
+        const SrvCmd cmd = srv_cmd_unpack(r);
+        const uint32_t nb = cmd.nb;
+        const SrvLayout lay = srv_layout(nb, a.ds, a.bs);
+        uint8_t* data = zc + lay.data;
+        uint8_t* raw = zc + lay.raw;
+        uint8_t* status = zc + lay.status;
+        const bool ok = nb >= 1 && nb <= SRV_MAX_BLOCKS && PPFS_DBG_OK(data, nb * a.ds, zc, zc_bytes)
+            && PPFS_DBG_OK(raw, nb * a.bs, zc, zc_bytes) && PPFS_DBG_OK(status, nb, zc, zc_bytes);
+        uint8_t* want = cmd.want_data ? data : nullptr;
+        if (ok && cmd.op == SRV_DECODE) {
+            if constexpr (CODEC == 1)
+                crc_check_blocks(raw, want, status, nb, a.crc, tables, lds, w0, W);
+            else if constexpr (CODEC == 2)
+                ham_decode_blocks(raw, want, status, nb, cmd.write_back ? 1 : 0, a.ham, lds, w0, W);
+            else
+                parity_check_blocks(raw, want, status, nb, a.bs, lds, w0, W);
+        }
+        if (ok && cmd.op == SRV_WRITE) { // the old blocks' check: status, Hamming's write-back
+            if constexpr (CODEC == 1)
+                crc_check_blocks(raw, nullptr, status, nb, a.crc, tables, lds, w0, W);
+            else if constexpr (CODEC == 2)
+                ham_decode_blocks(raw, nullptr, status, nb, 1, a.ham, lds, w0, W);
+            else
+                parity_check_blocks(raw, nullptr, status, nb, a.bs, lds, w0, W);
+            __threadfence_system(); // status and write-back bytes before the encode reads them
+            __syncthreads();
+        }
+        if (ok && (cmd.op == SRV_ENCODE || cmd.op == SRV_WRITE)) {
+            const uint8_t* skip = cmd.op == SRV_WRITE ? status : nullptr;
+            if constexpr (CODEC == 1)
+                crc_encode_blocks(data, raw, skip, nb, a.crc, tables, lds, w0, W);
+            else if constexpr (CODEC == 2)
+                ham_encode_blocks(data, raw, skip, nb, a.ham, lds, w0, W);
+            else
+                parity_encode_blocks(data, raw, skip, nb, a.bs, lds, w0, W);
+        }
+        seen = r;
+        srv::finish_request(box, r, ++served);
+    }
+    if (threadIdx.x == 0)
+        srv::st_sys(&box->alive, gen | SRV_EXITED);
 }
 
 } // namespace ppfs
@@ -688,6 +819,32 @@ extern "C" hipError_t ppfs_parity_check(const uint8_t* r, uint8_t* d, uint8_t* s
     if (ppfs_bitfast_supported(bs))
         return ppfs_parity_fast_check(r, d, st, nb, bs, s);
     hipLaunchKernelGGL(parity_check_kernel, dim3(bk_grid(nb)), dim3(256), 0, s, r, d, st, nb, bs);
+    return hipGetLastError();
+}
+
+// resident small-batch server for CRC / Hamming / parity contexts (api.cpp server_call)
+extern "C" hipError_t ppfs_bit_server_launch(int ecc_type, uint32_t bs, uint32_t ds, uint32_t crc_n, uint64_t crc_mask,
+    uint32_t ham_L, SrvBox* box, uint8_t* zc, uint64_t zc_bytes, const uint8_t* tab, uint32_t gen, uint32_t idle_us,
+    hipStream_t s)
+{
+    BitSrv a {};
+    a.crc = CrcArgs { bs, ds, crc_n, (ds + 63) / 64, (crc_n + 3) / 4, crc_mask };
+    a.ham = HamArgs { bs, ds, 8 * bs, ham_L };
+    a.bs = bs;
+    a.ds = ds;
+    switch (ecc_type) {
+    case 1:
+        hipLaunchKernelGGL(bit_server_kernel<1>, dim3(1), dim3(256), 0, s, box, zc, zc_bytes, a, tab, gen, idle_us);
+        break;
+    case 2:
+        hipLaunchKernelGGL(bit_server_kernel<2>, dim3(1), dim3(256), 0, s, box, zc, zc_bytes, a, tab, gen, idle_us);
+        break;
+    case 3:
+        hipLaunchKernelGGL(bit_server_kernel<3>, dim3(1), dim3(256), 0, s, box, zc, zc_bytes, a, tab, gen, idle_us);
+        break;
+    default:
+        return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

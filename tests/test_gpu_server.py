@@ -149,3 +149,77 @@ def test_server_large_batches_take_the_chunked_path(oracle):
         eng.encode_host(data, raw)
         assert np.array_equal(raw, oracle.rs_encode(bs, t, data))
     eng.close()
+
+
+# ------------------------------------------------------------------------------------
+# CRC / Hamming / parity (bit_server_kernel)
+# ------------------------------------------------------------------------------------
+from paritypartyfs_amd import ECC_CRC, ECC_HAMMING, ECC_PARITY  # noqa: E402
+
+BIT_CASES = [("crc", 0xea, 256), ("crc", 0x9960034c, 4096), ("crc", 0xc1acf, 512), ("crc", 0x42F0E1EBA9EA3693 >> 1, 1024),
+             ("ham", 0, 256), ("ham", 0, 4096), ("ham", 0, 64), ("par", 0, 256), ("par", 0, 4096), ("par", 0, 2)]
+
+
+def bit_engine(oracle, codec, imp, bs, server=True):
+    old = os.environ.get("PPFS_ECC_SERVER")
+    os.environ["PPFS_ECC_SERVER"] = "1" if server else "0"
+    try:
+        if codec == "crc":
+            eng = EccEngine(ECC_CRC, bs, crc_polynomial_explicit=oracle.crc_explicit(imp))
+        elif codec == "ham":
+            eng = EccEngine(ECC_HAMMING, bs)
+        else:
+            eng = EccEngine(ECC_PARITY, bs)
+        eng.encode_host(np.zeros(eng.data_size, np.uint8), np.zeros(eng.raw_block_size, np.uint8))
+    finally:
+        if old is None:
+            del os.environ["PPFS_ECC_SERVER"]
+        else:
+            os.environ["PPFS_ECC_SERVER"] = old
+    return eng
+
+
+@pytest.mark.parametrize("codec,imp,bs", BIT_CASES, ids=[f"{c}-{bs}" + (f"-{i:x}" if i else "") for c, i, bs in BIT_CASES])
+@pytest.mark.parametrize("nb", [1, 7, 64])
+def test_bit_server_matches_oracle_and_launch_path(oracle, codec, imp, bs, nb):
+    a = bit_engine(oracle, codec, imp, bs, server=True)
+    b = bit_engine(oracle, codec, imp, bs, server=False)
+    n, k = a.raw_block_size, a.data_size
+    rng = rng_for("bitsrv", codec, imp, bs, nb)
+    data = rng.integers(0, 256, nb * k, dtype=np.uint8)
+    old = rng.integers(0, 256, nb * n, dtype=np.uint8)  # old raw contents (tail bits the encode keeps)
+    ra, rb = old.copy(), old.copy()
+    a.encode_host(data, ra)
+    b.encode_host(data, rb)
+    assert np.array_equal(ra, rb)
+    if codec == "crc":
+        P = oracle.crc_explicit(imp)
+        assert np.array_equal(ra, oracle.crc_encode(bs, P, data, raw_old=old))
+    elif codec == "ham":
+        assert np.array_equal(ra, oracle.ham_encode(bs, data, raw_old=old))
+    else:
+        assert np.array_equal(ra, oracle.parity_encode(bs, data, raw_old=old))
+    # corrupt: 0..2 bit flips per block
+    bad = ra.copy().reshape(nb, n)
+    for blk in range(nb):
+        for f in rng.choice(n * 8, blk % 3, replace=False):
+            bad[blk, f // 8] ^= 0x80 >> (f % 8)
+    bad = bad.reshape(-1)
+    for wb in (True, False):
+        outs = []
+        for e in (a, b):
+            img, out, st = bad.copy(), np.zeros(nb * k, np.uint8), np.full(nb, 77, np.uint8)
+            e.decode_host(img, out, st, write_back=wb)
+            outs.append((img, out, st))
+        (ia, oa, sa), (ib, ob, sb) = outs
+        assert np.array_equal(sa, sb) and np.array_equal(ia, ib)
+        ok = sa != 5  # payloads are defined where the block was not rejected
+        assert np.array_equal(oa.reshape(nb, k)[ok], ob.reshape(nb, k)[ok])
+    new = rng.integers(0, 256, nb * k, dtype=np.uint8)
+    wa, wb_ = bad.copy(), bad.copy()
+    sa, sb = np.full(nb, 77, np.uint8), np.full(nb, 77, np.uint8)
+    a.write_host(new, wa, sa)
+    b.write_host(new, wb_, sb)
+    assert np.array_equal(sa, sb) and np.array_equal(wa, wb_)
+    a.close()
+    b.close()
