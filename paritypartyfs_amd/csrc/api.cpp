@@ -32,6 +32,8 @@ int ppfs_rs_fast_supported(int n, int t2);
 int ppfs_rs_fast_tables_bytes(int t2);
 hipError_t ppfs_rs_fast_encode(int t2, const uint8_t* d, uint8_t* r, uint64_t nb, const uint8_t* tab, hipStream_t s);
 hipError_t ppfs_flag_launch(uint32_t* flag, uint32_t v, hipStream_t s);
+hipError_t ppfs_rs_generic_server_launch(int n, int t2, ppfs::SrvBox* box, uint8_t* zc, uint64_t zc_bytes,
+    const uint8_t* tab, uint32_t gen, uint32_t idle_us, hipStream_t s);
 hipError_t ppfs_bit_server_launch(int ecc_type, uint32_t bs, uint32_t ds, uint32_t crc_n, uint64_t crc_mask, uint32_t ham_L,
     ppfs::SrvBox* box, uint8_t* zc, uint64_t zc_bytes, const uint8_t* tab, uint32_t gen, uint32_t idle_us, hipStream_t s);
 hipError_t ppfs_rs_server_launch(int t2, ppfs::SrvBox* box, uint8_t* zc, uint64_t zc_bytes, const uint8_t* tab,
@@ -965,7 +967,8 @@ static int device_op(ppfs_ecc_ctx* c, HostOp op, uint8_t* d, const Layout& L, si
 constexpr size_t kSmallBlocks = 64; // one tile: the per-block IBlockDevice calls
 
 // ---- resident small-batch server (server_box.hpp, rs_wg.hpp rs_wg_server_kernel) ----
-// RS with 2t <= 8 or 2t = 32 (rs_wg / rs_pair servers), CRC, Hamming, parity (bit_server_kernel):
+// every codec (RS: rs_wg / rs255 / rs_pair / generic servers by table layout; CRC, Hamming, parity:
+// bit_server_kernel):
 // a per-block call posts its request to the resident
 // workgroup instead of launching kernels and synchronizing a stream (measured on the box, RS(255,249),
 // one block: launch + stream synchronize alone 10.3 us, a whole decode_host call 16.2 us).
@@ -977,7 +980,8 @@ static bool server_eligible(ppfs_ecc_ctx* c)
     if (c->srv_ok < 0) {
         const char* e = std::getenv("PPFS_ECC_SERVER");
         const bool off = e && e[0] == '0';
-        const bool rs = c->p.ecc_type == PPFS_ECC_REED_SOLOMON && c->rs_fast && (c->rs_t2 <= 8 || c->rs_t2 == 32);
+        const bool rs = c->p.ecc_type == PPFS_ECC_REED_SOLOMON
+            && (!c->rs_fast || c->rs_t2 <= 8 || c->rs_t2 == 10 || c->rs_t2 == 16 || c->rs_t2 == 32);
         const bool bit = c->p.ecc_type == PPFS_ECC_CRC || c->p.ecc_type == PPFS_ECC_HAMMING
             || c->p.ecc_type == PPFS_ECC_PARITY;
         c->srv_ok = (!off && (rs || bit)) ? 1 : 0;
@@ -1001,8 +1005,12 @@ static int server_launch(ppfs_ecc_ctx* c)
     const uint32_t gen = (++c->srv_gen) & ~ppfs::SRV_EXITED;
     c->srv_gen = gen;
     __atomic_store_n(&c->h_box->stop, 0u, __ATOMIC_RELEASE);
-    if (c->p.ecc_type == PPFS_ECC_REED_SOLOMON)
+    if (c->p.ecc_type == PPFS_ECC_REED_SOLOMON && c->rs_fast)
         HIP_TRY(ppfs_rs_server_launch(c->rs_t2, c->d_box, c->d_zc, c->zc_bytes, c->d_tables, gen, kSrvIdleUs, c->srv_stream),
+            "server launch");
+    else if (c->p.ecc_type == PPFS_ECC_REED_SOLOMON)
+        HIP_TRY(ppfs_rs_generic_server_launch(c->rs_n, c->rs_t2, c->d_box, c->d_zc, c->zc_bytes, c->d_tables, gen, kSrvIdleUs,
+                    c->srv_stream),
             "server launch");
     else
         HIP_TRY(ppfs_bit_server_launch((int)c->p.ecc_type, c->raw, c->data, (uint32_t)c->crc_n, c->crc_mask, c->ham_L, c->d_box,

@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include "dbg.hpp"
+#include "srv_device.hpp"
 #include <stdint.h>
 
 #include "gf_common.hpp"
@@ -1077,6 +1078,66 @@ __global__ __launch_bounds__(256, 2) void rs255_decode_kernel(uint8_t* __restric
         if (status)
             wave_stage_out(status + b0, st_lds, nb, lane);
     }
+}
+
+// Resident small-batch server for 8 < 2t <= 16 (server_box.hpp protocol): one wave runs a request
+// of <= 64 blocks as the partial-tile path of the kernels above (lane = block).  A write is the
+// old blocks' decode for their status, then the encode.
+template <int T2, int NS = 0>
+__global__ __launch_bounds__(64, 1) void rs255_server_kernel(SrvBox* box, uint8_t* zc, uint64_t zc_bytes,
+    const uint8_t* __restrict__ tables, uint32_t gen, uint32_t idle_us)
+{
+    using Cf = RsCfg<T2, NS>;
+    constexpr int K = Cf::K;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[Cf::OFF_WAVES + Cf::WAVE_BYTES];
+    __shared__ uint32_t s_cmd[2];
+    load_tables(lds, tables, Cf::TBL_BYTES + GF_BYTES);
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    uint8_t* tile = lds + Cf::OFF_WAVES;
+    uint8_t* st_lds = tile + Cf::WAVE_BUF;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t last = t0;
+    uint32_t seen = srv::ld_sys(&box->done), served = 0;
+    if (lane == 0)
+        srv::st_sys(&box->alive, gen);
+    for (;;) {
+        const uint32_t r = srv::next_request(box, seen, last, t0, idle_us, s_cmd);
+        if (r == 0)
+            break;
+        const SrvCmd cmd = srv_cmd_unpack(r);
+        const uint32_t nb = cmd.nb;
+        const SrvLayout lay = srv_layout(nb, (uint32_t)K, (uint32_t)RS_N);
+        uint8_t* data = zc + lay.data;
+        uint8_t* raw = zc + lay.raw;
+        uint8_t* status = zc + lay.status;
+        const bool ok = nb >= 1 && nb <= (uint32_t)RS_WT && PPFS_DBG_OK(data, nb * K, zc, zc_bytes)
+            && PPFS_DBG_OK(raw, nb * RS_N, zc, zc_bytes) && PPFS_DBG_OK(status, nb, zc, zc_bytes);
+        if (ok && (cmd.op == SRV_DECODE || cmd.op == SRV_WRITE)) {
+            const bool dec = cmd.op == SRV_DECODE, want = dec && cmd.want_data;
+            wave_stage_in(tile, raw, nb * RS_N, lane);
+            wave_fence();
+            rs_decode_lane<T2, NS>(tile, lds, lane, lane < nb, raw, lane, dec && cmd.write_back, want, st_lds, []() {},
+                nb * RS_N);
+            wave_fence();
+            if (want)
+                wave_stage_out(data, tile, nb * K, lane);
+            wave_stage_out(status, st_lds, nb, lane);
+            wave_fence();
+        }
+        if (ok && (cmd.op == SRV_ENCODE || cmd.op == SRV_WRITE)) {
+            wave_stage_in(tile, data, nb * K, lane);
+            wave_fence();
+            rs_encode_lane<T2, NS>(tile, lds, lane, []() {});
+            wave_fence();
+            wave_stage_out(raw, tile, nb * RS_N, lane);
+            wave_fence();
+        }
+        seen = r;
+        srv::finish_request(box, r, ++served);
+    }
+    if (lane == 0)
+        srv::st_sys(&box->alive, gen | SRV_EXITED);
 }
 
 } // namespace ppfs

@@ -231,6 +231,14 @@ PPFS_DBG_ACCESSOR(PPFS_CAT(ppfs_dbg_faults_rs_t, PPFS_T2))
 
 // resident small-batch servers (api.cpp server_call): 2t <= 8 rs_wg.hpp rs_wg_server_kernel,
 // 2t > 16 rs_pair.hpp rs_pair_server_kernel
+#if PPFS_T2 > 8 && PPFS_T2 <= 16
+extern "C" hipError_t PPFS_CAT(ppfs_rs_server_launch_t, PPFS_T2)(ppfs::SrvBox* box, uint8_t* zc, uint64_t zc_bytes,
+    const uint8_t* tab, uint32_t gen, uint32_t idle_us, hipStream_t s)
+{
+    hipLaunchKernelGGL((rs255_server_kernel<PPFS_T2>), dim3(1), dim3(64), 0, s, box, zc, zc_bytes, tab, gen, idle_us);
+    return hipGetLastError();
+}
+#endif
 #if PPFS_T2 > 16
 extern "C" hipError_t PPFS_CAT(ppfs_rs_server_launch_t, PPFS_T2)(ppfs::SrvBox* box, uint8_t* zc, uint64_t zc_bytes,
     const uint8_t* tab, uint32_t gen, uint32_t idle_us, hipStream_t s)

@@ -6,7 +6,7 @@
 #include "dbg.hpp"
 #include "gf_common.hpp"
 #include "rs_layout.hpp"
-#include "server_box.hpp"
+#include "srv_device.hpp"
 
 namespace ppfs {
 
@@ -30,12 +30,10 @@ struct GfG {
 };
 
 // tables layout for the generic path: gf block (1 KiB) then generator g[0..2t] (256 B)
-__global__ __launch_bounds__(256) void rs_generic_encode_kernel(const uint8_t* __restrict__ data,
-    uint8_t* __restrict__ raw, uint64_t nblocks, int n, int t2, const uint8_t* __restrict__ tables)
+// one block per thread (the kernel below and rs_generic_server_kernel)
+__device__ __forceinline__ void rs_generic_encode_one(const uint8_t* __restrict__ data, uint8_t* __restrict__ raw,
+    uint64_t blk, uint64_t nblocks, int n, int t2, const uint8_t* __restrict__ tables)
 {
-    const uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (blk >= nblocks)
-        return;
     const GfG gf { tables };
     const uint8_t* g = tables + GF_BYTES;
     const int k = n - t2;
@@ -59,13 +57,18 @@ __global__ __launch_bounds__(256) void rs_generic_encode_kernel(const uint8_t* _
         o[t2 + j] = d[j];
 }
 
-__global__ __launch_bounds__(64) void rs_generic_decode_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
-    uint8_t* __restrict__ status, uint8_t* __restrict__ spill, uint64_t nblocks, int n, int t2, int write_back,
-    const uint8_t* __restrict__ tables)
+__global__ __launch_bounds__(256) void rs_generic_encode_kernel(const uint8_t* __restrict__ data,
+    uint8_t* __restrict__ raw, uint64_t nblocks, int n, int t2, const uint8_t* __restrict__ tables)
 {
     const uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (blk >= nblocks)
-        return;
+    if (blk < nblocks)
+        rs_generic_encode_one(data, raw, blk, nblocks, n, t2, tables);
+}
+
+__device__ __forceinline__ void rs_generic_decode_one(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
+    uint8_t* __restrict__ status, uint8_t* __restrict__ spill, uint64_t blk, uint64_t nblocks, int n, int t2,
+    int write_back, const uint8_t* __restrict__ tables)
+{
     const GfG gf { tables };
     const int k = n - t2;
     uint8_t* c = raw + blk * (uint64_t)n;
@@ -178,6 +181,57 @@ __global__ __launch_bounds__(64) void rs_generic_decode_kernel(uint8_t* __restri
     }
 }
 
+__global__ __launch_bounds__(64) void rs_generic_decode_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
+    uint8_t* __restrict__ status, uint8_t* __restrict__ spill, uint64_t nblocks, int n, int t2, int write_back,
+    const uint8_t* __restrict__ tables)
+{
+    const uint64_t blk = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (blk < nblocks)
+        rs_generic_decode_one(raw, data, status, spill, blk, nblocks, n, t2, write_back, tables);
+}
+
+// Resident small-batch server for the generic RS path (shortened codes, parity lengths without a
+// fast instantiation; server_box.hpp protocol): one 64-thread workgroup, thread b takes block b of
+// a request, requests without spill only (a shortened code's write-back past the block end goes
+// through the launch path).  A write is the old block's decode for its status, then the encode.
+__global__ __launch_bounds__(64, 1) void rs_generic_server_kernel(SrvBox* box, uint8_t* zc, uint64_t zc_bytes, int n,
+    int t2, const uint8_t* __restrict__ tables, uint32_t gen, uint32_t idle_us)
+{
+    __shared__ uint32_t s_cmd[2];
+    const uint32_t k = (uint32_t)(n - t2);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t last = t0;
+    uint32_t seen = srv::ld_sys(&box->done), served = 0;
+    if (threadIdx.x == 0)
+        srv::st_sys(&box->alive, gen);
+    for (;;) {
+        const uint32_t r = srv::next_request(box, seen, last, t0, idle_us, s_cmd);
+        if (r == 0)
+            break;
+        const SrvCmd cmd = srv_cmd_unpack(r);
+        const uint32_t nb = cmd.nb, b = threadIdx.x;
+        const SrvLayout lay = srv_layout(nb, k, (uint32_t)n);
+        uint8_t* data = zc + lay.data;
+        uint8_t* raw = zc + lay.raw;
+        uint8_t* status = zc + lay.status;
+        const bool ok = nb >= 1 && nb <= SRV_MAX_BLOCKS && PPFS_DBG_OK(data, nb * k, zc, zc_bytes)
+            && PPFS_DBG_OK(raw, nb * (uint32_t)n, zc, zc_bytes) && PPFS_DBG_OK(status, nb, zc, zc_bytes);
+        if (ok && b < nb) {
+            if (cmd.op == SRV_DECODE)
+                rs_generic_decode_one(raw, cmd.want_data ? data : nullptr, status, nullptr, b, nb, n, t2,
+                    cmd.write_back ? 1 : 0, tables);
+            if (cmd.op == SRV_WRITE) // the old block's status only (rs_block_device.cpp:61-93)
+                rs_generic_decode_one(raw, nullptr, status, nullptr, b, nb, n, t2, 0, tables);
+            if (cmd.op == SRV_ENCODE || cmd.op == SRV_WRITE)
+                rs_generic_encode_one(data, raw, b, nb, n, t2, tables);
+        }
+        seen = r;
+        srv::finish_request(box, r, ++served);
+    }
+    if (threadIdx.x == 0)
+        srv::st_sys(&box->alive, gen | SRV_EXITED);
+}
+
 } // namespace ppfs
 
 using namespace ppfs;
@@ -243,8 +297,8 @@ extern "C" hipError_t ppfs_rs_fast_decode(int t2, uint8_t* r, uint8_t* d, uint8_
     }
 }
 
-// resident small-batch servers (2t <= 8: segment-layout tables; 2t = 32: pair layout)
-#define PPFS_RS_SERVER_CASES(X) X(2) X(4) X(6) X(8) X(32)
+// resident small-batch servers (2t <= 8: segment-layout tables; 10, 16: lane-per-block; 32: pair layout)
+#define PPFS_RS_SERVER_CASES(X) X(2) X(4) X(6) X(8) X(10) X(16) X(32)
 #define X(T)                                                                                                           \
     extern "C" hipError_t ppfs_rs_server_launch_t##T(ppfs::SrvBox*, uint8_t*, uint64_t, const uint8_t*, uint32_t,      \
         uint32_t, hipStream_t);
@@ -262,6 +316,13 @@ extern "C" hipError_t ppfs_rs_server_launch(int t2, ppfs::SrvBox* box, uint8_t* 
     default:
         return hipErrorInvalidValue;
     }
+}
+
+extern "C" hipError_t ppfs_rs_generic_server_launch(int n, int t2, SrvBox* box, uint8_t* zc, uint64_t zc_bytes,
+    const uint8_t* tab, uint32_t gen, uint32_t idle_us, hipStream_t s)
+{
+    hipLaunchKernelGGL(rs_generic_server_kernel, dim3(1), dim3(64), 0, s, box, zc, zc_bytes, n, t2, tab, gen, idle_us);
+    return hipGetLastError();
 }
 
 extern "C" hipError_t ppfs_rs_generic_encode(const uint8_t* d, uint8_t* r, uint64_t nb, int n, int t2,

@@ -1,5 +1,5 @@
 """GPU tests of the resident small-batch server (api.cpp server_call, rs_wg.hpp rs_wg_server_kernel):
-the per-block readBlock / writeBlock calls of RS with 2t <= 8 or 2t = 32 (batches of <= 64 blocks through
+the per-block readBlock / writeBlock calls of every codec (batches of <= 64 blocks through
 the host entry points) are served by one resident workgroup polling a mailbox in host-coherent
 memory.  Every result is compared with the oracle (rs_block_device.cpp semantics: payload,
 status, written-back codeword bytes) and with the launch path (PPFS_ECC_SERVER=0); the server is
@@ -19,8 +19,10 @@ pytestmark = pytest.mark.gpu
 
 from paritypartyfs_amd import ECC_REED_SOLOMON, EccEngine
 
-# the 2t <= 8 segment path and the 2t = 32 pair path (n = 255)
-SERVER_CASES = [(512, 3), (255, 1), (255, 2), (256, 4), (256, 16), (4096, 16)]
+# every RS table layout: 2t <= 8 segment path, 2t = 10 / 16 lane-per-block, 2t = 32 pair path,
+# and the generic path (2t = 12 at n = 255; shortened codes n < 255)
+SERVER_CASES = [(512, 3), (255, 1), (255, 2), (256, 4), (256, 16), (4096, 16), (1024, 5), (4096, 8), (255, 6),
+                (64, 3), (128, 10), (32, 1)]
 
 
 def rng_for(*k):
