@@ -65,8 +65,15 @@ def main():
         eng.encode(d[i], c[i])
     res["dec_hot_us"] = timed(lambda i: eng.decode(c[0], o[0], st, write_back=True))
     res["dec_cold_us"] = timed(lambda i: eng.decode(c[i % R], o[i % R], st, write_back=True))
+    # one byte error per codeword, no write-back (the errors stay): the correction's cost
+    res["dec_clean_nowb_hot_us"] = timed(lambda i: eng.decode(c[0], o[0], st, write_back=False))
+    pos = torch.arange(nb, device=dev, dtype=torch.int64) * n + torch.randint(0, n, (nb,), device=dev, generator=g)
+    bad = c[1].clone()
+    bad[pos] ^= torch.randint(1, 256, (nb,), dtype=torch.uint8, device=dev, generator=g)
+    res["dec_1err_nowb_hot_us"] = timed(lambda i: eng.decode(bad, o[0], st, write_back=False))
+    assert int((st == 1).sum().item()) == nb  # every block corrected
     alg = (n + k) * nb
-    for key in ("enc_hot_us", "enc_cold_us", "dec_hot_us", "dec_cold_us"):
+    for key in ("enc_hot_us", "enc_cold_us", "dec_hot_us", "dec_cold_us", "dec_1err_nowb_hot_us"):
         res[key.replace("_us", "_frac")] = round(alg / (res[key] * 1e-6) / 8e12, 4)
     print(json.dumps(res), flush=True)
 
