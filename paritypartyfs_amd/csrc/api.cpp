@@ -223,7 +223,7 @@ template <int T2> std::vector<uint8_t> build_rs_wg_tables_t()
 {
     using L = ppfs::RsWgLayout<T2>;
     const GfHost& G = gf();
-    std::vector<uint8_t> out((size_t)L::TABLE_BYTES, 0);
+    std::vector<uint8_t> out((size_t)L::BLOB_BYTES, 0);
     const std::vector<uint8_t> g = rs_generator(T2);
     // top-aligned 8-byte entry of a remainder r (coefficient q at byte 8 - 2t + q)
     auto put = [&](int off, int table, int v, const std::vector<uint8_t>& r, uint8_t scale) {
@@ -242,6 +242,13 @@ template <int T2> std::vector<uint8_t> build_rs_wg_tables_t()
             for (int h = 0; h < 2; ++h)
                 for (int v = 0; v < 16; ++v)
                     put(L::OFF_MAP + m * L::MAP_STRIDE, 2 * q + h, v, xq, (uint8_t)(v << (4 * h)));
+        }
+    for (int m = 0; m < 7; ++m)
+        for (int q = 0; q < T2; ++q) {
+            const std::vector<uint8_t> xq = rs_xpow_mod(q + 32 * (m + 1), g, T2);
+            for (int h = 0; h < 2; ++h)
+                for (int v = 0; v < 16; ++v)
+                    put(L::OFF_MAP32 + m * L::MAP_STRIDE, 2 * q + h, v, xq, (uint8_t)(v << (4 * h)));
         }
     for (int q = 0; q < T2; ++q)
         for (int h = 0; h < 2; ++h)

@@ -104,6 +104,10 @@ constexpr int DEC_NBUF = DEC_FULL ? 0 : PPFS_WG_DEC_NBUF;
 #ifndef PPFS_WG_RP
 #define PPFS_WG_RP 0
 #endif
+// PPFS_WG_ENC_W8 = NBUF (3 or 4): the 8-wave encode (rs_wg.hpp rs_wg_encode8_kernel); 0 = off
+#ifndef PPFS_WG_ENC_W8
+#define PPFS_WG_ENC_W8 0
+#endif
 #if PPFS_WG_RP
 #include "rs_wg_rp.hpp"
 #endif
@@ -178,6 +182,9 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
 #if PPFS_WG_RP
     hipLaunchKernelGGL((wg::rs_wg_encode_rp_kernel<PPFS_T2, PPFS_WG_RP, PPFS_ENC_NTST>),
         dim3(rs_tile_grid(nb, PPFS_WG_RP)), dim3(256), 0, s, d, r, nb, tab);
+#elif PPFS_WG_ENC_W8
+    hipLaunchKernelGGL((wg::rs_wg_encode8_kernel<PPFS_T2, (PPFS_T2 > 6 ? 3 : PPFS_WG_ENC_W8), 2, PPFS_ENC_NTST>),
+        dim3(rs_tile_grid(nb, 2)), dim3(512), 0, s, d, r, nb, tab);
 #else
     if constexpr (PPFS_WG_ENC_IMG)
         hipLaunchKernelGGL((wg::rs_wg_encode_img_kernel<PPFS_T2, PPFS_WG_ENC_IMG_WPC, PPFS_ENC_NTST>),

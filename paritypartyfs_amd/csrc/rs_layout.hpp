@@ -9,6 +9,7 @@
 //   SL   slicing-by-8: table 2i+h, value v -> (v << 4h) * x^(2t+i) mod g      (16 tables)
 //   MAP  m = 0,1,2: table 2q+h, value v -> (v << 4h) * x^(q + 64(m+1)) mod g (2t tables each):
 //        moves a segment remainder from segment m+1 to its place in the codeword
+//   MAP32 the same for 32-byte segments, m = 0..6 (the 8-wave encode; appended after GF)
 //   SYN  table 2q+h, value v -> bytes i-1 = (v << 4h) * alpha^(i (q - 2t)), i = 1..2t: the
 //        syndromes S_i = c(alpha^i) from r' = x^2t c(x) mod g (rs_block_device.cpp:131-141)
 //   GF   the 1 KiB EXP2 / LOG / QS block of gf_common.hpp
@@ -27,12 +28,16 @@ template <int T2> struct RsWgLayout {
     static constexpr int OFF_SYN = OFF_MAP + 3 * MAP_STRIDE;
     static constexpr int OFF_GF = OFF_SYN + 2 * T2 * TBL;
     static constexpr int TABLE_BYTES = OFF_GF + GF_BYTES;
-    static_assert(TABLE_BYTES % 16 == 0, "tables are copied in 16-byte pieces");
+    // MAP32 (after the decode layout, read by the 8-wave encode only): m = 0..6, the x^(q + 32(m+1))
+    // maps of 32-byte segments
+    static constexpr int OFF_MAP32 = TABLE_BYTES;
+    static constexpr int BLOB_BYTES = OFF_MAP32 + 7 * MAP_STRIDE;
+    static_assert(TABLE_BYTES % 16 == 0 && BLOB_BYTES % 16 == 0, "tables are copied in 16-byte pieces");
 };
 
 constexpr int rs_wg_table_bytes(int t2)
 {
-    return 16 * 128 + 3 * 2 * t2 * 128 + 2 * t2 * 128 + GF_BYTES;
+    return 16 * 128 + 3 * 2 * t2 * 128 + 2 * t2 * 128 + GF_BYTES + 7 * 2 * t2 * 128;
 }
 
 // Pair RS path (rs_pair.hpp), 16 < 2t <= 32: the same 32-byte top-aligned state, two lanes per

@@ -152,12 +152,12 @@ __device__ __forceinline__ void step8(uint32_t (&s)[2], uint32_t lo, uint32_t hi
     xor_entries<2 * NL>(s, e);
 }
 
-// r = sum_j B[64S + j] x^(2t + j) mod g over segment S of a LEN-byte row at LDS byte `row`
-template <int T2, int LEN, int S>
+// r = sum_j B[SEG S + j] x^(2t + j) mod g over segment S (SEG bytes) of a LEN-byte row at LDS byte `row`
+template <int T2, int LEN, int S, int SEG = 64>
 __device__ __forceinline__ void seg_remainder(uint32_t (&s)[2], const uint8_t* lds, uint32_t row)
 {
-    constexpr int LO = 64 * S;
-    constexpr int LS = (LEN - LO) < 64 ? (LEN - LO) : 64;
+    constexpr int LO = SEG * S;
+    constexpr int LS = (LEN - LO) < SEG ? (LEN - LO) : SEG;
     constexpr int NC = (LS + 7) / 8;
     constexpr int TOPN = LS - 8 * (NC - 1);
     constexpr int NR = 2 * NC + 1;
@@ -189,7 +189,8 @@ __device__ __forceinline__ void seg_remainder(uint32_t (&s)[2], const uint8_t* l
     }
 }
 
-// s <- s(x) * x^(64 S) mod g through the segment's map tables (S >= 1)
+// s <- s(x) * x^(SEG S) mod g through the segment's map tables (S >= 1; SEG = 64, or 32 for the
+// 8-wave encode, which copies MAP32 to OFF_MAP)
 template <int T2, int S> __device__ __forceinline__ void seg_map(uint32_t (&s)[2], const uint8_t* lds)
 {
     using L = RsWgLayout<T2>;
@@ -614,6 +615,153 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_kernel(const uint8_t* _
         uint8_t* dst = raw + t * (TB * 255);
         const uint32_t nout = nb * 255u;
         for (uint32_t p = tid; 16u * p < nout; p += NTHR) {
+            const uint4 v = enc_piece<T2>(lds, buf, par, p);
+            if (!PPFS_DBG_OK(dst + 16u * p, min(16u, nout - 16u * p), raw, nblocks * 255u))
+                continue;
+            if (16u * p + 16u <= nout)
+                *(uint4*)(dst + 16u * p) = v;
+            else
+                st_bytes(dst + 16u * p, v, nout - 16u * p);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// 8-wave encode (PPFS_WG_ENC_W8): a 512-thread workgroup per tile, wave s computing the remainder of
+// 32-byte segment s of every row (4 slicing steps instead of 8) and moving it with the MAP32 table
+// of x^(32 s); 2 DMA and 2 emission pieces per thread.  Same ring of LDS tile buffers and counted
+// waits as rs_wg_encode_kernel; twice the waves per CU for the same bytes in flight.
+// ------------------------------------------------------------------------------------
+template <int T2, int LEN, int S>
+__device__ __forceinline__ void seg8_one(uint32_t (&s)[2], const uint8_t* lds, uint32_t row, uint32_t wave)
+{
+    if constexpr (S < 8) {
+        if (wave == (uint32_t)S) {
+            seg_remainder<T2, LEN, S, 32>(s, lds, row);
+            if constexpr (S > 0)
+                seg_map<T2, S>(s, lds); // LDS holds MAP32 at OFF_MAP: map S-1 = x^(q + 32 S)
+        } else {
+            seg8_one<T2, LEN, S + 1>(s, lds, row, wave);
+        }
+    }
+}
+
+template <int T2, int LEN>
+__device__ __forceinline__ void phase_remainder8(uint8_t* lds, uint32_t buf, uint32_t par, uint32_t wave, uint32_t blk)
+{
+    uint32_t s[2];
+    seg8_one<T2, LEN, 0>(s, lds, buf + PAD + (uint32_t)LEN * blk, wave);
+    const uint64_t v = ((uint64_t)s[1] << 32) | s[0];
+    __hip_atomic_fetch_xor((unsigned long long*)(lds + par + 8u * blk), (unsigned long long)v, __ATOMIC_RELAXED,
+        __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// LDS-DMA of NPIECE 16-byte pieces by 512 threads: piece p = tid + 512 k, exactly 2 per wave
+template <int NPIECE>
+__device__ __forceinline__ void dma_tile512(uint8_t* dst, const uint8_t* __restrict__ src, uint32_t tid,
+    [[maybe_unused]] const uint8_t* base, [[maybe_unused]] uint64_t extent)
+{
+    static_assert(NPIECE > 512 + 448 && NPIECE <= 1024, "2 pieces per thread, every wave active in each");
+    const uint32_t lbase = __builtin_amdgcn_readfirstlane(lds_addr(dst) + (tid & ~63u) * 16u);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t p = tid + 512u * k;
+        if ((k < 1 || p < (uint32_t)NPIECE) && PPFS_DBG_OK(src + (size_t)p * 16, 16, base, extent))
+            dma16(src + (size_t)p * 16, lbase + 8192u * k);
+    }
+}
+
+template <int T2> struct Lds8 {
+    using L = RsWgLayout<T2>;
+    static constexpr int TBL = L::OFF_MAP + 7 * L::MAP_STRIDE; // SL + MAP32 (copied to OFF_MAP)
+    static constexpr int OFF_PAR = TBL;
+    static constexpr int OFF_BUF = OFF_PAR + 1024 + 64;
+    static_assert(OFF_BUF % 16 == 0 && TBL % 16 == 0, "aligned buffers");
+};
+
+template <int T2, int NBUF = 3, int WPC = 2, int NTST = 1>
+__global__ __launch_bounds__(512, WPC) void rs_wg_encode8_kernel(const uint8_t* __restrict__ data,
+    uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables)
+{
+    static_assert(NBUF >= 3 && NBUF <= 4, "ring of tile buffers");
+    using L = RsWgLayout<T2>;
+    using D = Lds8<T2>;
+    constexpr int NT = 512;
+    constexpr int BYTES = D::OFF_BUF + NBUF * BUF;
+    constexpr int LDS_ALLOC = lds_alloc<BYTES, WPC>();
+    static_assert(WPC * LDS_ALLOC <= 163840, "LDS for WPC workgroups per CU");
+    constexpr int K = L::K;
+    constexpr int IN_PIECES = TB * K / 16;   // 996 for 2t = 6
+    constexpr int OUT_PIECES = TB * 255 / 16; // 1020
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_ALLOC];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
+    const uint32_t row = lane_row(lane);
+    for (uint32_t p = tid; p < (uint32_t)L::OFF_MAP / 16; p += NT) // SL
+        *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
+    for (uint32_t p = tid; p < 7u * L::MAP_STRIDE / 16; p += NT) // MAP32
+        *(uint4*)(lds + L::OFF_MAP + 16 * p) = *(const uint4*)(tables + L::OFF_MAP32 + 16 * p);
+    if (tid < 128)
+        *(uint64_t*)(lds + D::OFF_PAR + 8 * tid) = 0;
+    const uint64_t nfull = nblocks / TB, ntiles = (nblocks + TB - 1) / TB;
+    uint64_t t = blockIdx.x;
+    uint32_t cur = 0, pc = 0;
+    if (t < nfull)
+        dma_tile512<IN_PIECES>(lds + D::OFF_BUF + PAD, data + t * (TB * K), tid, data, nblocks * K);
+    uint32_t hist = 0, iter = 0;
+#pragma unroll
+    for (int j = 1; j <= NBUF - 2; ++j) {
+        const bool go = t + j * gridDim.x < nfull;
+        if (go)
+            dma_tile512<IN_PIECES>(lds + D::OFF_BUF + j * BUF + PAD, data + (t + j * gridDim.x) * (TB * K), tid, data,
+                nblocks * K);
+        hist = (hist << 1) | (go ? 1u : 0u);
+    }
+    vm_wait_newer(2u * __builtin_popcount(hist)); // tile t landed, the later ones may fly
+    for (; t < nfull; t += gridDim.x) {
+        barrier_lds(); // A: tile t in LDS, last tile's emission reads done
+        const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + pc * 512u;
+        {
+            const uint64_t ahead = t + (uint64_t)(NBUF - 1) * gridDim.x;
+            const bool go = ahead < nfull;
+            if (go)
+                dma_tile512<IN_PIECES>(lds + D::OFF_BUF + ring_add(cur, NBUF - 1, NBUF) * BUF + PAD, data + ahead * (TB * K),
+                    tid, data, nblocks * K);
+            hist = (hist << 1) | (go ? 1u : 0u);
+        }
+        if (wave == 0)
+            *(uint64_t*)(lds + D::OFF_PAR + (pc ^ 1u) * 512u + 8u * lane) = 0;
+        phase_remainder8<T2, K>(lds, buf, par, wave, row);
+        barrier_lds(); // B: parity slots complete
+        uint8_t* dst = raw + t * (TB * 255);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint32_t p = tid + 512u * k;
+            const uint4 o = enc_piece<T2>(lds, buf, par, p);
+            if ((k < 1 || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, raw, nblocks * 255u))
+                st_nt<NTST>(dst + 16u * p, o);
+        }
+        // tile t + G landed: count every operation issued after its DMA (2 stores and 2 DMA
+        // instructions per wave and tile; fewer newer operations only lower the count)
+        ++iter;
+        const uint32_t st = 2u * (iter < (uint32_t)(NBUF - 1) ? iter : (uint32_t)(NBUF - 1));
+        vm_wait_newer(st + 2u * __builtin_popcount(hist & ((1u << (NBUF - 2)) - 1u)));
+        cur = ring_add(cur, 1, NBUF);
+        pc ^= 1u;
+    }
+    if (t == nfull && nfull < ntiles) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier_lds();
+        const uint32_t nb = (uint32_t)(nblocks - t * TB);
+        const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + pc * 512u;
+        if (PPFS_DBG_OK(data + t * (TB * K), nb * K, data, nblocks * K))
+            for (uint32_t i = tid; i < nb * K; i += NT)
+                lds[buf + PAD + i] = data[t * (TB * K) + i];
+        barrier_lds();
+        phase_remainder8<T2, K>(lds, buf, par, wave, row);
+        barrier_lds();
+        uint8_t* dst = raw + t * (TB * 255);
+        const uint32_t nout = nb * 255u;
+        for (uint32_t p = tid; 16u * p < nout; p += NT) {
             const uint4 v = enc_piece<T2>(lds, buf, par, p);
             if (!PPFS_DBG_OK(dst + 16u * p, min(16u, nout - 16u * p), raw, nblocks * 255u))
                 continue;
