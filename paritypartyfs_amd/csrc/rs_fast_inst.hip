@@ -104,6 +104,12 @@ constexpr int DEC_NBUF = DEC_FULL ? 0 : PPFS_WG_DEC_NBUF;
 #ifndef PPFS_WG_RP
 #define PPFS_WG_RP 0
 #endif
+// PPFS_WG_DYN: bit 0 = encode, bit 1 = decode take their tiles from a ticket counter (rs_wg.hpp
+// rs_wg_encode_dyn_kernel) instead of the static t += G walk; bit 2 = the static walk through the
+// same kernel (ablation)
+#ifndef PPFS_WG_DYN
+#define PPFS_WG_DYN 0
+#endif
 // PPFS_WG_ENC_W8 = NBUF (3 or 4): the 8-wave encode (rs_wg.hpp rs_wg_encode8_kernel); 0 = off
 #ifndef PPFS_WG_ENC_W8
 #define PPFS_WG_ENC_W8 0
@@ -182,6 +188,10 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
 #if PPFS_WG_RP
     hipLaunchKernelGGL((wg::rs_wg_encode_rp_kernel<PPFS_T2, PPFS_WG_RP, PPFS_ENC_NTST>),
         dim3(rs_tile_grid(nb, PPFS_WG_RP)), dim3(256), 0, s, d, r, nb, tab);
+#elif PPFS_WG_DYN & 1
+    hipLaunchKernelGGL((wg::rs_wg_encode_dyn_kernel<PPFS_T2, ENC_NBUF, ENC_WPC, PPFS_ENC_MODE, PPFS_ENC_NTST, (PPFS_WG_DYN & 4) != 0>),
+        dim3(rs_tile_grid(nb, ENC_WPC)), dim3(320), 0, s, d, r, nb, tab,
+        (uint32_t*)(const_cast<uint8_t*>(tab) + RsWgLayout<PPFS_T2>::OFF_CTR));
 #elif PPFS_WG_ENC_W8
     hipLaunchKernelGGL((wg::rs_wg_encode8_kernel<PPFS_T2, (PPFS_T2 > 6 ? 3 : PPFS_WG_ENC_W8), 2, PPFS_ENC_NTST>),
         dim3(rs_tile_grid(nb, 2)), dim3(512), 0, s, d, r, nb, tab);

@@ -31,13 +31,18 @@ template <int T2> struct RsWgLayout {
     // MAP32 (after the decode layout, read by the 8-wave encode only): m = 0..6, the x^(q + 32(m+1))
     // maps of 32-byte segments
     static constexpr int OFF_MAP32 = TABLE_BYTES;
-    static constexpr int BLOB_BYTES = OFF_MAP32 + 7 * MAP_STRIDE;
+    // CTR: zeroed tile-ticket counters of the dynamic-tile kernels (rs_wg.hpp): encode at +0,
+    // decode at +2048; in each, 8 counters (one per XCD) and the workgroups-done count, one
+    // 128-byte line each.  Each launch leaves them at zero.
+    static constexpr int OFF_CTR = OFF_MAP32 + 7 * MAP_STRIDE;
+    static constexpr int CTR_BYTES = 4096;
+    static constexpr int BLOB_BYTES = OFF_CTR + CTR_BYTES;
     static_assert(TABLE_BYTES % 16 == 0 && BLOB_BYTES % 16 == 0, "tables are copied in 16-byte pieces");
 };
 
 constexpr int rs_wg_table_bytes(int t2)
 {
-    return 16 * 128 + 3 * 2 * t2 * 128 + 2 * t2 * 128 + GF_BYTES + 7 * 2 * t2 * 128;
+    return 16 * 128 + 3 * 2 * t2 * 128 + 2 * t2 * 128 + GF_BYTES + 7 * 2 * t2 * 128 + 4096;
 }
 
 // Pair RS path (rs_pair.hpp), 16 < 2t <= 32: the same 32-byte top-aligned state, two lanes per
