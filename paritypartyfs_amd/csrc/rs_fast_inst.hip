@@ -104,18 +104,21 @@ constexpr int DEC_NBUF = DEC_FULL ? 0 : PPFS_WG_DEC_NBUF;
 #ifndef PPFS_WG_RP
 #define PPFS_WG_RP 0
 #endif
-// PPFS_WG_DYN: bit 0 = encode, bit 1 = decode take their tiles from a ticket counter (rs_wg.hpp
+// PPFS_WG_DYN: bit 0 = encode, bit 1 = decode take their tiles from a ticket counter (rs_wg_ablate.hpp
 // rs_wg_encode_dyn_kernel) instead of the static t += G walk; bit 2 = the static walk through the
 // same kernel (ablation)
 #ifndef PPFS_WG_DYN
 #define PPFS_WG_DYN 0
 #endif
-// PPFS_WG_ENC_W8 = NBUF (3 or 4): the 8-wave encode (rs_wg.hpp rs_wg_encode8_kernel); 0 = off
+// PPFS_WG_ENC_W8 = NBUF (3 or 4): the 8-wave encode (rs_wg_ablate.hpp rs_wg_encode8_kernel); 0 = off
 #ifndef PPFS_WG_ENC_W8
 #define PPFS_WG_ENC_W8 0
 #endif
 #if PPFS_WG_RP
 #include "rs_wg_rp.hpp"
+#endif
+#if PPFS_WG_ENC_W8 || PPFS_WG_DYN
+#include "rs_wg_ablate.hpp"
 #endif
 #ifndef PPFS_ENC_MODE
 #define PPFS_ENC_MODE 3 // ablation builds only: rs_wg.hpp MODE bits (remainder / codeword emission)
