@@ -1532,29 +1532,38 @@ extern "C" int ppfs_vote3_host(int device, const uint8_t* a, const uint8_t* b, c
     DeviceGuard guard(device);
     HIP_TRY(guard.err, "set device");
     // its own non-blocking stream, drained before anything is freed (not the legacy null stream,
-    // which does not order against other non-blocking streams)
+    // which does not order against other non-blocking streams).  The caller's (pageable) buffers
+    // are copied by the CPU through page-locked staging, as the engine's host calls do: the DMA
+    // engines only ever touch memory this call allocated and still holds.
     hipStream_t s = nullptr;
     HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "vote3 stream");
-    uint8_t* d = nullptr;
-    const size_t dmg_off = (4 * nbytes + 255) & ~(size_t)255;
-    hipError_t e = hipMalloc(&d, dmg_off + nrec * sizeof(uint32_t));
+    uint8_t *d = nullptr, *h = nullptr;
+    const size_t dmg_off = (4 * nbytes + 255) & ~(size_t)255, total = dmg_off + nrec * sizeof(uint32_t);
+    hipError_t e = hipMalloc(&d, total);
     if (e == hipSuccess)
-        e = hipMemcpyAsync(d, a, nbytes, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(d + nbytes, b, nbytes, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(d + 2 * nbytes, c, nbytes, hipMemcpyHostToDevice, s);
+        e = hipHostMalloc((void**)&h, total, hipHostMallocDefault);
+    if (e == hipSuccess) {
+        std::memcpy(h, a, nbytes);
+        std::memcpy(h + nbytes, b, nbytes);
+        std::memcpy(h + 2 * nbytes, c, nbytes);
+        e = hipMemcpyAsync(d, h, 3 * nbytes, hipMemcpyHostToDevice, s);
+    }
     if (e == hipSuccess)
         e = ppfs_vote3_launch(d, d + nbytes, d + 2 * nbytes, d + 3 * nbytes, rec_bytes, nrec,
             damaged ? (uint32_t*)(d + dmg_off) : nullptr, s);
     if (e == hipSuccess)
-        e = hipMemcpyAsync(out, d + 3 * nbytes, nbytes, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess && damaged)
-        e = hipMemcpyAsync(damaged, d + dmg_off, nrec * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+        e = hipMemcpyAsync(h + 3 * nbytes, d + 3 * nbytes, total - 3 * nbytes, hipMemcpyDeviceToHost, s);
     const hipError_t es = hipStreamSynchronize(s);
     if (e == hipSuccess)
         e = es;
+    if (e == hipSuccess) {
+        std::memcpy(out, h + 3 * nbytes, nbytes);
+        if (damaged)
+            std::memcpy(damaged, h + dmg_off, nrec * sizeof(uint32_t));
+    }
     const int r = e != hipSuccess ? fail(PPFS_ECC_EHIP, "vote3", e) : 0;
+    if (h)
+        (void)hipHostFree(h);
     if (d)
         (void)hipFree(d);
     (void)hipStreamDestroy(s);

@@ -306,7 +306,6 @@ __device__ __forceinline__ uint32_t be_window(const uint8_t* l, uint32_t o)
     return (uint32_t)(e >> (32 - k));
 }
 
-__device__ __forceinline__ uint32_t be_bit(const uint8_t* l, uint32_t i) { return (l[i >> 3] >> (7 - (i & 7u))) & 1u; }
 
 // XOR of (r0 + q) over set bits q of a big-endian word X (bit q = MSB-first position q)
 __device__ __forceinline__ uint32_t word_index_xor(uint32_t X, uint32_t r0)
@@ -359,14 +358,10 @@ __device__ __forceinline__ uint32_t ham_place_word(const uint8_t* dbuf, uint32_t
         return 0;
     uint32_t X;
     if (w == 0) {
-        X = 0;
-        for (uint32_t q = 3; q < 32 && q <= a.L; ++q) {
-            if (is_pow2(q))
-                continue;
-            const uint32_t i = q - ilog2(q) - 2;
-            X |= be_bit(dbuf, i) << (31 - q);
-        }
-        return X;
+        // payload bits 0, 1-3, 4-10, 11-25 sit at raw positions 3, 5-7, 9-15, 17-31
+        const uint32_t D = be_window(dbuf, 0);
+        X = ((D >> 31) << 28) | (((D >> 28) & 0x7u) << 24) | (((D >> 21) & 0x7Fu) << 16) | ((D >> 6) & 0x7FFFu);
+        return X & qmask(0, (int)a.L);
     }
     const uint32_t j1 = ilog2(r0), j2 = ilog2(r0 + 31);
     const int k = (j1 == j2 && !is_pow2(r0)) ? 32 : (int)((1u << j2) - r0);
@@ -541,13 +536,11 @@ __device__ __forceinline__ void ham_decode_blocks(uint8_t* __restrict__ raw, uin
                 if (v < ndw) {
                     const uint32_t i0 = 32 * v;
                     if (v == 0) {
-                        for (uint32_t q = 0; q < 32; ++q) {
-                            const uint32_t i = q;
-                            uint32_t j = ilog2(i + 2);
-                            if (i > (2u << j) - j - 3)
-                                j++;
-                            y |= be_bit(buf, i + j + 2) << (31 - q);
-                        }
+                        // payload bits 0, 1-3, 4-10, 11-25, 26-31 from raw positions 3, 5-7, 9-15,
+                        // 17-31, 33-38 (the inverse of ham_place_word's head word)
+                        const uint32_t R0 = be_window(buf, 0), R1 = be_window(buf, 32);
+                        y = (((R0 >> 28) & 1u) << 31) | (((R0 >> 24) & 0x7u) << 28) | (((R0 >> 16) & 0x7Fu) << 21)
+                            | ((R0 & 0x7FFFu) << 6) | ((R1 >> 25) & 0x3Fu);
                     } else {
                         uint32_t j1 = ilog2(i0 + 2);
                         if (i0 > (2u << j1) - j1 - 3)
