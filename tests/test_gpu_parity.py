@@ -303,7 +303,8 @@ def test_crc_encode_check_match_oracle(oracle, imp, bs):
 # ------------------------------------------------------------------------------------
 # Hamming
 # ------------------------------------------------------------------------------------
-@pytest.mark.parametrize("bs,nb", [(8, 1000), (16, 1000), (64, 1000), (256, 1000), (512, 1000), (1024, 1000),
+@pytest.mark.parametrize("bs,nb", [(8, 1000), (16, 1000), (32, 1000), (64, 1000), (128, 1000),
+                                   (256, 1000), (512, 1000), (1024, 1000),
                                    (2048, 700), (4096, 300), (4096, 5003)])
 def test_hamming_matches_oracle(oracle, bs, nb):
     """bs >= 1024 runs the streaming kernels of bit_fast.hip; 5003 blocks of 4 KiB make every

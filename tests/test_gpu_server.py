@@ -159,7 +159,8 @@ def test_server_large_batches_take_the_chunked_path(oracle):
 from paritypartyfs_amd import ECC_CRC, ECC_HAMMING, ECC_PARITY  # noqa: E402
 
 BIT_CASES = [("crc", 0xea, 256), ("crc", 0x9960034c, 4096), ("crc", 0xc1acf, 512), ("crc", 0x42F0E1EBA9EA3693 >> 1, 1024),
-             ("ham", 0, 256), ("ham", 0, 4096), ("ham", 0, 64), ("par", 0, 256), ("par", 0, 4096), ("par", 0, 2)]
+             ("ham", 0, 256), ("ham", 0, 4096), ("ham", 0, 64), ("ham", 0, 8), ("par", 0, 256),
+             ("par", 0, 4096), ("par", 0, 2)]
 
 
 def bit_engine(oracle, codec, imp, bs, server=True):
