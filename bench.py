@@ -7,7 +7,8 @@ rs_block_device.cpp:57), 2^20 blocks per GPU, synthetic uniform payloads.
 `--block-size 4096 --t 16` runs configs[4]'s RS(255,223) shard instead (2^20 blocks per GPU).
 
 One step = encode(2^20 payloads -> codewords)            [rs255 encode kernel]
-         + inject exactly one byte error into every codeword (one torch scatter of wrong bytes)
+         + inject exactly one byte error into every codeword (the engine's inject kernel stores
+           the precomputed wrong byte of every block; --inject torch: torch's index_put_)
          + decode(codewords -> payloads, status, in-place write-back)   [rs255 decode kernel]
 value = algorithmic bytes of all ranks (encode k+n B + decode n+k B per block) / step time.
 
@@ -51,6 +52,8 @@ def parse(argv=None):
     ap.add_argument("--blocks", type=int, default=1 << 20, help="blocks per GPU")
     ap.add_argument("--block-size", type=int, default=512)
     ap.add_argument("--t", type=int, default=3)
+    ap.add_argument("--inject", choices=("engine", "torch"), default="engine",
+                    help="fault-injection form: the engine's one-byte-per-block kernel or torch index_put_")
     ap.add_argument("--prewarm-s", type=float, default=1.0, help="untimed clock ramp before the warmup steps")
     ap.add_argument("--standalone-launches", type=int, default=30, help="back-to-back launches per kernel")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -316,8 +319,8 @@ def main(argv=None):
     out = torch.empty(nb * k, dtype=torch.uint8, device=dev)
     status = torch.empty(nb, dtype=torch.uint8, device=dev)
     # one error per codeword: position uniform in [0,255), value uniform in [1,255]
-    err_pos = (torch.arange(nb, device=dev, dtype=torch.int64) * n
-               + torch.randint(0, n, (nb,), device=dev, generator=gen))
+    err_col = torch.randint(0, n, (nb,), device=dev, generator=gen)
+    err_pos = torch.arange(nb, device=dev, dtype=torch.int64) * n + err_col
     err_val = torch.randint(1, 256, (nb,), dtype=torch.uint8, device=dev, generator=gen)
     stream = torch.cuda.current_stream()
     # The payloads never change, so every step's clean codewords are identical: the corrupted
@@ -326,10 +329,17 @@ def main(argv=None):
     eng.encode(data, cw, nblocks=nb)
     clean_cw = cw.clone()
     bad_bytes = cw[err_pos] ^ err_val
+    err_col8 = err_col.to(torch.uint8)
     torch.cuda.synchronize()
 
-    def inject():
-        cw.index_put_((err_pos,), bad_bytes)
+    if args.inject == "engine":
+        from paritypartyfs_amd import inject_bytes
+
+        def inject():
+            inject_bytes(cw, n, err_col8, bad_bytes, nblocks=nb, stream=stream)
+    else:
+        def inject():
+            cw.index_put_((err_pos,), bad_bytes)
 
     def step():
         eng.encode(data, cw, nblocks=nb)

@@ -171,6 +171,17 @@ int ppfs_vote3_host(int device, const uint8_t* a, const uint8_t* b, const uint8_
 int ppfs_copy_device(void* d_dst, const void* d_src, size_t bytes, void* stream);
 
 /*
+ * Fault injection, one byte per block: block b of the raw image (stride bytes per block) gets
+ * byte pos[b] set to val[b] (mode 0) or XORed with val[b] (mode 1); pos[b] >= stride leaves the
+ * block alone.  Positions are one byte each, so only the first 256 bytes of a block are
+ * reachable.  The device-side counterpart of the reference's bit flipper
+ * (usage_simulator/simulation/src/bit_flipper.cpp), which is out of scope as a simulator: this
+ * entry exists for bench.py's corrupt-then-decode step and the tests.  Not a reference interface.
+ */
+int ppfs_inject_device(uint8_t* d_raw, size_t stride, size_t nblocks, const uint8_t* d_pos, const uint8_t* d_val,
+    int mode, void* stream);
+
+/*
  * Page-lock / release a caller buffer (hipHostRegister), e.g. the host mirror of a disk image
  * (replacing FileDisk's seekp + fstream I/O, lib/disk/src/file_disk.cpp:56-101,
  * by an mmap'd or resident image the *_host calls then DMA directly).

@@ -9,10 +9,10 @@ loaded from the in-tree libppfs_ecc.so.  Python pieces:
 """
 from ._native import (ECC_CRC, ECC_HAMMING, ECC_NONE, ECC_PARITY, ECC_REED_SOLOMON, STATUS_CORRECTED,
                       STATUS_CORRECTION_ERROR, STATUS_OK, NativeLibraryMissing)
-from .ecc import EccEngine, EccGroup, crc_implicit_to_explicit, device_copy, pinned, vote3, vote3_host
+from .ecc import EccEngine, EccGroup, crc_implicit_to_explicit, device_copy, inject_bytes, pinned, vote3, vote3_host
 
 __all__ = [
-    "EccEngine", "EccGroup", "crc_implicit_to_explicit", "device_copy", "pinned", "vote3", "vote3_host", "NativeLibraryMissing",
+    "EccEngine", "EccGroup", "crc_implicit_to_explicit", "device_copy", "inject_bytes", "pinned", "vote3", "vote3_host", "NativeLibraryMissing",
     "ECC_NONE", "ECC_CRC", "ECC_HAMMING", "ECC_PARITY", "ECC_REED_SOLOMON",
     "STATUS_OK", "STATUS_CORRECTED", "STATUS_CORRECTION_ERROR",
 ]

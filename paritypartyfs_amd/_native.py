@@ -37,6 +37,7 @@ EXPORTED_SYMBOLS = (
     "ppfs_vote3_device",
     "ppfs_vote3_host",
     "ppfs_copy_device",
+    "ppfs_inject_device",
     "ppfs_ecc_host_register",
     "ppfs_ecc_host_unregister",
     "ppfs_ecc_group_create",
@@ -125,6 +126,8 @@ def lib() -> ctypes.CDLL:
     L.ppfs_vote3_device.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p, c_void_p]
     L.ppfs_copy_device.restype = c_int
     L.ppfs_copy_device.argtypes = [c_void_p, c_void_p, c_size_t, c_void_p]
+    L.ppfs_inject_device.restype = c_int
+    L.ppfs_inject_device.argtypes = [c_void_p, c_size_t, c_size_t, c_void_p, c_void_p, c_int, c_void_p]
     L.ppfs_vote3_host.restype = c_int
     L.ppfs_vote3_host.argtypes = [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_size_t, c_void_p]
     L.ppfs_ecc_host_register.restype = c_int

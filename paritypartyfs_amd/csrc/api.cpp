@@ -64,6 +64,8 @@ hipError_t ppfs_gather_rows_launch(const uint8_t* src, uint64_t src_rows, uint8_
 hipError_t ppfs_vote3_launch(const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* out, uint64_t rec_bytes,
     uint64_t nrec, uint32_t* damaged, hipStream_t s);
 hipError_t ppfs_copy_launch(uint8_t* dst, const uint8_t* src, uint64_t bytes, hipStream_t s);
+hipError_t ppfs_inject_launch(uint8_t* raw, uint64_t stride, uint64_t nblocks, const uint8_t* pos, const uint8_t* val,
+    int mode, hipStream_t s);
 }
 
 namespace {
@@ -297,6 +299,15 @@ std::vector<uint8_t> build_rs_pair_tables(int t2)
             if (xr[q])
                 xpm[p * 32 + (32 - t2 + q)] = G.log[xr[q]];
     }
+    // byte-slice tables (rs_bs.hpp): by linearity, byte v at chunk position q maps to the XOR of
+    // its two nibble entries; row v, slot 2q + c
+    uint8_t* bs = xpm + 255 * 32;
+    for (int v = 0; v < 256; ++v)
+        for (int q = 0; q < 8; ++q)
+            for (int c = 0; c < 2; ++c)
+                for (int k = 0; k < 16; ++k)
+                    bs[v * 256 + (2 * q + c) * 16 + k] = out[(size_t)(2 * q) * 512 + (size_t)c * 256 + (size_t)(v & 15) * 16 + k]
+                        ^ out[(size_t)(2 * q + 1) * 512 + (size_t)c * 256 + (size_t)(v >> 4) * 16 + k];
     return out;
 }
 
@@ -1516,6 +1527,20 @@ extern "C" int ppfs_copy_device(void* d_dst, const void* d_src, size_t bytes, vo
     return sync_check(
         check_hip(ppfs_copy_launch((uint8_t*)d_dst, (const uint8_t*)d_src, bytes, (hipStream_t)stream), "copy"), stream,
         "copy (async)");
+}
+
+extern "C" int ppfs_inject_device(uint8_t* d_raw, size_t stride, size_t nblocks, const uint8_t* d_pos,
+    const uint8_t* d_val, int mode, void* stream)
+{
+    if (nblocks && (!d_raw || !d_pos || !d_val))
+        return fail(PPFS_ECC_EINVAL, "inject: null argument");
+    if (nblocks && !stride)
+        return fail(PPFS_ECC_EINVAL, "inject: zero stride");
+    if (mode != 0 && mode != 1)
+        return fail(PPFS_ECC_EINVAL, "inject: mode must be 0 (set) or 1 (xor)");
+    return sync_check(check_hip(ppfs_inject_launch(d_raw, stride, nblocks, d_pos, d_val, mode, (hipStream_t)stream),
+                          "inject"),
+        stream, "inject (async)");
 }
 
 extern "C" int ppfs_vote3_host(int device, const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* out,

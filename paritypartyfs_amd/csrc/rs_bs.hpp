@@ -1,0 +1,394 @@
+#pragma once
+// rs_bs.hpp -- byte-slice RS(255, 223) encode / decode for gfx950 (2t = 32, cfg5: t = 16).
+//
+// Reference semantics: lib/blockdevice/src/rs_block_device.cpp (encode :95-117, decode :119-183);
+// the maths is rs_pair.hpp's (two lanes per block, lane c holds bytes [16c, 16c+16) of the
+// 32-byte remainder state, slicing-by-8 Horner steps from the top chunk down, decode from
+// c mod g with the XP-row single-error check), with the lookups redesigned:
+//
+//   - BYTE-indexed tables (RsPairLayout::OFF_BS, 64 KiB): one ds_read_b128 per chunk byte and
+//     lane instead of two nibble reads -- half the LDS bytes and half the XORs of the nibble
+//     kernels (8 entries x 4 dwords + the shifted state: 16 v_bitop3 per 8 payload bytes, not 32).
+//   - Conflict-free whatever the byte values: table row v (256 B = the 64 banks) holds the eight
+//     chunk positions q x two columns c side by side, slot 2q + c.  A ds_read_b128 is serviced in
+//     16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32; MI355X_MICROARCH.md, LDS); each
+//     group holds 8 pairs (partner = lane ^ 1, a quad_perm DPP) with 8 distinct rotations k, and
+//     pair k looks up its chunk byte (m + k) mod 8 at step m: the 16 lanes of a group read 16
+//     distinct slots, i.e. 16 distinct 4-bank groups, for any 16 rows.
+//   - Lookup address = v_perm(slot offsets, rotated chunk): byte 1 = the chunk byte (row), byte 0
+//     = the lane's slot offset; the rotation is two v_perm per chunk with lane-constant selectors.
+//   - The 64 KiB table is shared by one workgroup per CU of NW waves; every wave works alone on
+//     its own 32-block tiles (8,160 B, LDS-DMA'd into the codeword image of
+//     rs_pair_encode_img_kernel), so the tile loop has no workgroup barrier.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rs_pair.hpp"
+
+namespace ppfs {
+namespace bs {
+
+using wg::dma16;
+using wg::lds_addr;
+using wg::st_bytes;
+using wg::st_nt;
+
+constexpr int TBW = 32;            // blocks per wave tile
+constexpr int IMGW = TBW * 255;    // 8,160 B: one wave tile's codeword image
+constexpr int IMG_PIECES = IMGW / 16; // 510 16-byte pieces in and out
+constexpr int KP = (IMG_PIECES + 63) / 64; // 8 DMA / store wave-instructions per tile
+constexpr int OFF_TAB = 0;         // the byte-slice tables sit at LDS address 0
+constexpr int TAB_BYTES = 256 * 256;
+
+// lane constants: column, block in the wave tile, rotation and the v_perm selectors
+struct BsLane {
+    uint32_t c, blk;
+    uint32_t sel_lo, sel_hi; // rotated chunk: byte m = chunk byte (m + k) mod 8 (v_perm of hi:lo)
+    uint32_t off_a, off_b;   // slot offsets 16 (2 ((m + k) mod 8) + c), m = 0..3 / 4..7, one per byte
+};
+
+__device__ __forceinline__ BsLane bs_lane(uint32_t lane)
+{
+    BsLane L;
+    L.c = lane & 1u;
+    const uint32_t p = (lane >> 1) & 15u;       // pair within the half-wave
+    const uint32_t k = (p & 1u) | ((p >> 2) << 1); // distinct within each ds_read_b128 lane group
+    // half-wave h takes blocks h, h + 2, ...: a ds_read_b32 group's 16 rows (255 B apart in the
+    // image) then fall at most 2 to a bank
+    L.blk = 2u * p + (lane >> 5);
+    uint32_t sl = 0, sh = 0, oa = 0, ob = 0;
+#pragma unroll
+    for (uint32_t m = 0; m < 4; ++m) {
+        sl |= ((m + k) & 7u) << (8 * m);
+        sh |= ((m + 4u + k) & 7u) << (8 * m);
+        oa |= (32u * ((m + k) & 7u) + 16u * L.c) << (8 * m);
+        ob |= (32u * ((m + 4u + k) & 7u) + 16u * L.c) << (8 * m);
+    }
+    L.sel_lo = sl;
+    L.sel_hi = sh;
+    L.off_a = oa;
+    L.off_b = ob;
+    return L;
+}
+
+// v_perm selector: byte 0 = byte m of the offsets word (S0), byte 1 = byte m of the rotated chunk
+// word (S1), bytes 2-3 = 0
+template <int M> constexpr uint32_t addr_sel() { return 0x0C0C0000u | ((uint32_t)M << 8) | (4u + (uint32_t)M); }
+
+// the 8 byte lookups of one chunk (lo, hi = chunk bytes 0-3 / 4-7), XORed into acc
+__device__ __forceinline__ void bs_lookups(uint32_t (&acc)[4], const uint8_t* lds, const BsLane& L, uint32_t lo, uint32_t hi)
+{
+    const uint32_t rl = __builtin_amdgcn_perm(hi, lo, L.sel_lo), rh = __builtin_amdgcn_perm(hi, lo, L.sel_hi);
+    uint4 e[8];
+    e[0] = pair::ld16(lds, OFF_TAB + __builtin_amdgcn_perm(L.off_a, rl, addr_sel<0>()));
+    e[1] = pair::ld16(lds, OFF_TAB + __builtin_amdgcn_perm(L.off_a, rl, addr_sel<1>()));
+    e[2] = pair::ld16(lds, OFF_TAB + __builtin_amdgcn_perm(L.off_a, rl, addr_sel<2>()));
+    e[3] = pair::ld16(lds, OFF_TAB + __builtin_amdgcn_perm(L.off_a, rl, addr_sel<3>()));
+    e[4] = pair::ld16(lds, OFF_TAB + __builtin_amdgcn_perm(L.off_b, rh, addr_sel<0>()));
+    e[5] = pair::ld16(lds, OFF_TAB + __builtin_amdgcn_perm(L.off_b, rh, addr_sel<1>()));
+    e[6] = pair::ld16(lds, OFF_TAB + __builtin_amdgcn_perm(L.off_b, rh, addr_sel<2>()));
+    e[7] = pair::ld16(lds, OFF_TAB + __builtin_amdgcn_perm(L.off_b, rh, addr_sel<3>()));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        auto w = [&](int i) -> uint32_t { return q == 0 ? e[i].x : q == 1 ? e[i].y : q == 2 ? e[i].z : e[i].w; };
+        uint32_t a = xor3(acc[q], w(0), w(1));
+        a = xor3(a, w(2), w(3));
+        a = xor3(a, w(4), w(5));
+        acc[q] = xor3(a, w(6), w(7));
+    }
+}
+
+// Remainder column c of a LEN-byte row at LDS byte `row` (rs_pair.hpp pair_remainder with the
+// byte lookups; the top chunk holds LEN - 8 (NC - 1) bytes)
+template <int LEN>
+__device__ __forceinline__ void bs_remainder(uint32_t (&s)[4], const uint8_t* lds, uint32_t row, const BsLane& L)
+{
+    constexpr int NC = (LEN + 7) / 8;
+    constexpr int TOPN = LEN - 8 * (NC - 1);
+    const uint32_t sh = (row & 3u) * 8u;
+    const uint32_t* w = (const uint32_t*)(lds + (row & ~3u));
+    const uint32_t c = L.c, cm = c ? ~0u : 0u;
+    uint32_t up = w[2 * NC];
+#pragma unroll
+    for (int j = NC - 1; j >= 0; --j) {
+        const uint32_t d1 = w[2 * j + 1], d0 = w[2 * j];
+        uint32_t hi = __builtin_amdgcn_alignbit(up, d1, sh); // payload bytes 8j+4 .. 8j+7
+        uint32_t lo = __builtin_amdgcn_alignbit(d1, d0, sh); // payload bytes 8j .. 8j+3
+        up = d0;
+        if (j == NC - 1) {
+            if constexpr (TOPN < 4) {
+                lo &= (1u << (8 * TOPN)) - 1u;
+                hi = 0;
+            } else if constexpr (TOPN == 4) {
+                hi = 0;
+            } else if constexpr (TOPN < 8) {
+                hi &= (1u << (8 * (TOPN - 4))) - 1u;
+            }
+            s[0] = s[1] = s[2] = s[3] = 0;
+            bs_lookups(s, lds, L, lo, hi);
+        } else {
+            const uint32_t p2 = pair::pair_xchg<1>(s[2]), p3 = pair::pair_xchg<1>(s[3]);
+            lo ^= c ? s[2] : p2; // fold the top 8 coefficients (column 1's upper half)
+            hi ^= c ? s[3] : p3;
+            uint32_t n[4] = { p2 & cm, p3 & cm, s[0], s[1] }; // state * x^8
+            bs_lookups(n, lds, L, lo, hi);
+            s[0] = n[0];
+            s[1] = n[1];
+            s[2] = n[2];
+            s[3] = n[3];
+        }
+    }
+}
+
+// c mod g of the LDS codeword row (2t = 32): the payload's remainder XOR the stored parity
+__device__ __forceinline__ void bs_cmodg(uint32_t (&s)[4], const uint8_t* lds, uint32_t row, const BsLane& L)
+{
+    bs_remainder<223>(s, lds, row + 32u, L);
+    const uint32_t a = row + 16u * L.c, sh = (a & 3u) * 8u;
+    const uint32_t* w = (const uint32_t*)(lds + (a & ~3u));
+    uint32_t d[5];
+#pragma unroll
+    for (int m = 0; m < 5; ++m)
+        d[m] = w[m];
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+        s[m] ^= __builtin_amdgcn_alignbit(d[m + 1], d[m], sh);
+}
+
+// LDS-DMA of a wave tile: image piece i = lane + 64 k lands at img + 16 i; its source is
+// src + src_off(i) (-1: nothing to load)
+template <typename F>
+__device__ __forceinline__ void dma_wave(uint32_t img_base, const uint8_t* __restrict__ src, uint32_t lane, F src_off,
+    [[maybe_unused]] const uint8_t* gbase, [[maybe_unused]] uint64_t extent)
+{
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+        const uint32_t i = lane + 64u * (uint32_t)k;
+        const int so = src_off(i);
+        if (((k + 1) * 64 <= IMG_PIECES || i < (uint32_t)IMG_PIECES) && so >= 0 && PPFS_DBG_OK(src + so, 16, gbase, extent))
+            dma16(src + so, __builtin_amdgcn_readfirstlane(img_base + 1024u * (uint32_t)k));
+    }
+}
+
+// the lane's 16 parity bytes into the image gap [255 blk + 16 c, +16)
+__device__ __forceinline__ void put_parity(uint8_t* lds, uint32_t img, const BsLane& L, const uint32_t (&s)[4])
+{
+    uint8_t* const gap = lds + img + 255u * L.blk + 16u * L.c;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        gap[k] = (uint8_t)(s[k >> 2] >> (8 * (k & 3)));
+}
+
+// LDS plan: [0, 64 KiB) byte-slice tables | (decode: GF block, NW x 1 KiB syndrome slots) |
+// NW x NBUF wave images | 64 B slack (the rows' last-word reads and the decode emission's second
+// window run past the last image)
+template <int NW, int NBUF, bool DEC> struct BsLds {
+    static constexpr int OFF_GF = TAB_BYTES;
+    static constexpr int OFF_SLOT = OFF_GF + (DEC ? GF_BYTES : 0);
+    static constexpr int OFF_IMG = OFF_SLOT + (DEC ? NW * TBW * 32 : 0);
+    static constexpr int BYTES = OFF_IMG + NW * NBUF * IMGW + 64;
+    static_assert(BYTES <= 163840, "one workgroup per CU: 160 KiB of LDS");
+    static_assert(OFF_IMG % 16 == 0 && IMGW % 16 == 0, "aligned images");
+};
+
+// Encode: 2^k payloads -> codewords.  Workgroup b's wave w takes wave tiles b NW + w + j S
+// (S = grid NW).  NBUF = 1: a wave DMAs its next tile once its emission has read the image;
+// NBUF = 2: the next tile is DMA'd at the top of the iteration into the other buffer.
+template <int T2, int NW, int NBUF, int NTST = 1>
+__global__ __launch_bounds__(64 * NW, 1) void rs_bs_encode_kernel(const uint8_t* __restrict__ data,
+    uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables)
+{
+    static_assert(T2 == 32, "byte-slice path: 2t = 32 (image pieces need 16 | 2t, state byte q = coefficient q)");
+    static_assert(NBUF == 1 || NBUF == 2, "NBUF");
+    using L = RsPairLayout<T2>;
+    using D = BsLds<NW, NBUF, false>;
+    constexpr int K = L::K;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[D::BYTES];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
+    for (uint32_t p = tid; p < (uint32_t)TAB_BYTES / 16; p += 64u * NW)
+        *(uint4*)(lds + OFF_TAB + 16 * p) = *(const uint4*)(tables + L::OFF_BS + 16 * p);
+    __syncthreads();
+    const BsLane Ln = bs_lane(lane);
+    const uint32_t img0 = D::OFF_IMG + wave * (uint32_t)(NBUF * IMGW);
+    const uint32_t base0 = __builtin_amdgcn_readfirstlane(lds_addr(lds + img0));
+    const uint64_t nfull = nblocks / TBW, ntiles = (nblocks + TBW - 1) / TBW;
+    const uint64_t S = (uint64_t)gridDim.x * NW;
+    uint64_t t = (uint64_t)blockIdx.x * NW + wave;
+    auto src_off = [](uint32_t i) { return pair::img_src<T2>(i); };
+    const uint8_t* const dextent = data;
+    if (t < nfull)
+        dma_wave(base0, data + t * (TBW * K), lane, src_off, dextent, nblocks * K);
+    uint32_t cur = 0;
+    bool first = true;
+    for (; t < nfull; t += S) {
+        const uint64_t nx = t + S;
+        const uint32_t img = img0 + cur * IMGW;
+        if constexpr (NBUF == 2) {
+            // the other buffer's emission reads finished in the previous iteration (its stores
+            // consumed them); the DMA count below relies on 8 instructions per tile
+            if (nx < nfull) {
+                dma_wave(base0 + (cur ^ 1u) * IMGW, data + nx * (TBW * K), lane, src_off, dextent, nblocks * K);
+                if (first)
+                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); // tile t's DMA; tile nx's may fly
+                else
+                    asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); // + the last tile's 8 stores
+            } else {
+                if (first)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            }
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        first = false;
+        uint32_t s[4];
+        bs_remainder<K>(s, lds, img + 255u * Ln.blk + (uint32_t)T2, Ln);
+        put_parity(lds, img, Ln, s);
+        uint8_t* dst = raw + t * (TBW * 255);
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+            const uint32_t i = lane + 64u * (uint32_t)k;
+            if (((k + 1) * 64 <= IMG_PIECES || i < (uint32_t)IMG_PIECES) && PPFS_DBG_OK(dst + 16u * i, 16, raw, nblocks * 255u))
+                st_nt<NTST>(dst + 16u * i, pair::ld16(lds, img + 16u * i));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // the image is read: free for the next DMA
+        if constexpr (NBUF == 1) {
+            if (nx < nfull)
+                dma_wave(base0, data + nx * (TBW * K), lane, src_off, dextent, nblocks * K);
+        } else {
+            cur ^= 1u;
+        }
+    }
+    if (t == nfull && nfull < ntiles) {
+        // the one partial tile (nblocks % 32 blocks), staged byte by byte into the image
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t img = img0 + cur * IMGW;
+        const uint32_t nb = (uint32_t)(nblocks - t * TBW);
+        const uint8_t* src = data + t * (TBW * K);
+        if (!PPFS_DBG_OK(src, nb * (uint32_t)K, data, nblocks * K))
+            return;
+        for (uint32_t j = lane; j < nb * (uint32_t)K; j += 64u) {
+            const uint32_t b = j / (uint32_t)K;
+            lds[img + 255u * b + (uint32_t)T2 + (j - (uint32_t)K * b)] = src[j];
+        }
+        wave_fence();
+        uint32_t s[4];
+        bs_remainder<K>(s, lds, img + 255u * Ln.blk + (uint32_t)T2, Ln);
+        if (Ln.blk < nb)
+            put_parity(lds, img, Ln, s);
+        wave_fence();
+        uint8_t* dst = raw + t * (TBW * 255);
+        const uint32_t nout = nb * 255u;
+        for (uint32_t i = lane; 16u * i < nout; i += 64u) {
+            const uint4 v = pair::ld16(lds, img + 16u * i);
+            if (!PPFS_DBG_OK(dst + 16u * i, min(16u, nout - 16u * i), raw, nblocks * 255u))
+                continue;
+            if (16u * i + 16u <= nout)
+                *(uint4*)(dst + 16u * i) = v;
+            else
+                st_bytes(dst + 16u * i, v, nout - 16u * i);
+        }
+    }
+}
+
+// Decode with status and write-back (rs_pair_decode_kernel's semantics): c mod g per block,
+// single error confirmed against the XP row, else all 32 syndromes and BM / roots / Forney (out
+// of line); corrections patch the image row and, with write-back, the codeword byte in HBM; the
+// payload pieces come straight from the image.  Single-buffered: the correction path's XP-row
+// loads are compiler-counted, and their waits would drain a prefetch.
+template <int T2, int NW, int NTST = 1>
+__global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __restrict__ raw,
+    uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables,
+    int write_back)
+{
+    static_assert(T2 == 32, "byte-slice path: 2t = 32");
+    using L = RsPairLayout<T2>;
+    using D = BsLds<NW, 1, true>;
+    constexpr int K = L::K;
+    constexpr int OUT_PIECES = TBW * K / 16; // 446
+    constexpr int KO = (OUT_PIECES + 63) / 64;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[D::BYTES];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
+    for (uint32_t p = tid; p < (uint32_t)TAB_BYTES / 16; p += 64u * NW)
+        *(uint4*)(lds + OFF_TAB + 16 * p) = *(const uint4*)(tables + L::OFF_BS + 16 * p);
+    for (uint32_t p = tid; p < (uint32_t)GF_BYTES / 16; p += 64u * NW)
+        *(uint4*)(lds + D::OFF_GF + 16 * p) = *(const uint4*)(tables + L::OFF_GF + 16 * p);
+    __syncthreads();
+    const BsLane Ln = bs_lane(lane);
+    const bool wb = write_back != 0, want = data != nullptr;
+    const uint32_t img = D::OFF_IMG + wave * (uint32_t)IMGW;
+    const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(lds + img));
+    const uint32_t slot = D::OFF_SLOT + wave * (uint32_t)(TBW * 32) + 32u * Ln.blk;
+    const uint32_t row = img + 255u * Ln.blk;
+    const uint8_t* const xpm = tables + L::OFF_XPM;
+    const uint64_t nfull = nblocks / TBW, ntiles = (nblocks + TBW - 1) / TBW;
+    const uint64_t S = (uint64_t)gridDim.x * NW;
+    uint64_t t = (uint64_t)blockIdx.x * NW + wave;
+    auto src_off = [](uint32_t i) { return (int)(16u * i); };
+    if (t < nfull)
+        dma_wave(base, raw + t * (TBW * 255), lane, src_off, raw, nblocks * 255u);
+    for (; t < nfull; t += S) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        uint32_t s[4];
+        bs_cmodg(s, lds, row, Ln);
+        *(uint4*)(lds + slot + 16u * Ln.c) = make_uint4(s[0], s[1], s[2], s[3]); // read by the general path
+        wave_fence();
+        const uint64_t gblk = t * TBW + Ln.blk;
+        const uint32_t st = pair::pair_correct<T2, true, 2, 1>(
+            lds, D::OFF_GF, xpm, row, slot, Ln.c, s, true, raw, gblk, wb, nblocks * 255u);
+        if (status && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
+            status[gblk] = (uint8_t)st;
+        wave_fence(); // corrections patched into the image rows
+        if (want) {
+            uint8_t* dst = data + t * (TBW * K);
+#pragma unroll
+            for (int k = 0; k < KO; ++k) {
+                const uint32_t p = lane + 64u * (uint32_t)k;
+                if (((k + 1) * 64 <= OUT_PIECES || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, data, nblocks * K))
+                    st_nt<NTST>(dst + 16u * p, pair::pair_dec_piece<T2>(lds, img - pair::PAD, p));
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint64_t nx = t + S;
+        if (nx < nfull)
+            dma_wave(base, raw + nx * (TBW * 255), lane, src_off, raw, nblocks * 255u);
+    }
+    if (t == nfull && nfull < ntiles) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t nb = (uint32_t)(nblocks - t * TBW);
+        const uint8_t* src = raw + t * (TBW * 255);
+        if (!PPFS_DBG_OK(src, nb * 255u, raw, nblocks * 255u))
+            return;
+        for (uint32_t j = lane; j < nb * 255u; j += 64u)
+            lds[img + j] = src[j];
+        wave_fence();
+        uint32_t s[4];
+        bs_cmodg(s, lds, row, Ln);
+        *(uint4*)(lds + slot + 16u * Ln.c) = make_uint4(s[0], s[1], s[2], s[3]);
+        wave_fence();
+        const bool valid = Ln.blk < nb;
+        const uint64_t gblk = t * TBW + Ln.blk;
+        const uint32_t st = pair::pair_correct<T2, true, 2, 1>(
+            lds, D::OFF_GF, xpm, row, slot, Ln.c, s, valid, raw, gblk, wb, nblocks * 255u);
+        if (status && valid && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
+            status[gblk] = (uint8_t)st;
+        wave_fence();
+        if (want) {
+            uint8_t* dst = data + t * (TBW * K);
+            const uint32_t nout = nb * (uint32_t)K;
+            for (uint32_t p = lane; 16u * p < nout; p += 64u) {
+                const uint4 v = pair::pair_dec_piece<T2>(lds, img - pair::PAD, p);
+                if (!PPFS_DBG_OK(dst + 16u * p, min(16u, nout - 16u * p), data, nblocks * K))
+                    continue;
+                if (16u * p + 16u <= nout)
+                    *(uint4*)(dst + 16u * p) = v;
+                else
+                    st_bytes(dst + 16u * p, v, nout - 16u * p);
+            }
+        }
+    }
+}
+
+} // namespace bs
+} // namespace ppfs

@@ -2,6 +2,7 @@
 #include "rs_fast.hpp"
 #include "rs_wg.hpp"
 #include "rs_pair.hpp"
+#include "rs_bs.hpp"
 
 #ifndef PPFS_T2
 #error "compile with -DPPFS_T2=<2t>"
@@ -157,6 +158,21 @@ constexpr int DEC_NBUF = DEC_FULL ? 0 : PPFS_WG_DEC_NBUF;
 #ifndef PPFS_PAIR_IMG_WPC
 #define PPFS_PAIR_IMG_WPC (PPFS_PAIR_IMG_NW == 4 ? 4 : 6)
 #endif
+// byte-slice kernels (rs_bs.hpp) for 2t = 32: one workgroup of PPFS_BS_NW waves per CU, each wave
+// on its own 32-block tiles; PPFS_BS_ENC_NBUF image buffers per wave for encode (decode: 1)
+#ifndef PPFS_PAIR_BS
+#define PPFS_PAIR_BS 1
+#endif
+#ifndef PPFS_BS_NW
+#define PPFS_BS_NW 8
+#endif
+#ifndef PPFS_BS_ENC_NW
+#define PPFS_BS_ENC_NW PPFS_BS_NW
+#endif
+#ifndef PPFS_BS_ENC_NBUF
+#define PPFS_BS_ENC_NBUF 1
+#endif
+constexpr bool PAIR_BS = PPFS_PAIR_BS && PPFS_T2 == 32;
 constexpr bool PAIR_IMG = PPFS_PAIR_IMG && (PPFS_T2 % 16 == 0);
 constexpr int PAIR_ENC_WPC = PAIR_IMG ? PPFS_PAIR_IMG_WPC : pair::wpc_of(PPFS_PAIR_ENC), PAIR_DEC_WPC = pair::wpc_of(PPFS_PAIR_DEC);
 #endif
@@ -207,7 +223,10 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
             0, s, d, r, nb, tab);
 #endif
 #elif PPFS_T2 > 16
-    if constexpr (PAIR_IMG)
+    if constexpr (PAIR_BS)
+        hipLaunchKernelGGL((bs::rs_bs_encode_kernel<PPFS_T2, PPFS_BS_ENC_NW, PPFS_BS_ENC_NBUF>),
+            dim3(rs_tile_grid(nb, 1, bs::TBW * PPFS_BS_ENC_NW)), dim3(64 * PPFS_BS_ENC_NW), 0, s, d, r, nb, tab);
+    else if constexpr (PAIR_IMG)
         hipLaunchKernelGGL((pair::rs_pair_encode_img_kernel<PPFS_T2, PPFS_PAIR_IMG_WPC, PPFS_PAIR_IMG_NW>),
             dim3(rs_tile_grid(nb, PAIR_ENC_WPC, 32 * PPFS_PAIR_IMG_NW)), dim3(64 * PPFS_PAIR_IMG_NW), 0, s, d, r, nb, tab);
     else
@@ -239,6 +258,10 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
         0, s, r, d, st, nb, tab, wb);
 #endif
 #elif PPFS_T2 > 16
+    if constexpr (PAIR_BS)
+        hipLaunchKernelGGL((bs::rs_bs_decode_kernel<PPFS_T2, PPFS_BS_NW>), dim3(rs_tile_grid(nb, 1, bs::TBW * PPFS_BS_NW)),
+            dim3(64 * PPFS_BS_NW), 0, s, r, d, st, nb, tab, wb);
+    else
     hipLaunchKernelGGL((pair::rs_pair_decode_kernel<PPFS_T2, PPFS_PAIR_DEC>),
         dim3(rs_tile_grid(nb, PPFS_PAIR_DEC_FULL ? (1 << 24) : PAIR_DEC_WPC)),
         dim3(pair::NTHR), 0, s, r, d, st, nb, tab, wb);

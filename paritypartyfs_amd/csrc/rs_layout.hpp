@@ -55,6 +55,10 @@ constexpr int rs_wg_table_bytes(int t2)
 //        for a zero coefficient -- the remainder of a single error e at byte p is e * row p,
 //        which is how the decoder confirms the single-error case
 //   XPM  the same rows for x^p mod g (decode from c mod g)
+//   BS   byte-slice tables of the rs_bs.hpp kernels (2t = 32), 64 KiB: row v (256 B) holds, in
+//        slot 2q + c (16 B), bytes [16c, 16c+16) of v * x^(2t+q) mod g = SL[2q][v & 15] ^
+//        SL[2q+1][v >> 4] -- the eight byte positions of a chunk side by side, so that lanes
+//        reading distinct slots hit distinct banks whatever byte values they look up
 template <int T2> struct RsPairLayout {
     static_assert(T2 > 16 && T2 <= 32 && (T2 % 2) == 0, "pair RS path: 2t in (16, 32]");
     static constexpr int N = 255, K = N - T2;
@@ -63,9 +67,12 @@ template <int T2> struct RsPairLayout {
     static constexpr int OFF_XP = OFF_GF + GF_BYTES;
     static constexpr int ENC_BYTES = OFF_GF;
     static constexpr int OFF_XPM = OFF_XP + 255 * 32; // rows x^p mod g (decode from c mod g)
-    static constexpr int TABLE_BYTES = OFF_XPM + 255 * 32;
+    static constexpr int OFF_BS = OFF_XPM + 255 * 32;
+    static constexpr int BS_BYTES = 256 * 256;
+    static constexpr int TABLE_BYTES = OFF_BS + BS_BYTES;
+    static_assert(OFF_BS % 16 == 0, "aligned byte-slice tables");
 };
 
-constexpr int rs_pair_table_bytes() { return 16 * 512 + GF_BYTES + 2 * 255 * 32; }
+constexpr int rs_pair_table_bytes() { return 16 * 512 + GF_BYTES + 2 * 255 * 32 + 256 * 256; }
 
 } // namespace ppfs

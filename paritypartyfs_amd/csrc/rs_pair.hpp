@@ -52,9 +52,13 @@ static_assert(col::PAD == 48 && col::BUF == 16464, "emission helpers assume rs_e
 constexpr int PAD = col::PAD, BUF = col::BUF;
 constexpr int wpc_of(int wpc, int nbuf, int = 1, int = 0) { return (void)nbuf, wpc; }
 
-// value of the partner lane (lane ^ 4)
-__device__ __forceinline__ uint32_t pair_xchg(uint32_t v)
+// value of the partner lane: lane ^ 4 (XM = 4, this file's kernels) or lane ^ 1 (XM = 1, the
+// byte-slice kernels of rs_bs.hpp)
+template <int XM = 4> __device__ __forceinline__ uint32_t pair_xchg(uint32_t v)
 {
+    static_assert(XM == 4 || XM == 1, "partner lane");
+    if constexpr (XM == 1)
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false); // quad_perm [1,0,3,2]
     // row_shl:4 writes banks 0 and 2 (lanes with bit 2 clear take lane + 4), row_shr:4 banks 1, 3
     const int x = __builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xF, 0x5, false);
     return (uint32_t)__builtin_amdgcn_update_dpp(x, (int)v, 0x114, 0xF, 0xA, false);
@@ -190,7 +194,7 @@ __device__ __forceinline__ void pair_remainder(uint32_t (&s)[4], const uint8_t* 
     }
 }
 
-__device__ __forceinline__ uint32_t pair_or(uint32_t v) { return v | pair_xchg(v); }
+template <int XM = 4> __device__ __forceinline__ uint32_t pair_or(uint32_t v) { return v | pair_xchg<XM>(v); }
 
 // General correction (2+ errors), out of line; both lanes of the pair: lane c computes S_i for
 // i = 16c+1 .. 16c+16 into the block's slot (over r', which both lanes have read), then lane 0
@@ -238,12 +242,12 @@ __device__ __noinline__ void pair_correct_general(uint8_t* lds, uint32_t goff, u
 
 // Decode correction for the pair's block; s = the lane's column of r' = x^2t c(x) mod g.  Single
 // error: S_1, S_2 -> X = S_2/S_1, e = S_1/X, confirmed iff r' == e * XP row LOG X.
-template <int T2, bool RM = false, int TAG = 0>
+template <int T2, bool RM = false, int TAG = 0, int XM = 4>
 __device__ __forceinline__ uint32_t pair_correct(uint8_t* lds, uint32_t goff, const uint8_t* __restrict__ xp, uint32_t row,
     uint32_t slot,
     uint32_t c, const uint32_t (&s)[4], bool valid, uint8_t* __restrict__ raw_g, uint64_t gblk, bool wb, uint64_t raw_bytes)
 {
-    const bool err = valid && pair_or(s[0] | s[1] | s[2] | s[3]) != 0u;
+    const bool err = valid && pair_or<XM>(s[0] | s[1] | s[2] | s[3]) != 0u;
     if (!__builtin_amdgcn_ballot_w64(err))
         return 0u;
     const Gf gf { lds + goff };
@@ -258,8 +262,8 @@ __device__ __forceinline__ uint32_t pair_correct(uint8_t* lds, uint32_t goff, co
         s1 ^= rb ? v1 : 0u;
         s2 ^= rb ? v2 : 0u;
     }
-    s1 ^= pair_xchg(s1);
-    s2 ^= pair_xchg(s2);
+    s1 ^= pair_xchg<XM>(s1);
+    s2 ^= pair_xchg<XM>(s2);
     const uint32_t l1 = gf.log(s1), l2 = gf.log(s2);
     uint32_t lx = l2 + 255u - l1;
     lx = lx >= 255u ? lx - 255u : lx;
@@ -275,7 +279,7 @@ __device__ __forceinline__ uint32_t pair_correct(uint8_t* lds, uint32_t goff, co
         const uint32_t ev = x == 0xFFu ? 0u : gf.exp(le + x);
         bad |= ev != rb ? 1u : 0u;
     }
-    const bool geo = err && pair_or(bad) == 0u;
+    const bool geo = err && pair_or<XM>(bad) == 0u;
     if (geo && c == 0)
         col_fix(lds, row, raw_g, gblk, wb, lx, gf.exp(le), raw_bytes);
     if (err && !geo)

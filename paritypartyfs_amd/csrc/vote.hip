@@ -108,6 +108,59 @@ extern "C" hipError_t ppfs_copy_launch(uint8_t* dst, const uint8_t* src, uint64_
     return hipGetLastError();
 }
 
+// ---- fault injection: one byte per block (bench step, tests) ----
+// Block b of a raw image at `stride` bytes per block gets byte pos[b] replaced by val[b] (mode 0)
+// or XORed with it (mode 1); pos[b] >= stride skips the block.  The counterpart of the
+// reference's bit flipper (usage_simulator/simulation/src/bit_flipper.cpp), used by bench.py to
+// corrupt every codeword of a step: torch's index_put_ of the same bytes reads 8-byte indices and
+// costs ~2x this kernel.  Each thread takes 4 consecutive blocks: one
+// 4-byte load of their positions and one of their values, then four byte stores.
+namespace ppfs {
+template <int MODE>
+__global__ __launch_bounds__(256) void inject_kernel(uint8_t* __restrict__ raw, uint64_t stride, uint64_t nblocks,
+    const uint8_t* __restrict__ pos, const uint8_t* __restrict__ val)
+{
+    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, b0 = 4 * q;
+    if (b0 >= nblocks)
+        return;
+    uint32_t p4, v4;
+    if (b0 + 4 <= nblocks && ((uintptr_t)(pos + b0) & 3u) == 0 && ((uintptr_t)(val + b0) & 3u) == 0) {
+        p4 = *(const uint32_t*)(pos + b0);
+        v4 = *(const uint32_t*)(val + b0);
+    } else {
+        p4 = v4 = 0xFFFFFFFFu;
+        for (uint64_t j = 0; j < 4 && b0 + j < nblocks; ++j) {
+            p4 = (p4 & ~(0xFFu << (8 * j))) | ((uint32_t)pos[b0 + j] << (8 * j));
+            v4 = (v4 & ~(0xFFu << (8 * j))) | ((uint32_t)val[b0 + j] << (8 * j));
+        }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t p = (p4 >> (8 * j)) & 0xFFu;
+        if (b0 + j >= nblocks || p >= stride)
+            continue;
+        uint8_t* d = raw + (b0 + j) * stride + p;
+        const uint8_t v = (uint8_t)(v4 >> (8 * j));
+        *d = MODE == 0 ? v : (uint8_t)(*d ^ v);
+    }
+}
+} // namespace ppfs
+
+extern "C" hipError_t ppfs_inject_launch(uint8_t* raw, uint64_t stride, uint64_t nblocks, const uint8_t* pos,
+    const uint8_t* val, int mode, hipStream_t s)
+{
+    if (nblocks == 0)
+        return hipSuccess;
+    const uint64_t grid = ((nblocks + 3) / 4 + 255) / 256;
+    if (grid > 0x7FFFFFFFull)
+        return hipErrorInvalidValue;
+    if (mode == 0)
+        hipLaunchKernelGGL(ppfs::inject_kernel<0>, dim3((uint32_t)grid), dim3(256), 0, s, raw, stride, nblocks, pos, val);
+    else
+        hipLaunchKernelGGL(ppfs::inject_kernel<1>, dim3((uint32_t)grid), dim3(256), 0, s, raw, stride, nblocks, pos, val);
+    return hipGetLastError();
+}
+
 // Completion flag of the small-batch launch path (api.cpp wait_flag): queued after a call's
 // kernels on the same stream, it makes their outputs visible system-wide and stores `v` (release)
 // into host-coherent memory, where the host spins on it.  Cheaper than hipStreamSynchronize's

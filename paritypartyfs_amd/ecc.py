@@ -281,9 +281,24 @@ def device_copy(dst, src, nbytes: Optional[int] = None, stream=None) -> None:
     check(lib().ppfs_copy_device(_ptr(dst), _ptr(src), n, _stream_handle(stream)))
 
 
+def inject_bytes(raw, stride: int, pos, val, nblocks: Optional[int] = None, xor: bool = False, stream=None) -> None:
+    """Corrupt one byte per block of a device raw image (torch uint8 tensors): block b's byte
+    pos[b] becomes val[b] (or byte ^ val[b] with xor=True); pos[b] >= stride skips the block.
+    bench.py's fault injection (not part of the reference interface; the reference's bit flipper,
+    usage_simulator/simulation/src/bit_flipper.cpp, is a simulator and out of scope)."""
+    nb = int(pos.numel() if nblocks is None else nblocks)
+    for name, t in (("raw", raw), ("pos", pos), ("val", val)):
+        if not t.is_cuda or t.element_size() != 1 or not t.is_contiguous():
+            raise ValueError(f"inject_bytes: {name} must be a contiguous CUDA uint8 tensor")
+    if stride <= 0 or nb > pos.numel() or nb > val.numel() or nb * stride > raw.numel():
+        raise ValueError("inject_bytes: a buffer is shorter than nblocks implies")
+    check(lib().ppfs_inject_device(_ptr(raw), stride, nb, _ptr(pos), _ptr(val), 1 if xor else 0,
+                                   _stream_handle(stream)))
+
+
 def crc_implicit_to_explicit(p: int) -> int:
     """CrcPolynomial::MsgImplicit (crc_polynomial.cpp:41-54) -> explicit form."""
     return int(lib().ppfs_ecc_crc_implicit_to_explicit(ctypes.c_uint64(p)))
 
 
-__all__ = ["EccEngine", "crc_implicit_to_explicit", "device_copy", "pinned", "vote3", "vote3_host", "_native"]
+__all__ = ["EccEngine", "crc_implicit_to_explicit", "device_copy", "inject_bytes", "pinned", "vote3", "vote3_host", "_native"]

@@ -173,3 +173,32 @@ def test_debug_bounds_checks_positive_control():
         assert n == -1
     else:
         assert n >= 1, n
+
+
+@pytest.mark.parametrize("nb,stride,xor", [(1, 255, False), (5, 255, True), (1 << 16, 255, False),
+                                           (4099, 249, True), (1003, 4096, False)])
+def test_inject_bytes_matches_index_put(nb, stride, xor):
+    """bench.py's fault injection (ppfs_inject_device): one byte per block, set or XOR, equal to
+    torch's indexing of the same bytes; positions >= stride leave their block untouched; ragged
+    block counts (not a multiple of the kernel's 4 blocks per thread) and an offset (unaligned)
+    position array."""
+    from paritypartyfs_amd import inject_bytes
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(nb)
+    raw = torch.randint(0, 256, (nb * stride,), dtype=torch.uint8, device=dev, generator=g)
+    pos_all = torch.randint(0, 256, (nb + 1,), dtype=torch.uint8, device=dev, generator=g)
+    pos = pos_all[1:]  # 1-byte offset: the kernel's unaligned path
+    val = torch.randint(1, 256, (nb,), dtype=torch.uint8, device=dev, generator=g)
+    want = raw.clone().view(nb, stride)
+    p = pos.long()
+    keep = p < stride
+    rows = torch.arange(nb, device=dev)[keep]
+    cols = p[keep]
+    want[rows, cols] = (want[rows, cols] ^ val[keep]) if xor else val[keep]
+    inject_bytes(raw, stride, pos, val, xor=xor)
+    torch.cuda.synchronize()
+    assert torch.equal(raw.view(nb, stride), want)
+    with pytest.raises(ValueError):
+        inject_bytes(raw, stride, pos, val, nblocks=nb + 1)

@@ -27,7 +27,11 @@ def main():
     col2 = col.view(nb, 1)
     bad2 = bad.view(nb, 1)
     rows = torch.arange(nb, device=dev)
+    from paritypartyfs_amd import inject_bytes
+
+    col8 = col.to(torch.uint8)
     forms = {
+        "ppfs_inject": lambda: inject_bytes(cw, n, col8, bad),
         "index_put_int64": lambda: cw.index_put_((pos,), bad),
         "scatter_dim1": lambda: v2.scatter_(1, col2, bad2),
         "adv_index_2d": lambda: v2.index_put_((rows, col), bad),
