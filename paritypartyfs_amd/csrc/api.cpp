@@ -308,6 +308,18 @@ std::vector<uint8_t> build_rs_pair_tables(int t2)
                 for (int k = 0; k < 16; ++k)
                     bs[v * 256 + (2 * q + c) * 16 + k] = out[(size_t)(2 * q) * 512 + (size_t)c * 256 + (size_t)(v & 15) * 16 + k]
                         ^ out[(size_t)(2 * q + 1) * 512 + (size_t)c * 256 + (size_t)(v >> 4) * 16 + k];
+    // S_1, S_2 contributions of the c mod g state bytes (rs_bs.hpp bs_correct; coefficient q of
+    // the state is byte 32 - 2t + q, exponent i q)
+    uint8_t* s12 = bs + 256 * 256;
+    for (int u = 0; u < 32; ++u) {
+        const int q = u - (32 - t2);
+        for (int v = 0; v < 256; ++v) {
+            if (q < 0)
+                continue;
+            s12[u * 512 + 2 * v] = G.mul((uint8_t)v, G.exp[q % 255]);
+            s12[u * 512 + 2 * v + 1] = G.mul((uint8_t)v, G.exp[(2 * q) % 255]);
+        }
+    }
     return out;
 }
 

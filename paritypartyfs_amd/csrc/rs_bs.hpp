@@ -155,6 +155,48 @@ __device__ __forceinline__ void bs_cmodg(uint32_t (&s)[4], const uint8_t* lds, u
         s[m] ^= __builtin_amdgcn_alignbit(d[m + 1], d[m], sh);
 }
 
+// Decode correction for the pair's block: rs_pair.hpp pair_correct (single error: X = S_2/S_1,
+// e = S_1/X, confirmed iff c mod g == e * (x^p mod g); else the general path), with S_1 and S_2
+// read from the S12 byte table -- 16 lookups per lane where the log / exp forms took 48.
+template <int T2, int TAG = 2>
+__device__ __forceinline__ uint32_t bs_correct(uint8_t* lds, uint32_t goff, uint32_t s12off, const uint8_t* __restrict__ xp,
+    uint32_t row, uint32_t slot, uint32_t c, const uint32_t (&s)[4], bool valid, uint8_t* __restrict__ raw_g, uint64_t gblk,
+    bool wb, uint64_t raw_bytes)
+{
+    const bool err = valid && pair::pair_or<1>(s[0] | s[1] | s[2] | s[3]) != 0u;
+    if (!__builtin_amdgcn_ballot_w64(err))
+        return 0u;
+    const Gf gf { lds + goff };
+    const uint16_t* t = (const uint16_t*)(lds + s12off + 8192u * c); // state byte u = 16c + k
+    uint32_t s12 = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        s12 ^= t[256 * k + ((s[k >> 2] >> (8 * (k & 3))) & 0xFFu)];
+    s12 ^= pair::pair_xchg<1>(s12);
+    const uint32_t s1 = s12 & 0xFFu, s2 = s12 >> 8;
+    const uint32_t l1 = gf.log(s1), l2 = gf.log(s2);
+    uint32_t lx = l2 + 255u - l1;
+    lx = lx >= 255u ? lx - 255u : lx;
+    uint32_t le = l1 + 255u - lx;
+    le = le >= 255u ? le - 255u : le;
+    const uint4 xr = *(const uint4*)(xp + 32u * lx + 16u * c); // XP rows stay in global memory (L2)
+    const uint32_t xw[4] = { xr.x, xr.y, xr.z, xr.w };
+    uint32_t bad = (s1 == 0u || s2 == 0u) ? 1u : 0u;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t x = (xw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+        const uint32_t rb = (s[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+        const uint32_t ev = x == 0xFFu ? 0u : gf.exp(le + x);
+        bad |= ev != rb ? 1u : 0u;
+    }
+    const bool geo = err && pair::pair_or<1>(bad) == 0u;
+    if (geo && c == 0)
+        col::col_fix(lds, row, raw_g, gblk, wb, lx, gf.exp(le), raw_bytes);
+    if (err && !geo)
+        pair::pair_correct_general<T2, true, TAG>(lds, goff, row, slot, c, raw_g, gblk, wb, raw_bytes);
+    return err ? 1u : 0u;
+}
+
 // LDS-DMA of a wave tile: image piece i = lane + 64 k lands at img + 16 i; its source is
 // src + src_off(i) (-1: nothing to load)
 template <typename F>
@@ -170,6 +212,36 @@ __device__ __forceinline__ void dma_wave(uint32_t img_base, const uint8_t* __res
     }
 }
 
+// Register prefetch of a wave tile (NBUF = 0): piece i = lane + 64 k into pf[k] with plain
+// 16-byte loads (compiler-counted), written into the image once the previous tile's emission has
+// read it -- a whole tile of compute covers the loads, with no second LDS image.
+template <typename F>
+__device__ __forceinline__ void load_wave(u32x4 (&pf)[KP], const uint8_t* __restrict__ src, uint32_t lane, F src_off,
+    [[maybe_unused]] const uint8_t* gbase, [[maybe_unused]] uint64_t extent)
+{
+    // every lane loads (pieces past the image or with no source re-read a piece of the tile), so
+    // that pf stays in registers
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+        const uint32_t i = lane + 64u * (uint32_t)k;
+        int so = src_off(i < (uint32_t)IMG_PIECES ? i : (uint32_t)IMG_PIECES - 1u);
+        so = so >= 0 ? so : 0;
+        if (PPFS_DBG_OK(src + so, 16, gbase, extent))
+            pf[k] = *(const u32x4*)(src + so);
+    }
+}
+
+template <typename F>
+__device__ __forceinline__ void put_wave(uint8_t* lds, uint32_t img, const u32x4 (&pf)[KP], uint32_t lane, F src_off)
+{
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+        const uint32_t i = lane + 64u * (uint32_t)k;
+        if (((k + 1) * 64 <= IMG_PIECES || i < (uint32_t)IMG_PIECES) && src_off(i) >= 0)
+            *(u32x4*)(lds + img + 16u * i) = pf[k];
+    }
+}
+
 // the lane's 16 parity bytes into the image gap [255 blk + 16 c, +16)
 __device__ __forceinline__ void put_parity(uint8_t* lds, uint32_t img, const BsLane& L, const uint32_t (&s)[4])
 {
@@ -179,27 +251,30 @@ __device__ __forceinline__ void put_parity(uint8_t* lds, uint32_t img, const BsL
         gap[k] = (uint8_t)(s[k >> 2] >> (8 * (k & 3)));
 }
 
-// LDS plan: [0, 64 KiB) byte-slice tables | (decode: GF block, NW x 1 KiB syndrome slots) |
+// LDS plan: [0, 64 KiB) byte-slice tables | (decode: GF block, S12 table, NW x 1 KiB syndrome
+// slots) |
 // NW x NBUF wave images | 64 B slack (the rows' last-word reads and the decode emission's second
 // window run past the last image)
 template <int NW, int NBUF, bool DEC> struct BsLds {
     static constexpr int OFF_GF = TAB_BYTES;
-    static constexpr int OFF_SLOT = OFF_GF + (DEC ? GF_BYTES : 0);
+    static constexpr int OFF_S12 = OFF_GF + (DEC ? GF_BYTES : 0);
+    static constexpr int OFF_SLOT = OFF_S12 + (DEC ? 32 * 256 * 2 : 0);
     static constexpr int OFF_IMG = OFF_SLOT + (DEC ? NW * TBW * 32 : 0);
-    static constexpr int BYTES = OFF_IMG + NW * NBUF * IMGW + 64;
+    static constexpr int BYTES = OFF_IMG + NW * (NBUF > 0 ? NBUF : 1) * IMGW + 64;
     static_assert(BYTES <= 163840, "one workgroup per CU: 160 KiB of LDS");
     static_assert(OFF_IMG % 16 == 0 && IMGW % 16 == 0, "aligned images");
 };
 
 // Encode: 2^k payloads -> codewords.  Workgroup b's wave w takes wave tiles b NW + w + j S
 // (S = grid NW).  NBUF = 1: a wave DMAs its next tile once its emission has read the image;
-// NBUF = 2: the next tile is DMA'd at the top of the iteration into the other buffer.
+// NBUF = 2: the next tile is DMA'd at the top of the iteration into the other buffer; NBUF = 0:
+// register prefetch (load_wave / put_wave).
 template <int T2, int NW, int NBUF, int NTST = 1>
 __global__ __launch_bounds__(64 * NW, 1) void rs_bs_encode_kernel(const uint8_t* __restrict__ data,
     uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables)
 {
     static_assert(T2 == 32, "byte-slice path: 2t = 32 (image pieces need 16 | 2t, state byte q = coefficient q)");
-    static_assert(NBUF == 1 || NBUF == 2, "NBUF");
+    static_assert(NBUF >= 0 && NBUF <= 2, "NBUF");
     using L = RsPairLayout<T2>;
     using D = BsLds<NW, NBUF, false>;
     constexpr int K = L::K;
@@ -209,15 +284,22 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_encode_kernel(const uint8_t*
         *(uint4*)(lds + OFF_TAB + 16 * p) = *(const uint4*)(tables + L::OFF_BS + 16 * p);
     __syncthreads();
     const BsLane Ln = bs_lane(lane);
-    const uint32_t img0 = D::OFF_IMG + wave * (uint32_t)(NBUF * IMGW);
+    const uint32_t img0 = D::OFF_IMG + wave * (uint32_t)((NBUF > 0 ? NBUF : 1) * IMGW);
     const uint32_t base0 = __builtin_amdgcn_readfirstlane(lds_addr(lds + img0));
     const uint64_t nfull = nblocks / TBW, ntiles = (nblocks + TBW - 1) / TBW;
     const uint64_t S = (uint64_t)gridDim.x * NW;
     uint64_t t = (uint64_t)blockIdx.x * NW + wave;
     auto src_off = [](uint32_t i) { return pair::img_src<T2>(i); };
     const uint8_t* const dextent = data;
-    if (t < nfull)
-        dma_wave(base0, data + t * (TBW * K), lane, src_off, dextent, nblocks * K);
+    [[maybe_unused]] u32x4 pf[KP];
+    if (t < nfull) {
+        if constexpr (NBUF == 0) {
+            load_wave(pf, data + t * (TBW * K), lane, src_off, dextent, nblocks * K);
+            put_wave(lds, img0, pf, lane, src_off);
+        } else {
+            dma_wave(base0, data + t * (TBW * K), lane, src_off, dextent, nblocks * K);
+        }
+    }
     uint32_t cur = 0;
     bool first = true;
     for (; t < nfull; t += S) {
@@ -238,8 +320,11 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_encode_kernel(const uint8_t*
                 else
                     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             }
-        } else {
+        } else if constexpr (NBUF == 1) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            if (nx < nfull)
+                load_wave(pf, data + nx * (TBW * K), lane, src_off, dextent, nblocks * K);
         }
         first = false;
         uint32_t s[4];
@@ -256,8 +341,11 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_encode_kernel(const uint8_t*
         if constexpr (NBUF == 1) {
             if (nx < nfull)
                 dma_wave(base0, data + nx * (TBW * K), lane, src_off, dextent, nblocks * K);
-        } else {
+        } else if constexpr (NBUF == 2) {
             cur ^= 1u;
+        } else {
+            if (nx < nfull)
+                put_wave(lds, img0, pf, lane, src_off);
         }
     }
     if (t == nfull && nfull < ntiles) {
@@ -297,14 +385,14 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_encode_kernel(const uint8_t*
 // of line); corrections patch the image row and, with write-back, the codeword byte in HBM; the
 // payload pieces come straight from the image.  Single-buffered: the correction path's XP-row
 // loads are compiler-counted, and their waits would drain a prefetch.
-template <int T2, int NW, int NTST = 1>
+template <int T2, int NW, int NBUF = 1, int NTST = 1>
 __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __restrict__ raw,
     uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables,
     int write_back)
 {
     static_assert(T2 == 32, "byte-slice path: 2t = 32");
     using L = RsPairLayout<T2>;
-    using D = BsLds<NW, 1, true>;
+    using D = BsLds<NW, NBUF, true>;
     constexpr int K = L::K;
     constexpr int OUT_PIECES = TBW * K / 16; // 446
     constexpr int KO = (OUT_PIECES + 63) / 64;
@@ -314,6 +402,8 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
         *(uint4*)(lds + OFF_TAB + 16 * p) = *(const uint4*)(tables + L::OFF_BS + 16 * p);
     for (uint32_t p = tid; p < (uint32_t)GF_BYTES / 16; p += 64u * NW)
         *(uint4*)(lds + D::OFF_GF + 16 * p) = *(const uint4*)(tables + L::OFF_GF + 16 * p);
+    for (uint32_t p = tid; p < (uint32_t)L::S12_BYTES / 16; p += 64u * NW)
+        *(uint4*)(lds + D::OFF_S12 + 16 * p) = *(const uint4*)(tables + L::OFF_S12 + 16 * p);
     __syncthreads();
     const BsLane Ln = bs_lane(lane);
     const bool wb = write_back != 0, want = data != nullptr;
@@ -326,17 +416,30 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
     const uint64_t S = (uint64_t)gridDim.x * NW;
     uint64_t t = (uint64_t)blockIdx.x * NW + wave;
     auto src_off = [](uint32_t i) { return (int)(16u * i); };
-    if (t < nfull)
-        dma_wave(base, raw + t * (TBW * 255), lane, src_off, raw, nblocks * 255u);
+    [[maybe_unused]] u32x4 pf[KP];
+    if (t < nfull) {
+        if constexpr (NBUF == 0) {
+            load_wave(pf, raw + t * (TBW * 255), lane, src_off, raw, nblocks * 255u);
+            put_wave(lds, img, pf, lane, src_off);
+        } else {
+            dma_wave(base, raw + t * (TBW * 255), lane, src_off, raw, nblocks * 255u);
+        }
+    }
     for (; t < nfull; t += S) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint64_t nx = t + S;
+        if constexpr (NBUF == 0) {
+            if (nx < nfull)
+                load_wave(pf, raw + nx * (TBW * 255), lane, src_off, raw, nblocks * 255u);
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         uint32_t s[4];
         bs_cmodg(s, lds, row, Ln);
         *(uint4*)(lds + slot + 16u * Ln.c) = make_uint4(s[0], s[1], s[2], s[3]); // read by the general path
         wave_fence();
         const uint64_t gblk = t * TBW + Ln.blk;
-        const uint32_t st = pair::pair_correct<T2, true, 2, 1>(
-            lds, D::OFF_GF, xpm, row, slot, Ln.c, s, true, raw, gblk, wb, nblocks * 255u);
+        const uint32_t st = bs_correct<T2>(
+            lds, D::OFF_GF, D::OFF_S12, xpm, row, slot, Ln.c, s, true, raw, gblk, wb, nblocks * 255u);
         if (status && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
             status[gblk] = (uint8_t)st;
         wave_fence(); // corrections patched into the image rows
@@ -350,9 +453,12 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const uint64_t nx = t + S;
-        if (nx < nfull)
-            dma_wave(base, raw + nx * (TBW * 255), lane, src_off, raw, nblocks * 255u);
+        if (nx < nfull) {
+            if constexpr (NBUF == 0)
+                put_wave(lds, img, pf, lane, src_off);
+            else
+                dma_wave(base, raw + nx * (TBW * 255), lane, src_off, raw, nblocks * 255u);
+        }
     }
     if (t == nfull && nfull < ntiles) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -369,8 +475,8 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
         wave_fence();
         const bool valid = Ln.blk < nb;
         const uint64_t gblk = t * TBW + Ln.blk;
-        const uint32_t st = pair::pair_correct<T2, true, 2, 1>(
-            lds, D::OFF_GF, xpm, row, slot, Ln.c, s, valid, raw, gblk, wb, nblocks * 255u);
+        const uint32_t st = bs_correct<T2>(
+            lds, D::OFF_GF, D::OFF_S12, xpm, row, slot, Ln.c, s, valid, raw, gblk, wb, nblocks * 255u);
         if (status && valid && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
             status[gblk] = (uint8_t)st;
         wave_fence();

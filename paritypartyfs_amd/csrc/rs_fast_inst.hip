@@ -167,10 +167,13 @@ constexpr int DEC_NBUF = DEC_FULL ? 0 : PPFS_WG_DEC_NBUF;
 #define PPFS_BS_NW 8
 #endif
 #ifndef PPFS_BS_ENC_NW
-#define PPFS_BS_ENC_NW PPFS_BS_NW
+#define PPFS_BS_ENC_NW 12 // 3 waves per SIMD (decode: PPFS_BS_NW = 8, LDS- and register-bound)
 #endif
 #ifndef PPFS_BS_ENC_NBUF
 #define PPFS_BS_ENC_NBUF 1
+#endif
+#ifndef PPFS_BS_DEC_NBUF
+#define PPFS_BS_DEC_NBUF 1 // 0 = register prefetch
 #endif
 constexpr bool PAIR_BS = PPFS_PAIR_BS && PPFS_T2 == 32;
 constexpr bool PAIR_IMG = PPFS_PAIR_IMG && (PPFS_T2 % 16 == 0);
@@ -259,7 +262,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
 #endif
 #elif PPFS_T2 > 16
     if constexpr (PAIR_BS)
-        hipLaunchKernelGGL((bs::rs_bs_decode_kernel<PPFS_T2, PPFS_BS_NW>), dim3(rs_tile_grid(nb, 1, bs::TBW * PPFS_BS_NW)),
+        hipLaunchKernelGGL((bs::rs_bs_decode_kernel<PPFS_T2, PPFS_BS_NW, PPFS_BS_DEC_NBUF>), dim3(rs_tile_grid(nb, 1, bs::TBW * PPFS_BS_NW)),
             dim3(64 * PPFS_BS_NW), 0, s, r, d, st, nb, tab, wb);
     else
     hipLaunchKernelGGL((pair::rs_pair_decode_kernel<PPFS_T2, PPFS_PAIR_DEC>),

@@ -59,6 +59,8 @@ constexpr int rs_wg_table_bytes(int t2)
 //        slot 2q + c (16 B), bytes [16c, 16c+16) of v * x^(2t+q) mod g = SL[2q][v & 15] ^
 //        SL[2q+1][v >> 4] -- the eight byte positions of a chunk side by side, so that lanes
 //        reading distinct slots hit distinct banks whatever byte values they look up
+//   S12  the rs_bs.hpp decode's first two syndromes from c mod g, 16 KiB: entry (u, v) (2 B at
+//        512 u + 2 v) = v alpha^u | (v alpha^(2u)) << 8, the contribution of state byte u = v
 template <int T2> struct RsPairLayout {
     static_assert(T2 > 16 && T2 <= 32 && (T2 % 2) == 0, "pair RS path: 2t in (16, 32]");
     static constexpr int N = 255, K = N - T2;
@@ -69,10 +71,12 @@ template <int T2> struct RsPairLayout {
     static constexpr int OFF_XPM = OFF_XP + 255 * 32; // rows x^p mod g (decode from c mod g)
     static constexpr int OFF_BS = OFF_XPM + 255 * 32;
     static constexpr int BS_BYTES = 256 * 256;
-    static constexpr int TABLE_BYTES = OFF_BS + BS_BYTES;
+    static constexpr int OFF_S12 = OFF_BS + BS_BYTES;
+    static constexpr int S12_BYTES = 32 * 256 * 2;
+    static constexpr int TABLE_BYTES = OFF_S12 + S12_BYTES;
     static_assert(OFF_BS % 16 == 0, "aligned byte-slice tables");
 };
 
-constexpr int rs_pair_table_bytes() { return 16 * 512 + GF_BYTES + 2 * 255 * 32 + 256 * 256; }
+constexpr int rs_pair_table_bytes() { return 16 * 512 + GF_BYTES + 2 * 255 * 32 + 256 * 256 + 32 * 256 * 2; }
 
 } // namespace ppfs
