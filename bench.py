@@ -513,6 +513,10 @@ def main(argv=None):
         kn = eng.kernel_name
         if kn.startswith("rs255-wg"):
             return f"rs_wg_{which}_kernel<{n - k}>"
+        if kn.startswith("rs255-bs"):  # 2t = 32 (rs_bs.hpp)
+            return f"rs_bs_{which}_kernel<{n - k}>"
+        if kn.startswith("rs255-w1"):  # 2t <= 8, wave-independent ablation (rs_w1.hpp)
+            return f"rs_w1_{which}_kernel<{n - k}>"
         if kn.startswith("rs255-pair"):  # 16 < 2t <= 32 (rs_pair.hpp)
             return f"rs_pair_{'decode' if which == 'decode' else 'encode_img'}_kernel<{n - k}>"
         if kn.startswith("rs255-slice8") and which == "encode" and n - k == 16:

@@ -31,6 +31,7 @@ extern "C" {
 int ppfs_rs_fast_supported(int n, int t2);
 int ppfs_rs_fast_tables_bytes(int t2);
 hipError_t ppfs_rs_fast_encode(int t2, const uint8_t* d, uint8_t* r, uint64_t nb, const uint8_t* tab, hipStream_t s);
+const char* ppfs_rs_fast_path(int t2);
 hipError_t ppfs_flag_launch(uint32_t* flag, uint32_t v, hipStream_t s);
 hipError_t ppfs_rs_generic_server_launch(int n, int t2, ppfs::SrvBox* box, uint8_t* zc, uint64_t zc_bytes,
     const uint8_t* tab, uint32_t gen, uint32_t idle_us, hipStream_t s);
@@ -524,7 +525,7 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
         tables.resize(4096 + 8192 + 1024, 0);
         if (c->rs_fast) {
             tables = build_rs_fast_tables(c->rs_t2);
-            c->kname = c->rs_t2 <= 8 ? "rs255-wg-seg4-lds" : (c->rs_t2 <= 16 ? "rs255-slice8-lds" : "rs255-pair-nibble-lds");
+            c->kname = ppfs_rs_fast_path(c->rs_t2);
         } else {
             tables.assign(1024 + 256, 0);
             build_gf_block(tables.data());

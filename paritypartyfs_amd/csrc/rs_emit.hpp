@@ -116,7 +116,7 @@ __device__ __forceinline__ void col_fix(uint8_t* lds, uint32_t row, uint8_t* __r
     const uint8_t fixed = (uint8_t)(lds[row + pos] ^ ev);
     lds[row + pos] = fixed;
     if (wb && PPFS_DBG_OK(raw_g + gblk * 255u + pos, 1, raw_g, raw_bytes))
-        raw_g[gblk * 255u + pos] = fixed;
+        wb_byte(raw_g + gblk * 255u + pos, fixed);
 }
 
 } // namespace col

@@ -3,6 +3,7 @@
 #include "rs_wg.hpp"
 #include "rs_pair.hpp"
 #include "rs_bs.hpp"
+#include "rs_w1.hpp"
 
 #ifndef PPFS_T2
 #error "compile with -DPPFS_T2=<2t>"
@@ -121,6 +122,23 @@ constexpr int DEC_NBUF = DEC_FULL ? 0 : PPFS_WG_DEC_NBUF;
 #if PPFS_WG_ENC_W8 || PPFS_WG_DYN
 #include "rs_wg_ablate.hpp"
 #endif
+// wave-independent kernels (rs_w1.hpp): one workgroup of PPFS_W1_NW waves per CU, every wave on
+// its own 64-block tiles; PPFS_W1_NBUF 1 = LDS-DMA, 0 = register prefetch
+#ifndef PPFS_WG_W1
+#define PPFS_WG_W1 0
+#endif
+#ifndef PPFS_W1_NW
+#define PPFS_W1_NW 8
+#endif
+#ifndef PPFS_W1_DEC_NW
+#define PPFS_W1_DEC_NW 8
+#endif
+#ifndef PPFS_W1_NBUF
+#define PPFS_W1_NBUF 1
+#endif
+#ifndef PPFS_W1_DEC_NBUF
+#define PPFS_W1_DEC_NBUF PPFS_W1_NBUF
+#endif
 #ifndef PPFS_ENC_MODE
 #define PPFS_ENC_MODE 3 // ablation builds only: rs_wg.hpp MODE bits (remainder / codeword emission)
 #endif
@@ -218,7 +236,10 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
     hipLaunchKernelGGL((wg::rs_wg_encode8_kernel<PPFS_T2, (PPFS_T2 > 6 ? 3 : PPFS_WG_ENC_W8), 2, PPFS_ENC_NTST>),
         dim3(rs_tile_grid(nb, 2)), dim3(512), 0, s, d, r, nb, tab);
 #else
-    if constexpr (PPFS_WG_ENC_IMG)
+    if constexpr (PPFS_WG_W1 & 1)
+        hipLaunchKernelGGL((w1::rs_w1_encode_kernel<PPFS_T2, PPFS_W1_NW, PPFS_W1_NBUF, PPFS_ENC_MODE, PPFS_ENC_NTST>),
+            dim3(rs_tile_grid(nb, 1, w1::TB * PPFS_W1_NW)), dim3(64 * PPFS_W1_NW), 0, s, d, r, nb, tab);
+    else if constexpr (PPFS_WG_ENC_IMG)
         hipLaunchKernelGGL((wg::rs_wg_encode_img_kernel<PPFS_T2, PPFS_WG_ENC_IMG_WPC, PPFS_ENC_NTST>),
             dim3(rs_tile_grid(nb, 1 << 24)), dim3(256), 0, s, d, r, nb, tab);
     else
@@ -245,6 +266,17 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
     return hipGetLastError();
 }
 
+extern "C" const char* PPFS_CAT(ppfs_rs_fast_path_t, PPFS_T2)()
+{
+#if PPFS_T2 <= 8
+    return (PPFS_WG_W1 & 1) ? "rs255-w1-lds" : "rs255-wg-seg4-lds";
+#elif PPFS_T2 > 16
+    return PAIR_BS ? "rs255-bs-byte-lds" : "rs255-pair-nibble-lds";
+#else
+    return "rs255-slice8-lds";
+#endif
+}
+
 extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb,
     const uint8_t* tab, int wb, hipStream_t s)
 {
@@ -257,6 +289,10 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
         hipLaunchKernelGGL((wg::rs_wg_decode_rp_kernel<PPFS_T2, PPFS_WG_RP, PPFS_DEC_NTST, false>),
             dim3(rs_tile_grid(nb, PPFS_WG_RP)), dim3(256), 0, s, r, d, st, nb, tab, wb);
 #else
+    if constexpr (PPFS_WG_W1 & 2)
+        hipLaunchKernelGGL((w1::rs_w1_decode_kernel<PPFS_T2, PPFS_W1_DEC_NW, PPFS_W1_DEC_NBUF, PPFS_DEC_NTST>),
+            dim3(rs_tile_grid(nb, 1, w1::TB * PPFS_W1_DEC_NW)), dim3(64 * PPFS_W1_DEC_NW), 0, s, r, d, st, nb, tab, wb);
+    else
     hipLaunchKernelGGL((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC, PPFS_DEC_MODE, PPFS_DEC_NTST>), dim3(rs_tile_grid(nb, DEC_FULL ? (1 << 24) : DEC_WPC)), dim3(256),
         0, s, r, d, st, nb, tab, wb);
 #endif

@@ -283,6 +283,23 @@ extern "C" hipError_t ppfs_rs_fast_encode(int t2, const uint8_t* d, uint8_t* r, 
     }
 }
 
+#define X(T) extern "C" const char* ppfs_rs_fast_path_t##T();
+PPFS_RS_CASES(X)
+#undef X
+// name of the kernel path an instantiation was built with (ppfs_ecc_kernel_name)
+extern "C" const char* ppfs_rs_fast_path(int t2)
+{
+    switch (t2) {
+#define X(T)                                                                                                           \
+    case T:                                                                                                            \
+        return ppfs_rs_fast_path_t##T();
+        PPFS_RS_CASES(X)
+#undef X
+    default:
+        return "";
+    }
+}
+
 extern "C" hipError_t ppfs_rs_fast_decode(int t2, uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb,
     const uint8_t* tab, int wb, hipStream_t s)
 {

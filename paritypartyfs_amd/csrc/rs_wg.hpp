@@ -428,7 +428,7 @@ __device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, ui
             const uint8_t fixed = (uint8_t)(lds[row + pos] ^ e);
             lds[row + pos] = fixed;
             if (wb && PPFS_DBG_OK(raw_g + blk * 255u + pos, 1, raw_g, raw_bytes))
-                raw_g[blk * 255u + pos] = fixed;
+                wb_byte(raw_g + blk * 255u + pos, fixed);
         };
         if (__builtin_amdgcn_ballot_w64(err && !geo)) {
             if (err) {

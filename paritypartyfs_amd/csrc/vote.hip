@@ -115,6 +115,9 @@ extern "C" hipError_t ppfs_copy_launch(uint8_t* dst, const uint8_t* src, uint64_
 // corrupt every codeword of a step: torch's index_put_ of the same bytes reads 8-byte indices and
 // costs ~2x this kernel.  Each thread takes 4 consecutive blocks: one
 // 4-byte load of their positions and one of their values, then four byte stores.
+#ifndef PPFS_INJECT_NT
+#define PPFS_INJECT_NT 0 // ablation builds: non-temporal byte stores
+#endif
 namespace ppfs {
 template <int MODE>
 __global__ __launch_bounds__(256) void inject_kernel(uint8_t* __restrict__ raw, uint64_t stride, uint64_t nblocks,
@@ -141,7 +144,12 @@ __global__ __launch_bounds__(256) void inject_kernel(uint8_t* __restrict__ raw, 
             continue;
         uint8_t* d = raw + (b0 + j) * stride + p;
         const uint8_t v = (uint8_t)(v4 >> (8 * j));
-        *d = MODE == 0 ? v : (uint8_t)(*d ^ v);
+        const uint8_t w = MODE == 0 ? v : (uint8_t)(*d ^ v);
+#if PPFS_INJECT_NT
+        __builtin_nontemporal_store(w, d);
+#else
+        *d = w;
+#endif
     }
 }
 } // namespace ppfs
