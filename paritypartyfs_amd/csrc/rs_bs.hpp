@@ -155,12 +155,58 @@ __device__ __forceinline__ void bs_cmodg(uint32_t (&s)[4], const uint8_t* lds, u
         s[m] ^= __builtin_amdgcn_alignbit(d[m + 1], d[m], sh);
 }
 
+// General correction (2+ errors), out of line: rs_pair.hpp pair_correct_general with the pair's
+// data exchanged through DPP instead of an LDS slot (both lanes of a pair take this path together).
+// Lane c computes S_i, i = 16c+1 .. 16c+16, over the whole c mod g state (coefficient q has
+// exponent i q); lane 0 then holds S_1..S_32 and runs BM / roots / Forney.
+template <int T2>
+__device__ __noinline__ void bs_correct_general(uint8_t* lds, uint32_t goff, uint32_t row, uint32_t c, uint32_t s0,
+    uint32_t s1, uint32_t s2, uint32_t s3, uint8_t* __restrict__ raw_g, uint64_t gblk, bool wb, uint64_t raw_bytes)
+{
+    static_assert(T2 == 32, "state byte q = coefficient q");
+    const Gf gf { lds + goff };
+    const uint32_t own[4] = { s0, s1, s2, s3 };
+    uint32_t rw[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t p = pair::pair_xchg<1>(own[k]);
+        rw[k] = c ? p : own[k];
+        rw[4 + k] = c ? own[k] : p;
+    }
+    uint32_t sw[4] = { 0u, 0u, 0u, 0u };
+#pragma unroll
+    for (int ii = 0; ii < 16; ++ii) {
+        const uint32_t i = 16u * c + 1u + (uint32_t)ii;
+        uint32_t e = 0, sacc = 0;
+#pragma unroll
+        for (int q = 0; q < T2; ++q) {
+            const uint32_t rv = (rw[q >> 2] >> (8 * (q & 3))) & 0xFFu;
+            const uint32_t v = gf.exp(gf.log(rv) + e);
+            sacc ^= rv ? v : 0u;
+            e += i;
+            e = e >= 255u ? e - 255u : e;
+        }
+        sw[ii >> 2] |= sacc << (8 * (ii & 3));
+    }
+    uint32_t hi[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        hi[k] = pair::pair_xchg<1>(sw[k]); // lane 0: S_17..S_32 from lane 1
+    if (c == 0) {
+        uint32_t S[T2];
+#pragma unroll
+        for (int i = 0; i < T2; ++i)
+            S[i] = ((i < 16 ? sw[i >> 2] : hi[(i - 16) >> 2]) >> (8 * (i & 3))) & 0xFFu;
+        rs_correct_general<T2>(S, gf, [&](uint32_t pos, uint32_t ev) { col::col_fix(lds, row, raw_g, gblk, wb, pos, ev, raw_bytes); });
+    }
+}
+
 // Decode correction for the pair's block: rs_pair.hpp pair_correct (single error: X = S_2/S_1,
 // e = S_1/X, confirmed iff c mod g == e * (x^p mod g); else the general path), with S_1 and S_2
 // read from the S12 byte table -- 16 lookups per lane where the log / exp forms took 48.
-template <int T2, int TAG = 2>
+template <int T2>
 __device__ __forceinline__ uint32_t bs_correct(uint8_t* lds, uint32_t goff, uint32_t s12off, const uint8_t* __restrict__ xp,
-    uint32_t row, uint32_t slot, uint32_t c, const uint32_t (&s)[4], bool valid, uint8_t* __restrict__ raw_g, uint64_t gblk,
+    uint32_t row, uint32_t c, const uint32_t (&s)[4], bool valid, uint8_t* __restrict__ raw_g, uint64_t gblk,
     bool wb, uint64_t raw_bytes)
 {
     const bool err = valid && pair::pair_or<1>(s[0] | s[1] | s[2] | s[3]) != 0u;
@@ -193,7 +239,7 @@ __device__ __forceinline__ uint32_t bs_correct(uint8_t* lds, uint32_t goff, uint
     if (geo && c == 0)
         col::col_fix(lds, row, raw_g, gblk, wb, lx, gf.exp(le), raw_bytes);
     if (err && !geo)
-        pair::pair_correct_general<T2, true, TAG>(lds, goff, row, slot, c, raw_g, gblk, wb, raw_bytes);
+        bs_correct_general<T2>(lds, goff, row, c, s[0], s[1], s[2], s[3], raw_g, gblk, wb, raw_bytes);
     return err ? 1u : 0u;
 }
 
@@ -251,15 +297,13 @@ __device__ __forceinline__ void put_parity(uint8_t* lds, uint32_t img, const BsL
         gap[k] = (uint8_t)(s[k >> 2] >> (8 * (k & 3)));
 }
 
-// LDS plan: [0, 64 KiB) byte-slice tables | (decode: GF block, S12 table, NW x 1 KiB syndrome
-// slots) |
+// LDS plan: [0, 64 KiB) byte-slice tables | (decode: GF block, S12 table) |
 // NW x NBUF wave images | 64 B slack (the rows' last-word reads and the decode emission's second
 // window run past the last image)
 template <int NW, int NBUF, bool DEC> struct BsLds {
     static constexpr int OFF_GF = TAB_BYTES;
     static constexpr int OFF_S12 = OFF_GF + (DEC ? GF_BYTES : 0);
-    static constexpr int OFF_SLOT = OFF_S12 + (DEC ? 32 * 256 * 2 : 0);
-    static constexpr int OFF_IMG = OFF_SLOT + (DEC ? NW * TBW * 32 : 0);
+    static constexpr int OFF_IMG = OFF_S12 + (DEC ? 32 * 256 * 2 : 0);
     static constexpr int BYTES = OFF_IMG + NW * (NBUF > 0 ? NBUF : 1) * IMGW + 64;
     static_assert(BYTES <= 163840, "one workgroup per CU: 160 KiB of LDS");
     static_assert(OFF_IMG % 16 == 0 && IMGW % 16 == 0, "aligned images");
@@ -409,7 +453,6 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
     const bool wb = write_back != 0, want = data != nullptr;
     const uint32_t img = D::OFF_IMG + wave * (uint32_t)IMGW;
     const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(lds + img));
-    const uint32_t slot = D::OFF_SLOT + wave * (uint32_t)(TBW * 32) + 32u * Ln.blk;
     const uint32_t row = img + 255u * Ln.blk;
     const uint8_t* const xpm = tables + L::OFF_XPM;
     const uint64_t nfull = nblocks / TBW, ntiles = (nblocks + TBW - 1) / TBW;
@@ -435,11 +478,9 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
         }
         uint32_t s[4];
         bs_cmodg(s, lds, row, Ln);
-        *(uint4*)(lds + slot + 16u * Ln.c) = make_uint4(s[0], s[1], s[2], s[3]); // read by the general path
-        wave_fence();
         const uint64_t gblk = t * TBW + Ln.blk;
         const uint32_t st = bs_correct<T2>(
-            lds, D::OFF_GF, D::OFF_S12, xpm, row, slot, Ln.c, s, true, raw, gblk, wb, nblocks * 255u);
+            lds, D::OFF_GF, D::OFF_S12, xpm, row, Ln.c, s, true, raw, gblk, wb, nblocks * 255u);
         if (status && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
             status[gblk] = (uint8_t)st;
         wave_fence(); // corrections patched into the image rows
@@ -447,9 +488,11 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
             uint8_t* dst = data + t * (TBW * K);
 #pragma unroll
             for (int k = 0; k < KO; ++k) {
-                const uint32_t p = lane + 64u * (uint32_t)k;
+                uint32_t p = lane + 64u * (uint32_t)k;
+                asm volatile("" : "+v"(p)); // one piece live at a time
                 if (((k + 1) * 64 <= OUT_PIECES || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, data, nblocks * K))
                     st_nt<NTST>(dst + 16u * p, pair::pair_dec_piece<T2>(lds, img - pair::PAD, p));
+                asm volatile("" ::: "memory");
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -471,12 +514,10 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
         wave_fence();
         uint32_t s[4];
         bs_cmodg(s, lds, row, Ln);
-        *(uint4*)(lds + slot + 16u * Ln.c) = make_uint4(s[0], s[1], s[2], s[3]);
-        wave_fence();
         const bool valid = Ln.blk < nb;
         const uint64_t gblk = t * TBW + Ln.blk;
         const uint32_t st = bs_correct<T2>(
-            lds, D::OFF_GF, D::OFF_S12, xpm, row, slot, Ln.c, s, valid, raw, gblk, wb, nblocks * 255u);
+            lds, D::OFF_GF, D::OFF_S12, xpm, row, Ln.c, s, valid, raw, gblk, wb, nblocks * 255u);
         if (status && valid && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
             status[gblk] = (uint8_t)st;
         wave_fence();
