@@ -193,6 +193,9 @@ constexpr int DEC_NBUF = DEC_FULL ? 0 : PPFS_WG_DEC_NBUF;
 #ifndef PPFS_BS_DEC_NBUF
 #define PPFS_BS_DEC_NBUF 1 // 0 = register prefetch
 #endif
+#ifndef PPFS_BS_DEC_NTST
+#define PPFS_BS_DEC_NTST 1 // non-temporal payload stores of the decode
+#endif
 constexpr bool PAIR_BS = PPFS_PAIR_BS && PPFS_T2 == 32;
 constexpr bool PAIR_IMG = PPFS_PAIR_IMG && (PPFS_T2 % 16 == 0);
 constexpr int PAIR_ENC_WPC = PAIR_IMG ? PPFS_PAIR_IMG_WPC : pair::wpc_of(PPFS_PAIR_ENC), PAIR_DEC_WPC = pair::wpc_of(PPFS_PAIR_DEC);
@@ -298,7 +301,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
 #endif
 #elif PPFS_T2 > 16
     if constexpr (PAIR_BS)
-        hipLaunchKernelGGL((bs::rs_bs_decode_kernel<PPFS_T2, PPFS_BS_NW, PPFS_BS_DEC_NBUF>), dim3(rs_tile_grid(nb, 1, bs::TBW * PPFS_BS_NW)),
+        hipLaunchKernelGGL((bs::rs_bs_decode_kernel<PPFS_T2, PPFS_BS_NW, PPFS_BS_DEC_NBUF, PPFS_BS_DEC_NTST>), dim3(rs_tile_grid(nb, 1, bs::TBW * PPFS_BS_NW)),
             dim3(64 * PPFS_BS_NW), 0, s, r, d, st, nb, tab, wb);
     else
     hipLaunchKernelGGL((pair::rs_pair_decode_kernel<PPFS_T2, PPFS_PAIR_DEC>),
