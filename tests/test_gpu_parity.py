@@ -147,6 +147,33 @@ def test_rs_many_tiles_per_workgroup(oracle, bs, t):
     assert np.array_equal(host(raw_d), o_fixed)
 
 
+@pytest.mark.parametrize("bs,t", [(512, 3), (4096, 16)])
+def test_rs_ragged_tiles(oracle, bs, t):
+    """Batch sizes around the wave / workgroup tiles of the fast paths (64 blocks per tile for
+    2t <= 8, 32 per wave tile for the byte-slice 2t = 32 kernels): every partial-tile size from 1
+    to 33 blocks, exact multiples, and a grid whose last round covers only some waves (one resident
+    grid of 256 workgroups x 12 waves x 32 blocks, plus 5).  Encode, then decode with 0..t+3
+    errors per block and write-back, all vs the oracle."""
+    n, k, _ = oracle.rs_sizes(bs, t)
+    eng = EccEngine(ECC_REED_SOLOMON, bs, t)
+    for nb in list(range(1, 34)) + [63, 64, 65, 96, 127, 128, 129, 256 * 12 * 32 + 5]:
+        rng = rng_for("rsrag", bs, t, nb)
+        data = rng.integers(0, 256, nb * k, dtype=np.uint8)
+        raw_d = torch.zeros(nb * n, dtype=torch.uint8, device="cuda")
+        eng.encode(dev(data), raw_d, nblocks=nb)
+        cw = oracle.rs_encode(bs, t, data)
+        assert np.array_equal(host(raw_d), cw), nb
+        bad = inject_rs_fast(rng, cw, n, t, nb)
+        o_data, o_st, o_fixed, _, _ = oracle.rs_decode(bs, t, bad)
+        raw_d = dev(bad)
+        data_d = torch.zeros(nb * k, dtype=torch.uint8, device="cuda")
+        st_d = torch.full((nb,), 77, dtype=torch.uint8, device="cuda")
+        eng.decode(raw_d, data_d, st_d, write_back=True, nblocks=nb)
+        assert np.array_equal(host(st_d), o_st), nb
+        assert np.array_equal(host(data_d), o_data), nb
+        assert np.array_equal(host(raw_d), o_fixed), nb
+
+
 def test_rs_full_batch_roundtrip_properties():
     """BASELINE configs[1]/[2] at full size (2^20 RS(255,249) blocks): encode, one byte error per
     block, decode with write-back.  Size-independent properties: every payload restored, every
