@@ -909,6 +909,38 @@ static int ensure_staging(ppfs_ecc_ctx* c, size_t bytes)
 namespace {
 constexpr size_t kChunkBlocks = 1u << 15; // 32 Ki blocks per chunk (~8 MiB of RS codewords)
 
+// Host staging copies of the pageable host path (caller buffer <-> page-locked staging): one CPU
+// thread moves ~10 GB/s, well under the PCIe rate the page-locked path reaches, so copies of
+// >= 2 MiB are split over PPFS_ECC_COPY_THREADS threads (default 4; 1 = single-threaded).
+int copy_threads()
+{
+    static const int n = [] {
+        const char* e = std::getenv("PPFS_ECC_COPY_THREADS");
+        const int v = e ? std::atoi(e) : 4;
+        return v < 1 ? 1 : (v > 16 ? 16 : v);
+    }();
+    return n;
+}
+
+void par_memcpy(void* dst, const void* src, size_t n)
+{
+    const int nt = copy_threads();
+    if (nt == 1 || n < (2u << 20)) {
+        std::memcpy(dst, src, n);
+        return;
+    }
+    const size_t part = ((n + nt - 1) / nt + 4095) & ~(size_t)4095;
+    std::thread th[16];
+    int k = 0;
+    for (size_t off = part; off < n; off += part, ++k) {
+        const size_t len = std::min(part, n - off);
+        th[k] = std::thread([=] { std::memcpy((uint8_t*)dst + off, (const uint8_t*)src + off, len); });
+    }
+    std::memcpy(dst, src, std::min(part, n));
+    for (int i = 0; i < k; ++i)
+        th[i].join();
+}
+
 struct Layout { // offsets inside one staging buffer
     size_t data, raw, status, spill, idx, gat, total;
 };
@@ -1255,7 +1287,7 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
             if (direct)
                 return 0; // the whole range landed in the caller's image (unchanged blocks: same bytes)
             if (eager)
-                std::memcpy(raw + b0 * c->raw, h + L.raw, nb * c->raw);
+                par_memcpy(raw + b0 * c->raw, h + L.raw, nb * c->raw);
             else
                 for (size_t b = 0; b < nb; ++b)
                     if (sts[b] == 1)
@@ -1267,7 +1299,7 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
             HIP_TRY(hipMemcpyAsync(o, d + L.raw, nb * c->raw, hipMemcpyDeviceToHost, s), "D2H raw");
             HIP_TRY(hipStreamSynchronize(s), "sync");
             if (!direct)
-                std::memcpy(raw + b0 * c->raw, h + L.raw, nb * c->raw);
+                par_memcpy(raw + b0 * c->raw, h + L.raw, nb * c->raw);
             return 0;
         }
         HIP_TRY(hipMemcpyAsync(d + L.idx, ix, nchg * sizeof(uint32_t), hipMemcpyHostToDevice, s), "H2D idx");
@@ -1296,9 +1328,9 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
         }
         uint8_t* h = c->h_pin[i];
         if (op == OP_ENCODE || op == OP_WRITE)
-            std::memcpy(raw + b0 * c->raw, h + L.raw, nb * c->raw);
+            par_memcpy(raw + b0 * c->raw, h + L.raw, nb * c->raw);
         if (op == OP_DECODE && data_out)
-            std::memcpy(data_out + b0 * c->data, h + L.data, nb * c->data);
+            par_memcpy(data_out + b0 * c->data, h + L.data, nb * c->data);
         if (status)
             std::memcpy(status + b0, h + L.status, nb);
         if (spill)
@@ -1326,9 +1358,9 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
                 HIP_TRY(hipMemcpyAsync(d + L.raw, raw + b0 * c->raw, nb * c->raw, hipMemcpyHostToDevice, s), "H2D raw");
         } else {
             if (need_data)
-                std::memcpy(h + L.data, data_in + b0 * c->data, nb * c->data);
+                par_memcpy(h + L.data, data_in + b0 * c->data, nb * c->data);
             if (need_raw)
-                std::memcpy(h + L.raw, raw + b0 * c->raw, nb * c->raw);
+                par_memcpy(h + L.raw, raw + b0 * c->raw, nb * c->raw);
             const size_t in_lo = need_data ? L.data : L.raw;
             const size_t in_hi = need_raw ? L.raw + nb * c->raw : L.data + nb * c->data;
             HIP_TRY(hipMemcpyAsync(d + in_lo, h + in_lo, in_hi - in_lo, hipMemcpyHostToDevice, s), "H2D");
