@@ -33,6 +33,10 @@ using wg::lds_addr;
 using wg::st_bytes;
 using wg::st_nt;
 
+#ifndef PPFS_BS_XCHG
+#define PPFS_BS_XCHG 0
+#endif
+
 constexpr int TBW = 32;            // blocks per wave tile
 constexpr int IMGW = TBW * 255;    // 8,160 B: one wave tile's codeword image
 constexpr int IMG_PIECES = IMGW / 16; // 510 16-byte pieces in and out
@@ -107,7 +111,8 @@ __device__ __forceinline__ void bs_remainder(uint32_t (&s)[4], const uint8_t* ld
     constexpr int TOPN = LEN - 8 * (NC - 1);
     const uint32_t sh = (row & 3u) * 8u;
     const uint32_t* w = (const uint32_t*)(lds + (row & ~3u));
-    const uint32_t c = L.c, cm = c ? ~0u : 0u;
+    uint32_t cm = L.c ? ~0u : 0u;
+    asm("" : "+v"(cm)); // a mask, not a select: keeps (dpp & cm) one v_and_b32_dpp
     uint32_t up = w[2 * NC];
 #pragma unroll
     for (int j = NC - 1; j >= 0; --j) {
@@ -127,10 +132,22 @@ __device__ __forceinline__ void bs_remainder(uint32_t (&s)[4], const uint8_t* ld
             s[0] = s[1] = s[2] = s[3] = 0;
             bs_lookups(s, lds, L, lo, hi);
         } else {
+            // fold the top 8 coefficients (column 1's upper half, broadcast to both lanes of the
+            // pair: quad_perm [1,1,3,3]); state * x^8: column 1 takes column 0's upper half
+            // (quad_perm [0,0,2,2]), column 0 takes zeros.  Each DPP move folds into its XOR / AND
+            // (v_xor_b32_dpp, v_and_b32_dpp).
+#if PPFS_BS_XCHG
+            // ablation builds: the partner exchange of rs_pair.hpp (DPP move, select, AND)
             const uint32_t p2 = pair::pair_xchg<1>(s[2]), p3 = pair::pair_xchg<1>(s[3]);
-            lo ^= c ? s[2] : p2; // fold the top 8 coefficients (column 1's upper half)
-            hi ^= c ? s[3] : p3;
-            uint32_t n[4] = { p2 & cm, p3 & cm, s[0], s[1] }; // state * x^8
+            lo ^= L.c ? s[2] : p2;
+            hi ^= L.c ? s[3] : p3;
+            uint32_t n[4] = { p2 & cm, p3 & cm, s[0], s[1] };
+#else
+            lo ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)s[2], 0xF5, 0xF, 0xF, true);
+            hi ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)s[3], 0xF5, 0xF, 0xF, true);
+            uint32_t n[4] = { (uint32_t)__builtin_amdgcn_mov_dpp((int)s[2], 0xA0, 0xF, 0xF, true) & cm,
+                (uint32_t)__builtin_amdgcn_mov_dpp((int)s[3], 0xA0, 0xF, 0xF, true) & cm, s[0], s[1] }; // state * x^8
+#endif
             bs_lookups(n, lds, L, lo, hi);
             s[0] = n[0];
             s[1] = n[1];
