@@ -94,11 +94,14 @@ def test_rs_decode_matches_oracle(oracle, bs, t, nblocks):
     assert np.array_equal(host(data_d).reshape(nblocks, k)[okb], data.reshape(nblocks, k)[okb])
 
 
-def test_rs_decode_no_writeback_and_status_only(oracle):
-    bs, t, nb = 512, 3, 777
+@pytest.mark.parametrize("bs,t", [(512, 3), (4096, 16)])
+def test_rs_decode_no_writeback_and_status_only(oracle, bs, t):
+    """Status-only decode (no payload output), no write-back: statuses as the reference, the
+    codewords untouched (t = 16: the byte-slice decode's emission-free path)."""
+    nb = 777
     n, k, _ = oracle.rs_sizes(bs, t)
     eng = EccEngine(ECC_REED_SOLOMON, bs, t)
-    rng = rng_for("rsnw")
+    rng = rng_for("rsnw", bs, t)
     cw = oracle.rs_encode(bs, t, rng.integers(0, 256, nb * k, dtype=np.uint8))
     bad = inject_rs(rng, cw, n, t, nb)
     o_data, o_st, _, _, _ = oracle.rs_decode(bs, t, bad)
