@@ -80,3 +80,21 @@ def test_debug_build_exports_its_counters():
     out = subprocess.run(["nm", "-D", "--defined-only", dbg], capture_output=True, text=True).stdout
     units = re.findall(r"\bT (ppfs_dbg_faults_\w+)$", out, flags=re.M)
     assert len(units) == 11, units  # 7 RS instantiations, generic RS, bit, bit-fast, vote
+
+
+def test_inject_rejects_bad_buffers_without_gpu(lib):
+    """bench.py's fault injection validates its buffers in the Python mirror (CPU tensors, short
+    position / value arrays) and the C ABI rejects null pointers and bad modes before any launch."""
+    import torch
+
+    from paritypartyfs_amd import inject_bytes
+
+    raw = torch.zeros(10 * 255, dtype=torch.uint8)
+    pos = torch.zeros(10, dtype=torch.uint8)
+    with pytest.raises(ValueError):
+        inject_bytes(raw, 255, pos, pos)  # host tensors
+    assert lib.ppfs_inject_device(None, 255, 4, None, None, 0, None) < 0
+    buf = ctypes.create_string_buffer(64)
+    assert lib.ppfs_inject_device(buf, 0, 4, buf, buf, 0, None) < 0  # zero stride
+    assert lib.ppfs_inject_device(buf, 16, 4, buf, buf, 2, None) < 0  # unknown mode
+    assert lib.ppfs_inject_device(None, 255, 0, None, None, 0, None) == 0  # nothing to do
