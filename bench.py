@@ -52,8 +52,10 @@ def parse(argv=None):
     ap.add_argument("--blocks", type=int, default=1 << 20, help="blocks per GPU")
     ap.add_argument("--block-size", type=int, default=512)
     ap.add_argument("--t", type=int, default=3)
-    ap.add_argument("--inject", choices=("engine", "torch"), default="engine",
-                    help="fault-injection form: the engine's one-byte-per-block kernel or torch index_put_")
+    ap.add_argument("--inject", choices=("engine", "engine-xor", "torch"), default="engine",
+                    help="fault-injection form: the engine's one-byte-per-block kernel storing the "
+                         "precomputed wrong byte (engine) or XORing the error value in (engine-xor: "
+                         "load + store), or torch index_put_")
     ap.add_argument("--prewarm-s", type=float, default=1.0, help="untimed clock ramp before the warmup steps")
     ap.add_argument("--standalone-launches", type=int, default=30, help="back-to-back launches per kernel")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -337,6 +339,11 @@ def main(argv=None):
 
         def inject():
             inject_bytes(cw, n, err_col8, bad_bytes, nblocks=nb, stream=stream)
+    elif args.inject == "engine-xor":
+        from paritypartyfs_amd import inject_bytes
+
+        def inject():
+            inject_bytes(cw, n, err_col8, err_val, nblocks=nb, xor=True, stream=stream)
     else:
         def inject():
             cw.index_put_((err_pos,), bad_bytes)

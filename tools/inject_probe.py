@@ -30,8 +30,10 @@ def main():
     from paritypartyfs_amd import inject_bytes
 
     col8 = col.to(torch.uint8)
+    xv = torch.randint(1, 256, (nb,), dtype=torch.uint8, device=dev, generator=g)  # XOR twice: net no change
     forms = {
         "ppfs_inject": lambda: inject_bytes(cw, n, col8, bad),
+        "ppfs_inject_xor2": lambda: (inject_bytes(cw, n, col8, xv, xor=True), inject_bytes(cw, n, col8, xv, xor=True)),
         "index_put_int64": lambda: cw.index_put_((pos,), bad),
         "scatter_dim1": lambda: v2.scatter_(1, col2, bad2),
         "adv_index_2d": lambda: v2.index_put_((rows, col), bad),
