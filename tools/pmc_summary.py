@@ -27,7 +27,8 @@ def short(name):
     # "void ppfs::rs255_encode_kernel<6, 0, 1, 1, 0>(unsigned char const*, ...)" -> rs255_encode_kernel<6, 0, 1, 1, 0>
     n = name.replace("void ", "")
     n = n.split("(")[0]
-    return n.replace("ppfs::", "").replace("wg::", "").replace("pair::", "").replace("bf::", "")
+    return (n.replace("ppfs::", "").replace("wg::", "").replace("pair::", "").replace("bf::", "")
+            .replace("bs::", "").replace("w1::", ""))
 
 
 def counters(path):
@@ -56,7 +57,7 @@ def main():
     red = os.path.join(d, "counters_median.json")  # tools/pmc_reduce.py, reduced on the box
     if os.path.exists(red):
         for k, cs in json.load(open(red)).items():
-            merged[k].update(cs)
+            merged[short(k)].update(cs)
     for sub in ("fetch", "write", "sq", "sq2"):
         for k, cs in counters(os.path.join(d, sub, f"{sub}_counter_collection.csv")).items():
             for c, v in cs.items():
@@ -68,7 +69,7 @@ def main():
     latest = {}
     for r in rows:
         k = short(r["Name"])
-        if not k.startswith(("rs255", "rs_wg", "rs_pair", "rs_solo", "crc", "ham", "parity", "rs_generic")):
+        if not k.startswith(("rs255", "rs_wg", "rs_pair", "rs_solo", "rs_bs", "rs_w1", "inject", "crc", "ham", "parity", "rs_generic")):
             continue
         c = merged.get(k, {})
         fetch = 2 * c.get("FETCH_SIZE", float("nan")) * 1024
@@ -86,8 +87,21 @@ def main():
     open(os.path.join(prof, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
     sha_path = os.path.join(d, "lib.sha256")  # the library build the counters were collected on
     lib_sha = open(sha_path).read().strip() if os.path.exists(sha_path) else None
-    json.dump({"tag": tag, "lib_sha256": lib_sha, "kernels": latest},
-              open(os.path.join(prof, "pmc_latest.json"), "w"), indent=1)
+    # profiles of other workloads on the SAME library build (e.g. the cfg5 bench) merge into it, so
+    # bench.py finds traffic for each of their kernels; a new build starts it afresh
+    path = os.path.join(prof, "pmc_latest.json")
+    try:
+        old = json.load(open(path))
+    except Exception:
+        old = {}
+    if old.get("lib_sha256") == lib_sha and lib_sha:
+        merged_k = dict(old.get("kernels", {}))
+        merged_k.update(latest)
+        tags = old.get("tag", "")
+        tag_out = tags if tag in tags.split("+") else tags + "+" + tag
+        json.dump({"tag": tag_out, "lib_sha256": lib_sha, "kernels": merged_k}, open(path, "w"), indent=1)
+    else:
+        json.dump({"tag": tag, "lib_sha256": lib_sha, "kernels": latest}, open(path, "w"), indent=1)
     print("\n".join(lines))
 
 
