@@ -30,7 +30,8 @@
 extern "C" {
 int ppfs_rs_fast_supported(int n, int t2);
 int ppfs_rs_fast_tables_bytes(int t2);
-hipError_t ppfs_rs_fast_encode(int t2, const uint8_t* d, uint8_t* r, uint64_t nb, const uint8_t* tab, hipStream_t s);
+hipError_t ppfs_rs_fast_encode(int t2, const uint8_t* d, uint8_t* r, uint64_t nb, const uint8_t* tab, hipStream_t s,
+    uint32_t* ctr);
 const char* ppfs_rs_fast_path(int t2);
 hipError_t ppfs_flag_launch(uint32_t* flag, uint32_t v, hipStream_t s);
 hipError_t ppfs_rs_generic_server_launch(int n, int t2, ppfs::SrvBox* box, uint8_t* zc, uint64_t zc_bytes,
@@ -469,6 +470,13 @@ struct ppfs_ecc_ctx {
     const char* kname = "";
     // device tables
     uint8_t* d_tables = nullptr;
+    // ticket counters of the dynamic-tile t <= 4 encode (rs_wg_tk.hpp): one 1,280-byte set per
+    // stream that encodes through this context (launches on one stream are ordered and the kernel
+    // leaves its set at zero; no two streams share a set); further streams use the static walk
+    static constexpr int kTkSlots = 16, kTkSetWords = 320;
+    uint32_t* d_ctr = nullptr;
+    hipStream_t tk_stream[kTkSlots] = {};
+    int tk_n = 0;
     // scratch for write_device status when the caller passes none
     uint8_t* d_scratch = nullptr;
     size_t scratch_bytes = 0;
@@ -491,6 +499,22 @@ struct ppfs_ecc_ctx {
     bool srv_launched = false;
     int srv_ok = -1;
 };
+
+namespace {
+// the ticket-counter set of stream s (nullptr: none left, the static kernel encodes)
+uint32_t* ctr_for(ppfs_ecc_ctx* c, hipStream_t s)
+{
+    if (!c->d_ctr)
+        return nullptr;
+    for (int i = 0; i < c->tk_n; ++i)
+        if (c->tk_stream[i] == s)
+            return c->d_ctr + (size_t)i * ppfs_ecc_ctx::kTkSetWords;
+    if (c->tk_n == ppfs_ecc_ctx::kTkSlots)
+        return nullptr;
+    c->tk_stream[c->tk_n] = s;
+    return c->d_ctr + (size_t)(c->tk_n++) * ppfs_ecc_ctx::kTkSetWords;
+}
+} // namespace
 
 extern "C" uint64_t ppfs_ecc_crc_implicit_to_explicit(uint64_t implicit_poly) { return (implicit_poly << 1) + 1; }
 
@@ -597,6 +621,16 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
         delete c;
         return fail(PPFS_ECC_EHIP, "hipSetDevice", e);
     }
+    if (c->rs_fast && c->rs_t2 <= 8) {
+        const size_t cb = sizeof(uint32_t) * ppfs_ecc_ctx::kTkSlots * ppfs_ecc_ctx::kTkSetWords;
+        e = hipMalloc(&c->d_ctr, cb);
+        if (e == hipSuccess)
+            e = hipMemset(c->d_ctr, 0, cb);
+        if (e != hipSuccess) {
+            ppfs_ecc_destroy(c);
+            return fail(PPFS_ECC_EHIP, "ticket counters", e);
+        }
+    }
     if (!tables.empty()) {
         e = hipMalloc(&c->d_tables, tables.size());
         if (e == hipSuccess)
@@ -643,6 +677,8 @@ extern "C" void ppfs_ecc_destroy(ppfs_ecc_ctx* c)
     }
     if (c->d_tables)
         (void)hipFree(c->d_tables);
+    if (c->d_ctr)
+        (void)hipFree(c->d_ctr);
     if (c->d_scratch)
         (void)hipFree(c->d_scratch);
     if (c->h_zc)
@@ -725,7 +761,7 @@ static int ppfs_ecc_encode_device_impl(ppfs_ecc_ctx* c, const uint8_t* d_data, u
         return check_hip(hipMemcpyAsync(d_raw, d_data, nblocks * c->raw, hipMemcpyDeviceToDevice, s), "copy");
     case PPFS_ECC_REED_SOLOMON:
         if (c->rs_fast && aligned16(d_data) && aligned16(d_raw))
-            return check_hip(ppfs_rs_fast_encode(c->rs_t2, d_data, d_raw, nblocks, c->d_tables, s), "rs encode");
+            return check_hip(ppfs_rs_fast_encode(c->rs_t2, d_data, d_raw, nblocks, c->d_tables, s, ctr_for(c, s)), "rs encode");
         if (c->rs_fast) {
             // fast tables but unaligned pointers: the generic kernel needs gf block + generator
             return fail(PPFS_ECC_EINVAL, "rs encode: device pointers must be 16-byte aligned");

@@ -119,6 +119,11 @@ constexpr int DEC_NBUF = DEC_FULL ? 0 : PPFS_WG_DEC_NBUF;
 #if PPFS_WG_RP
 #include "rs_wg_rp.hpp"
 #endif
+// dynamic tiles for the t <= 4 encode (rs_wg_tk.hpp) when the caller passes a counter set
+#ifndef PPFS_WG_TK
+#define PPFS_WG_TK 1
+#endif
+#include "rs_wg_tk.hpp"
 #if PPFS_WG_ENC_W8 || PPFS_WG_DYN
 #include "rs_wg_ablate.hpp"
 #endif
@@ -225,7 +230,7 @@ constexpr int SOLO_NW = PPFS_SOLO_NW, SOLO_WPC = PPFS_SOLO_WPC;
 #endif
 
 extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d, uint8_t* r, uint64_t nb,
-    const uint8_t* tab, hipStream_t s)
+    const uint8_t* tab, hipStream_t s, [[maybe_unused]] uint32_t* ctr)
 {
 #if PPFS_T2 <= 8
 #if PPFS_WG_RP
@@ -239,7 +244,10 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
     hipLaunchKernelGGL((wg::rs_wg_encode8_kernel<PPFS_T2, (PPFS_T2 > 6 ? 3 : PPFS_WG_ENC_W8), 2, PPFS_ENC_NTST>),
         dim3(rs_tile_grid(nb, 2)), dim3(512), 0, s, d, r, nb, tab);
 #else
-    if constexpr (PPFS_WG_W1 & 1)
+    if (PPFS_WG_TK && ctr && PPFS_ENC_MODE == 3 && !WG_FULL && !PPFS_WG_ENC_IMG && !(PPFS_WG_W1 & 1))
+        hipLaunchKernelGGL((wg::rs_wg_encode_tk_kernel<PPFS_T2, 2, PPFS_ENC_NTST>), dim3(rs_tile_grid(nb, 2)), dim3(256), 0, s, d,
+            r, nb, tab, ctr);
+    else if constexpr (PPFS_WG_W1 & 1)
         hipLaunchKernelGGL((w1::rs_w1_encode_kernel<PPFS_T2, PPFS_W1_NW, PPFS_W1_NBUF, PPFS_ENC_MODE, PPFS_ENC_NTST>),
             dim3(rs_tile_grid(nb, 1, w1::TB * PPFS_W1_NW)), dim3(64 * PPFS_W1_NW), 0, s, d, r, nb, tab);
     else if constexpr (PPFS_WG_ENC_IMG)

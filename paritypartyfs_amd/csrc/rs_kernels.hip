@@ -240,7 +240,8 @@ using namespace ppfs;
 #define PPFS_RS_CASES(X) X(2) X(4) X(6) X(8) X(10) X(16) X(32)
 
 #define X(T)                                                                                                           \
-    extern "C" hipError_t ppfs_rs_fast_encode_t##T(const uint8_t*, uint8_t*, uint64_t, const uint8_t*, hipStream_t);  \
+    extern "C" hipError_t ppfs_rs_fast_encode_t##T(const uint8_t*, uint8_t*, uint64_t, const uint8_t*, hipStream_t,   \
+        uint32_t*);                                                                                                    \
     extern "C" hipError_t ppfs_rs_fast_decode_t##T(uint8_t*, uint8_t*, uint8_t*, uint64_t, const uint8_t*, int,       \
         hipStream_t);
 PPFS_RS_CASES(X)
@@ -270,12 +271,12 @@ extern "C" int ppfs_rs_fast_tables_bytes(int t2)
 }
 
 extern "C" hipError_t ppfs_rs_fast_encode(int t2, const uint8_t* d, uint8_t* r, uint64_t nb, const uint8_t* tab,
-    hipStream_t s)
+    hipStream_t s, uint32_t* ctr)
 {
     switch (t2) {
 #define X(T)                                                                                                           \
     case T:                                                                                                            \
-        return ppfs_rs_fast_encode_t##T(d, r, nb, tab, s);
+        return ppfs_rs_fast_encode_t##T(d, r, nb, tab, s, ctr);
         PPFS_RS_CASES(X)
 #undef X
     default:

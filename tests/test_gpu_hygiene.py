@@ -202,3 +202,30 @@ def test_inject_bytes_matches_index_put(nb, stride, xor):
     assert torch.equal(raw.view(nb, stride), want)
     with pytest.raises(ValueError):
         inject_bytes(raw, stride, pos, val, nblocks=nb + 1)
+
+
+def test_rs_encode_on_many_concurrent_streams(oracle):
+    """The t <= 4 encode hands tiles out from per-stream ticket counters (rs_wg_tk.hpp, api.cpp
+    ctr_for): one context encoding on 20 streams at once -- 16 get their own counter sets, the
+    rest the static walk -- gives the oracle's codewords on every stream, twice over (the kernels
+    leave their sets at zero for the next launch)."""
+    bs, t, nb = 512, 3, 64 * 1536 + 7  # several tiles per workgroup, a ragged tail
+    n, k, _ = oracle.rs_sizes(bs, t)
+    eng = EccEngine(ECC_REED_SOLOMON, bs, t)
+    rng = np.random.default_rng(20)
+    data = rng.integers(0, 256, nb * k, dtype=np.uint8)
+    want = oracle.rs_encode(bs, t, data)
+    d = torch.from_numpy(data).cuda()
+    streams = [torch.cuda.Stream() for _ in range(20)]
+    outs = [torch.zeros(nb * n, dtype=torch.uint8, device="cuda") for _ in streams]
+    torch.cuda.synchronize()
+    for _ in range(2):
+        for s, o in zip(streams, outs):
+            o.zero_()
+        torch.cuda.synchronize()
+        for s, o in zip(streams, outs):
+            eng.encode(d, o, nblocks=nb, stream=s)
+        torch.cuda.synchronize()
+        for o in outs:
+            assert np.array_equal(o.cpu().numpy(), want)
+    eng.close()
