@@ -518,6 +518,9 @@ def main(argv=None):
 
     def kname(which):
         kn = eng.kernel_name
+        if kn.startswith("rs255-wg-tk"):  # 2t <= 8: ticket kernels (rs_wg_tk.hpp); tkenc: encode only
+            tk = which == "encode" or not kn.startswith("rs255-wg-tkenc")
+            return f"rs_wg_{which}{'_tk' if tk else ''}_kernel<{n - k}>"
         if kn.startswith("rs255-wg"):
             return f"rs_wg_{which}_kernel<{n - k}>"
         if kn.startswith("rs255-bs"):  # 2t = 32 (rs_bs.hpp)

@@ -41,7 +41,7 @@ hipError_t ppfs_bit_server_launch(int ecc_type, uint32_t bs, uint32_t ds, uint32
 hipError_t ppfs_rs_server_launch(int t2, ppfs::SrvBox* box, uint8_t* zc, uint64_t zc_bytes, const uint8_t* tab,
     uint32_t gen, uint32_t idle_us, hipStream_t s);
 hipError_t ppfs_rs_fast_decode(int t2, uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, const uint8_t* tab, int wb,
-    hipStream_t s);
+    hipStream_t s, uint32_t* ctr);
 hipError_t ppfs_rs_generic_encode(const uint8_t* d, uint8_t* r, uint64_t nb, int n, int t2, const uint8_t* tab,
     hipStream_t s);
 hipError_t ppfs_rs_generic_decode(uint8_t* r, uint8_t* d, uint8_t* st, uint8_t* spill, uint64_t nb, int n, int t2,
@@ -470,10 +470,11 @@ struct ppfs_ecc_ctx {
     const char* kname = "";
     // device tables
     uint8_t* d_tables = nullptr;
-    // ticket counters of the dynamic-tile t <= 4 encode (rs_wg_tk.hpp): one 1,280-byte set per
-    // stream that encodes through this context (launches on one stream are ordered and the kernel
-    // leaves its set at zero; no two streams share a set); further streams use the static walk
-    static constexpr int kTkSlots = 16, kTkSetWords = 320;
+    // ticket counters of the dynamic-tile t <= 4 encode and decode (rs_wg_tk.hpp): one 2,560-byte
+    // set per stream that runs them through this context, encode half then decode half (launches on
+    // one stream are ordered and a kernel leaves its half at zero; no two streams share a set);
+    // further streams use the static walk
+    static constexpr int kTkSlots = 16, kTkSetWords = 640; // encode 320 words, decode 320
     uint32_t* d_ctr = nullptr;
     hipStream_t tk_stream[kTkSlots] = {};
     int tk_n = 0;
@@ -513,6 +514,11 @@ uint32_t* ctr_for(ppfs_ecc_ctx* c, hipStream_t s)
         return nullptr;
     c->tk_stream[c->tk_n] = s;
     return c->d_ctr + (size_t)(c->tk_n++) * ppfs_ecc_ctx::kTkSetWords;
+}
+// a set's second half counts the decode's tiles (rs_wg_decode_tk_kernel)
+uint32_t* dec_ctr(uint32_t* set)
+{
+    return set ? set + ppfs_ecc_ctx::kTkSetWords / 2 : nullptr;
 }
 } // namespace
 
@@ -811,7 +817,8 @@ static int ppfs_ecc_decode_device_impl(ppfs_ecc_ctx* c, uint8_t* d_raw, uint8_t*
                     return r;
             }
             return check_hip(
-                ppfs_rs_fast_decode(c->rs_t2, d_raw, d_data, d_status, nblocks, c->d_tables, write_back, s),
+                ppfs_rs_fast_decode(c->rs_t2, d_raw, d_data, d_status, nblocks, c->d_tables, write_back, s,
+                    dec_ctr(ctr_for(c, s))),
                 "rs decode");
         }
         return check_hip(ppfs_rs_generic_decode(d_raw, d_data, d_status, d_spill, nblocks, c->rs_n, c->rs_t2,

@@ -119,9 +119,9 @@ constexpr int DEC_NBUF = DEC_FULL ? 0 : PPFS_WG_DEC_NBUF;
 #if PPFS_WG_RP
 #include "rs_wg_rp.hpp"
 #endif
-// dynamic tiles for the t <= 4 encode (rs_wg_tk.hpp) when the caller passes a counter set
+// dynamic tiles (rs_wg_tk.hpp) when the caller passes a counter set: bit 0 = encode, bit 1 = decode
 #ifndef PPFS_WG_TK
-#define PPFS_WG_TK 1
+#define PPFS_WG_TK 3
 #endif
 #include "rs_wg_tk.hpp"
 #if PPFS_WG_ENC_W8 || PPFS_WG_DYN
@@ -244,7 +244,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
     hipLaunchKernelGGL((wg::rs_wg_encode8_kernel<PPFS_T2, (PPFS_T2 > 6 ? 3 : PPFS_WG_ENC_W8), 2, PPFS_ENC_NTST>),
         dim3(rs_tile_grid(nb, 2)), dim3(512), 0, s, d, r, nb, tab);
 #else
-    if (PPFS_WG_TK && ctr && PPFS_ENC_MODE == 3 && !WG_FULL && !PPFS_WG_ENC_IMG && !(PPFS_WG_W1 & 1))
+    if ((PPFS_WG_TK & 1) && ctr && PPFS_ENC_MODE == 3 && !WG_FULL && !PPFS_WG_ENC_IMG && !(PPFS_WG_W1 & 1))
         hipLaunchKernelGGL((wg::rs_wg_encode_tk_kernel<PPFS_T2, 2, PPFS_ENC_NTST>), dim3(rs_tile_grid(nb, 2)), dim3(256), 0, s, d,
             r, nb, tab, ctr);
     else if constexpr (PPFS_WG_W1 & 1)
@@ -280,7 +280,12 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
 extern "C" const char* PPFS_CAT(ppfs_rs_fast_path_t, PPFS_T2)()
 {
 #if PPFS_T2 <= 8
-    return (PPFS_WG_W1 & 1) ? "rs255-w1-lds" : "rs255-wg-seg4-lds";
+    // the ticket kernels (rs_wg_tk.hpp) when the caller hands a counter set, which every engine
+    // context does for its first 16 streams
+    return (PPFS_WG_W1 & 1) ? "rs255-w1-lds"
+        : (PPFS_WG_TK & 3) == 3 ? "rs255-wg-tk-lds"
+        : (PPFS_WG_TK & 1)      ? "rs255-wg-tkenc-lds"
+                                : "rs255-wg-seg4-lds";
 #elif PPFS_T2 > 16
     return PAIR_BS ? "rs255-bs-byte-lds" : "rs255-pair-nibble-lds";
 #else
@@ -289,7 +294,7 @@ extern "C" const char* PPFS_CAT(ppfs_rs_fast_path_t, PPFS_T2)()
 }
 
 extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb,
-    const uint8_t* tab, int wb, hipStream_t s)
+    const uint8_t* tab, int wb, hipStream_t s, [[maybe_unused]] uint32_t* ctr)
 {
 #if PPFS_T2 <= 8
 #if PPFS_WG_RP
@@ -300,7 +305,10 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
         hipLaunchKernelGGL((wg::rs_wg_decode_rp_kernel<PPFS_T2, PPFS_WG_RP, PPFS_DEC_NTST, false>),
             dim3(rs_tile_grid(nb, PPFS_WG_RP)), dim3(256), 0, s, r, d, st, nb, tab, wb);
 #else
-    if constexpr (PPFS_WG_W1 & 2)
+    if ((PPFS_WG_TK & 2) && ctr && PPFS_DEC_MODE == 7 && !DEC_FULL && DEC_NBUF == 2 && DEC_WPC == 3 && !(PPFS_WG_W1 & 2))
+        hipLaunchKernelGGL((wg::rs_wg_decode_tk_kernel<PPFS_T2, 3, PPFS_DEC_NTST>), dim3(rs_tile_grid(nb, 3)), dim3(256), 0, s,
+            r, d, st, nb, tab, wb, ctr);
+    else if constexpr (PPFS_WG_W1 & 2)
         hipLaunchKernelGGL((w1::rs_w1_decode_kernel<PPFS_T2, PPFS_W1_DEC_NW, PPFS_W1_DEC_NBUF, PPFS_DEC_NTST>),
             dim3(rs_tile_grid(nb, 1, w1::TB * PPFS_W1_DEC_NW)), dim3(64 * PPFS_W1_DEC_NW), 0, s, r, d, st, nb, tab, wb);
     else

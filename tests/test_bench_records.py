@@ -26,7 +26,7 @@ def test_load_traffic_matches_build_kernel_and_blocks(tmp_path):
 def test_committed_pmc_summary_covers_the_bench_kernels():
     pmc = json.load(open(bench.os.path.join(bench.ROOT, "profiles", "pmc_latest.json")))
     ks = pmc["kernels"]
-    for name in ("rs_wg_encode_kernel<6>", "rs_wg_decode_kernel<6>"):  # the default bench line's kernels
+    for name in ("rs_wg_encode_tk_kernel<6>", "rs_wg_decode_tk_kernel<6>"):  # the default bench line's kernels
         assert name in ks and ks[name]["blocks"] == 1 << 20
         assert ks[name]["hbm_bytes_per_launch"] > 0
     for v in ks.values():  # any other profiled workload (cfg5) on the same build: well-formed

@@ -229,3 +229,38 @@ def test_rs_encode_on_many_concurrent_streams(oracle):
         for o in outs:
             assert np.array_equal(o.cpu().numpy(), want)
     eng.close()
+
+
+@pytest.mark.gpu
+def test_rs_decode_on_many_concurrent_streams(oracle):
+    """The t <= 4 decode takes its tiles from the second half of the stream's ticket set
+    (rs_wg_tk.hpp rs_wg_decode_tk_kernel): 20 streams decoding one context's batches at once, one
+    byte error in every codeword, give the payloads, status 1 and the repaired codewords on every
+    stream, twice over."""
+    bs, t, nb = 512, 3, 64 * 1536 + 7
+    n, k, _ = oracle.rs_sizes(bs, t)
+    eng = EccEngine(ECC_REED_SOLOMON, bs, t)
+    rng = np.random.default_rng(21)
+    data = rng.integers(0, 256, nb * k, dtype=np.uint8)
+    clean = oracle.rs_encode(bs, t, data)
+    cw = clean.reshape(nb, n).copy()
+    cw[np.arange(nb), rng.integers(0, n, nb)] ^= rng.integers(1, 256, nb).astype(np.uint8)
+    bad = torch.from_numpy(cw.reshape(-1)).cuda()
+    streams = [torch.cuda.Stream() for _ in range(20)]
+    raws = [torch.empty_like(bad) for _ in streams]
+    outs = [torch.empty(nb * k, dtype=torch.uint8, device="cuda") for _ in streams]
+    sts = [torch.empty(nb, dtype=torch.uint8, device="cuda") for _ in streams]
+    for _ in range(2):
+        for r, o, st in zip(raws, outs, sts):
+            r.copy_(bad)
+            o.zero_()
+            st.zero_()
+        torch.cuda.synchronize()
+        for s, r, o, st in zip(streams, raws, outs, sts):
+            eng.decode(r, o, st, write_back=True, nblocks=nb, stream=s)
+        torch.cuda.synchronize()
+        for r, o, st in zip(raws, outs, sts):
+            assert np.array_equal(o.cpu().numpy(), data)
+            assert int(st.min()) == 1 and int(st.max()) == 1
+            assert np.array_equal(r.cpu().numpy(), clean)
+    eng.close()
