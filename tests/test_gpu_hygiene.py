@@ -204,6 +204,33 @@ def test_inject_bytes_matches_index_put(nb, stride, xor):
         inject_bytes(raw, stride, pos, val, nblocks=nb + 1)
 
 
+@pytest.mark.parametrize("xor", [False, True])
+def test_inject_bytes_neighbours_share_sectors(xor):
+    """Positions at the start or end of every block put the injected bytes of consecutive blocks
+    in one 32-byte sector, within a thread's 4 blocks and across threads (the case a whole-sector
+    rewrite would have to merge); the image starts 7 bytes past a 32-byte
+    boundary.  Only the chosen bytes change, nothing outside the image."""
+    from paritypartyfs_amd import inject_bytes
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(77)
+    nb, stride = 40001, 255
+    base = torch.randint(0, 256, (nb * stride + 64,), dtype=torch.uint8, device=dev, generator=g)
+    raw = base[7: 7 + nb * stride]
+    edge = torch.tensor([0, 1, 2, 3, 251, 252, 253, 254], dtype=torch.uint8, device=dev)
+    pos = edge[torch.randint(0, 8, (nb,), device=dev, generator=g)]
+    val = torch.randint(1, 256, (nb,), dtype=torch.uint8, device=dev, generator=g)
+    before = base.clone()
+    want = raw.clone().view(nb, stride)
+    rows, cols = torch.arange(nb, device=dev), pos.long()
+    want[rows, cols] = (want[rows, cols] ^ val) if xor else val
+    inject_bytes(raw, stride, pos, val, xor=xor)
+    torch.cuda.synchronize()
+    assert torch.equal(raw.view(nb, stride), want)
+    assert torch.equal(base[:7], before[:7]) and torch.equal(base[7 + nb * stride:], before[7 + nb * stride:])
+
+
 def test_rs_encode_on_many_concurrent_streams(oracle):
     """The t <= 4 encode hands tiles out from per-stream ticket counters (rs_wg_tk.hpp, api.cpp
     ctr_for): one context encoding on 20 streams at once -- 16 get their own counter sets, the
