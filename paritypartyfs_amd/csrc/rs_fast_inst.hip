@@ -124,6 +124,13 @@ constexpr int DEC_NBUF = DEC_FULL ? 0 : PPFS_WG_DEC_NBUF;
 #define PPFS_WG_TK 3
 #endif
 #include "rs_wg_tk.hpp"
+// PPFS_WG_TKN = NBUF (ablation): the ticket encode over a ring of NBUF buffers (rs_wg_tk_ablate.hpp)
+#ifndef PPFS_WG_TKN
+#define PPFS_WG_TKN 0
+#endif
+#if PPFS_WG_TKN
+#include "rs_wg_tk_ablate.hpp"
+#endif
 #if PPFS_WG_ENC_W8 || PPFS_WG_DYN
 #include "rs_wg_ablate.hpp"
 #endif
@@ -244,6 +251,12 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
     hipLaunchKernelGGL((wg::rs_wg_encode8_kernel<PPFS_T2, (PPFS_T2 > 6 ? 3 : PPFS_WG_ENC_W8), 2, PPFS_ENC_NTST>),
         dim3(rs_tile_grid(nb, 2)), dim3(512), 0, s, d, r, nb, tab);
 #else
+#if PPFS_WG_TKN
+    if (ctr)
+        hipLaunchKernelGGL((wg::rs_wg_encode_tkn_kernel<PPFS_T2, PPFS_WG_TKN, 2, PPFS_ENC_NTST>), dim3(rs_tile_grid(nb, 2)), dim3(256), 0,
+            s, d, r, nb, tab, ctr);
+    else
+#endif
     if ((PPFS_WG_TK & 1) && ctr && PPFS_ENC_MODE == 3 && !WG_FULL && !PPFS_WG_ENC_IMG && !(PPFS_WG_W1 & 1))
         hipLaunchKernelGGL((wg::rs_wg_encode_tk_kernel<PPFS_T2, 2, PPFS_ENC_NTST>), dim3(rs_tile_grid(nb, 2)), dim3(256), 0, s, d,
             r, nb, tab, ctr);
