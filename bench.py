@@ -59,6 +59,10 @@ def parse(argv=None):
     ap.add_argument("--prewarm-s", type=float, default=1.0, help="untimed clock ramp before the warmup steps")
     ap.add_argument("--standalone-launches", type=int, default=30, help="back-to-back launches per kernel")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-configs", dest="configs", action="store_false",
+                    help="skip the per-config kernel leg (BASELINE configs[3] Hamming / CRC bs 4096 and "
+                         "configs[4] RS(255,223), rank 0 at N=1, outside the timed region)")
+    ap.add_argument("--config-reps", type=int, default=20)
     ap.add_argument("--cpu-sample-blocks", type=int, default=1 << 20)
     ap.add_argument("--cpu-faithful-blocks", type=int, default=1 << 18)
     ap.add_argument("--no-host-inclusive", dest="host_inclusive", action="store_false",
@@ -102,19 +106,52 @@ def _pool_time(fn, nparts):
     return time.perf_counter() - t0, res
 
 
+def usable_cpus():
+    """CPUs this process may actually use: the affinity mask, capped by the cgroup's CPU quota
+    (a GPU box's job sees the whole machine in os.cpu_count() but gets a share of it).  Returns
+    (cores, detail dict) -- the detail says where the figure came from."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    cores = min(aff, quota) if quota else aff
+    return cores, {"nproc": nproc, "affinity": aff, "cgroup_quota_cpus": quota}
+
+
+# BASELINE.md section 2: the reference's own CPU path (sources compiled unmodified, g++ -O2, 8-vCPU
+# Xeon, 8 threads), quoted -- not measured in this run
+REF_QUOTED = {
+    (512, 3): {"encode_blocks_per_s": 19899, "decode_1err_blocks_per_s": 349701, "threads": 8},
+    (4096, 16): {"encode_blocks_per_s": 15552, "decode_1err_blocks_per_s": 126088, "threads": 8},
+}
+
+
 def cpu_baseline(bs, t, nblocks, nfaithful, seed=1234):
     """Two CPU columns on the same synthetic workload (encode, then a 1-byte-error decode), one
-    thread per core over disjoint block ranges (the ctypes calls release the GIL):
+    thread per usable core over disjoint block ranges (the ctypes calls release the GIL):
       value / "port": the oracle's table-driven codec (LFSR encode, table syndromes; blocks with
           a non-zero syndrome run the restated reference decode) -- the strong CPU baseline;
-      "faithful": the oracle's reference-faithful restatement (schoolbook long-division encode,
-          Horner syndromes, BM / 255-point root search / Forney), SURVEY 8(d)'s
-          "reference-faithful variant", on a smaller sample."""
+      "faithful": the reference's algorithm restated over C arrays (schoolbook long-division
+          encode, Horner syndromes, BM / 255-point root search / Forney), SURVEY 8(d)'s
+          "reference-faithful variant", on a smaller sample.  Faithful to the algorithm, not to the
+          cost: it omits writeBlock's old-block read + decode (rs_block_device.cpp:61-93) and
+          PolynomialGF256's 256-entry temporaries (polynomial_gf256.cpp:101-127);
+      "reference_quoted": the reference's own per-call rates from BASELINE.md section 2 (not
+          measured here)."""
     from tests.oracle_lib import Oracle
 
     o = Oracle()
     n, k, _ = o.rs_sizes(bs, t)
-    cores = min(16, os.cpu_count() or 1)
+    cores, cpu_detail = usable_cpus()
     rng = np.random.default_rng(seed)
 
     def run(nb, enc_fn, dec_fn):
@@ -137,10 +174,26 @@ def cpu_baseline(bs, t, nblocks, nfaithful, seed=1234):
     te, td, ok = run(nblocks, lambda d: o.rs_encode_table(bs, t, d), lambda r: o.rs_decode_table(bs, t, r))
     fe, fd, fok = run(nfaithful, lambda d: o.rs_encode(bs, t, d), lambda r: o.rs_decode(bs, t, r))
     alg = k + n
+    quoted = None
+    if (bs, t) in REF_QUOTED:
+        qr = REF_QUOTED[(bs, t)]
+        qe, qd = qr["encode_blocks_per_s"], qr["decode_1err_blocks_per_s"]
+        quoted = {
+            "value": round(2 * alg / (1 / qe + 1 / qd) / GIB, 5),
+            "unit": "GiB/s",
+            "encode_blocks_per_s": qe,
+            "decode_1err_blocks_per_s": qd,
+            "threads": qr["threads"],
+            "kind": "reference (quoted, not measured in this run)",
+            "source": "BASELINE.md section 2: the reference's writeBlock (old-block read + decode + encode, "
+                      "rs_block_device.cpp:61-117) and readBlock with 1 error (:25-50,119-183), compiled "
+                      "unmodified (g++ -O2), 8-vCPU Xeon, 8 threads, +-30 %",
+        }
     return {
         "value": round(2 * alg * nblocks / (te + td) / GIB, 4),
         "unit": "GiB/s",
         "cores": cores,
+        "cores_detail": cpu_detail,
         "kind": "port",
         "sample": f"{nblocks} RS({n},{k}) blocks (the whole workload): encode + 1-byte-error decode, "
                   f"oracle/ppfs_oracle.c table codec on {cores} host threads over disjoint block ranges",
@@ -151,13 +204,16 @@ def cpu_baseline(bs, t, nblocks, nfaithful, seed=1234):
             "value": round(2 * alg * nfaithful / (fe + fd) / GIB, 4),
             "unit": "GiB/s",
             "cores": cores,
-            "kind": "port (reference-faithful algorithm)",
+            "kind": "port (reference algorithm, C arrays)",
             "sample": f"{nfaithful} RS({n},{k}) blocks: schoolbook long-division encode + Horner-syndrome / BM / "
-                      f"255-point root search / Forney decode (restated rs_block_device.cpp:95-280)",
+                      f"255-point root search / Forney decode (restated rs_block_device.cpp:95-280 over C arrays; "
+                      f"without writeBlock's old-block read + decode and PolynomialGF256's temporaries, so "
+                      f"faster than the reference's own code)",
             "encode_blocks_per_s": round(nfaithful / fe),
             "decode_blocks_per_s": round(nfaithful / fd),
             "verified": bool(fok),
         },
+        "reference_quoted": quoted,
     }
 
 
@@ -203,7 +259,10 @@ def timed_steps(step, steps, world, sync, device=None):
     import torch
     import torch.distributed as dist
 
-    if world > 1:
+    # under torchrun the collectives run whenever a process group exists, also at WORLD_SIZE=1:
+    # `torchrun --nproc-per-node 1 bench.py` then executes exactly the RCCL code of the 8-GPU run
+    coll = world > 1 or (dist.is_available() and dist.is_initialized())
+    if coll:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
@@ -211,7 +270,7 @@ def timed_steps(step, steps, world, sync, device=None):
         step()
     sync()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if coll:
         dist.barrier()
         tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -251,7 +310,7 @@ def load_traffic(kernel, nblocks, path=os.path.join(ROOT, "profiles", "pmc_lates
 def dry_run(args, world, rank):
     import torch.distributed as dist
 
-    if world > 1:
+    if world > 1 or os.environ.get("WORLD_SIZE"):
         dist.init_process_group("gloo")
     buf = np.zeros(1 << 16, np.uint8)
 
@@ -262,12 +321,19 @@ def dry_run(args, world, rank):
     for _ in range(args.warmup):
         step()
     elapsed = timed_steps(step, args.steps, world, lambda: None, None)
+    mine = {"rank": rank, "block_size": args.block_size, "t": args.t, "blocks": args.blocks}
+    gathered = [mine]
+    if dist.is_initialized():
+        gathered = [None] * dist.get_world_size()
+        dist.all_gather_object(gathered, mine)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "dry_run": True, "value": None, "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-                          "scaling": "weak", "note": "CPU stand-in for the engine: launcher / timing test only"}),
+                          "scaling": "weak", "note": "CPU stand-in for the engine: launcher / timing test only",
+                          # what every rank parsed: the driver's argv must reach the ranks unchanged
+                          "rank_args": gathered}),
               flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
@@ -293,11 +359,14 @@ def main(argv=None):
     import torch.distributed as dist
 
     red_dev = None  # where the max-reduce of the elapsed time lives (the GPU for RCCL)
-    if world > 1 and args.share_gpu:
+    if env_world is not None and args.share_gpu:
         torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
         dist.init_process_group("gloo")
         red_dev = torch.device("cpu")
-    elif world > 1:
+    elif env_world is not None:
+        # under torchrun -- the driver's N-GPU form, and also at WORLD_SIZE=1 -- always RCCL with
+        # its barrier and the GPU max-reduce, so a 1-GPU `torchrun --nproc-per-node 1` run executes
+        # exactly the code of the 8-GPU scaling run
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
@@ -334,16 +403,18 @@ def main(argv=None):
     err_col8 = err_col.to(torch.uint8)
     torch.cuda.synchronize()
 
+    # Every launch goes to torch's CURRENT stream at call time (no stream captured here): inside
+    # torch.cuda.graph() that is the capture stream, so --launch graph captures the injection too.
     if args.inject == "engine":
         from paritypartyfs_amd import inject_bytes
 
         def inject():
-            inject_bytes(cw, n, err_col8, bad_bytes, nblocks=nb, stream=stream)
+            inject_bytes(cw, n, err_col8, bad_bytes, nblocks=nb)
     elif args.inject == "engine-xor":
         from paritypartyfs_amd import inject_bytes
 
         def inject():
-            inject_bytes(cw, n, err_col8, err_val, nblocks=nb, xor=True, stream=stream)
+            inject_bytes(cw, n, err_col8, err_val, nblocks=nb, xor=True)
     else:
         def inject():
             cw.index_put_((err_pos,), bad_bytes)
@@ -571,6 +642,26 @@ def main(argv=None):
         host_incl["note"] = ("ppfs_ecc_{encode,decode}_host over the same 2^20 blocks: H2D + kernel + D2H wall "
                              "time, algorithmic bytes; never `value`")
 
+    # (5) the other BASELINE configs (driver-visible per-config kernel rates): configs[3] Hamming and
+    # CRC 0x9960034c at block_size 4096 and configs[4] RS(255,223), 2^20 blocks each, back-to-back
+    # launches of one kernel with a round-trip self-check (tools/bench_configs.py run_config)
+    cfg_lines = None
+    if args.configs and rank == 0 and world == 1:
+        from tools.bench_configs import baseline_configs, run_config
+
+        want = {"cfg4 hamming bs4096": "cfg4_hamming_bs4096", "cfg4 crc32 0x9960034c bs4096": "cfg4_crc_0x9960034c_bs4096",
+                "cfg5 rs255_t16 bs4096": "cfg5_rs255_223_bs4096", "cfg2-3 rs255_t3 bs512": "cfg2_3_rs255_249_bs512"}
+        cfg_lines = {}
+        for name, typ, cbs, ct, poly in baseline_configs():
+            if name not in want or (cbs, ct) == (args.block_size, args.t) and typ == ECC_REED_SOLOMON:
+                continue  # the bench's own workload is measured above
+            cfg_lines[want[name]] = run_config(name, typ, cbs, ct, poly, 1 << 20, args.config_reps, stream, dev)
+        cfg_lines["note"] = ("BASELINE configs measured outside the timed region: median of back-to-back launches "
+                             "of one kernel over 2^20 blocks (fence-free HIP events), algorithmic bytes (payload + raw "
+                             "per block) / time, fraction of 8 TB/s; 1-error decodes restore the corrupted image by "
+                             "an untimed copy before each launch; roundtrip_ok = decode(encode(x)) == x with the "
+                             "expected statuses")
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.block_size, args.t, min(args.cpu_sample_blocks, nb),
@@ -613,6 +704,7 @@ def main(argv=None):
                 "avg_launch_ms": round(dom_ms, 5),
             },
             "cpu_baseline": cpu,
+            "configs": cfg_lines,
             "kernels_ms": {"encode": round(enc_avg, 5), "inject": round(inj_avg, 5), "decode": round(dec_avg, 5)},
             "in_step_frac": {"encode": frac(enc_avg), "decode": frac(dec_avg)},
             "standalone": {
@@ -639,7 +731,9 @@ def main(argv=None):
             "payload_GiBps": round(value * k / alg_per_block, 3),
             "roofline_frac_of_device_copy": round(achieved / copy_gbs, 4) if copy_gbs else None,
             "host_inclusive": host_incl,
-            "kernel_path": eng.kernel_name,
+            "kernel_path": eng.stream_kernel_name(stream),
+            "collectives": ("rccl" if dist.is_initialized() and dist.get_backend() == "nccl"
+                            else "gloo" if dist.is_initialized() else "none (single process, no torchrun)"),
             "launch": f"hipGraph of {group} steps" if graph is not None else "eager",
             "host_issue_us_per_eager_step": round(t_issue * 1e6, 1),
             "device_ms_per_step": round(gpu_ms_per_step, 4),
@@ -647,7 +741,7 @@ def main(argv=None):
         }
         print(json.dumps(line), flush=True)
     eng.close()
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
     return 0
 

@@ -89,6 +89,11 @@ size_t ppfs_ecc_data_size(const ppfs_ecc_ctx* ctx);
 
 /* Short human-readable name of the kernel path the context dispatches to (for logs/tests). */
 const char* ppfs_ecc_kernel_name(const ppfs_ecc_ctx* ctx);
+/* The kernel path a device call of ctx on `stream` takes: as ppfs_ecc_kernel_name, except for
+ * RS 2t <= 8, whose ticket-counter kernels need one of the context's 16 per-stream counter sets:
+ * a 17th distinct stream, and any stream capturing a hipGraph, get the static-walk kernels
+ * ("rs255-wg-seg4-lds").  Engine extension, no reference counterpart. */
+const char* ppfs_ecc_stream_kernel_name(ppfs_ecc_ctx* ctx, void* stream);
 
 /*
  * Encode nblocks full payloads.  raw is read-modify-write: bits the codec does not define
@@ -188,6 +193,10 @@ int ppfs_inject_device(uint8_t* d_raw, size_t stride, size_t nblocks, const uint
  */
 int ppfs_ecc_host_register(void* ptr, size_t bytes);
 int ppfs_ecc_host_unregister(void* ptr);
+/* Ranges registered through ppfs_ecc_host_register and not yet unregistered: their number (and
+ * their total bytes in *bytes when bytes is non-null).  Diagnostics: tests assert that no range
+ * outlives the test that registered it.  Engine extension, no reference counterpart. */
+long long ppfs_ecc_host_registered(size_t* bytes);
 
 /*
  * Multi-GPU host path: a group of contexts, one per listed HIP device (a device may
@@ -220,6 +229,13 @@ long long ppfs_ecc_debug_faults(void);
 /* PPFS_ECC_DEBUG builds: launches one deliberately out-of-range row gather and returns how many
  * accesses the kernel reported (and skipped), >= 1 when the checks work; -1 in normal builds. */
 long long ppfs_ecc_debug_selftest(void);
+/* PPFS_ECC_DEBUG builds: copies the engine refused because an end was not page-locked host memory /
+ * device memory over its whole range (every hipMemcpy the library issues is checked first);
+ * -1 in normal builds. */
+long long ppfs_ecc_debug_dma_rejects(void);
+/* PPFS_ECC_DEBUG builds: positive control of those checks (a pageable source and a device range past
+ * its allocation must both be refused): 1 when they are, 0 when not, -1 in normal builds. */
+long long ppfs_ecc_debug_dma_selftest(void);
 
 #ifdef __cplusplus
 }

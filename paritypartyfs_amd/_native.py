@@ -26,6 +26,7 @@ EXPORTED_SYMBOLS = (
     "ppfs_ecc_raw_block_size",
     "ppfs_ecc_data_size",
     "ppfs_ecc_kernel_name",
+    "ppfs_ecc_stream_kernel_name",
     "ppfs_ecc_encode_device",
     "ppfs_ecc_decode_device",
     "ppfs_ecc_write_device",
@@ -40,6 +41,7 @@ EXPORTED_SYMBOLS = (
     "ppfs_inject_device",
     "ppfs_ecc_host_register",
     "ppfs_ecc_host_unregister",
+    "ppfs_ecc_host_registered",
     "ppfs_ecc_group_create",
     "ppfs_ecc_group_destroy",
     "ppfs_ecc_group_size",
@@ -50,6 +52,8 @@ EXPORTED_SYMBOLS = (
     "ppfs_ecc_last_error",
     "ppfs_ecc_debug_faults",
     "ppfs_ecc_debug_selftest",
+    "ppfs_ecc_debug_dma_rejects",
+    "ppfs_ecc_debug_dma_selftest",
 )
 
 
@@ -93,6 +97,14 @@ def lib() -> ctypes.CDLL:
     L.ppfs_ecc_debug_faults.argtypes = []
     L.ppfs_ecc_debug_selftest.restype = c_longlong
     L.ppfs_ecc_debug_selftest.argtypes = []
+    L.ppfs_ecc_debug_dma_rejects.restype = c_longlong
+    L.ppfs_ecc_debug_dma_rejects.argtypes = []
+    L.ppfs_ecc_debug_dma_selftest.restype = c_longlong
+    L.ppfs_ecc_debug_dma_selftest.argtypes = []
+    L.ppfs_ecc_host_registered.restype = c_longlong
+    L.ppfs_ecc_host_registered.argtypes = [POINTER(c_size_t)]
+    L.ppfs_ecc_stream_kernel_name.restype = c_char_p
+    L.ppfs_ecc_stream_kernel_name.argtypes = [c_void_p, c_void_p]
     L.ppfs_ecc_crc_implicit_to_explicit.restype = c_uint64
     L.ppfs_ecc_crc_implicit_to_explicit.argtypes = [c_uint64]
     L.ppfs_ecc_create.restype = c_int
@@ -164,6 +176,25 @@ class EccError(RuntimeError):
 def check(rc: int) -> None:
     if rc != 0:
         raise EccError(rc, lib().ppfs_ecc_last_error().decode(errors="replace"))
+
+
+def host_registered() -> tuple[int, int] | None:
+    """(ranges, bytes) still registered through ppfs_ecc_host_register; None if the library is not
+    loaded yet (nothing can have been registered through it then)."""
+    if _lib is None:
+        return None
+    b = c_size_t(0)
+    n = int(_lib.ppfs_ecc_host_registered(ctypes.byref(b)))
+    return n, int(b.value)
+
+
+def debug_dma_rejects() -> int | None:
+    """Copies a PPFS_ECC_DEBUG build refused (an end not page-locked / device memory over its whole
+    range); None for a normal build or when the library is not loaded yet."""
+    if _lib is None:
+        return None
+    v = int(_lib.ppfs_ecc_debug_dma_rejects())
+    return None if v < 0 else v
 
 
 def debug_faults() -> int | None:

@@ -11,9 +11,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <functional>
 #include <cstdio>
+#include <map>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -499,13 +501,43 @@ struct ppfs_ecc_ctx {
     uint32_t srv_gen = 0, srv_seq = 0, flag_seq = 0;
     bool srv_launched = false;
     int srv_ok = -1;
+    // a resident launch that did not leave when asked (server_stop): the context is unusable and
+    // destroy leaks what the launch may still read instead of freeing it under it
+    bool srv_stuck = false;
+    // Completion of the work this context queued on CALLER streams (the device entry points):
+    // one fence-free event per stream, re-recorded after every call, so that destroy waits for
+    // exactly that work (it reads the tables, counters and scratch destroy frees) and not for the
+    // whole device -- other contexts' resident servers, unrelated torch streams.  A stream beyond
+    // kEvSlots sets ev_overflow and destroy falls back to a device-wide synchronize.
+    static constexpr int kEvSlots = 32;
+    hipStream_t ev_stream[kEvSlots] = {};
+    hipEvent_t ev[kEvSlots] = {};
+    int ev_n = 0;
+    bool ev_overflow = false;
 };
 
 namespace {
-// the ticket-counter set of stream s (nullptr: none left, the static kernel encodes)
+// Is s capturing a hipGraph?  Work queued then runs later, once per replay, possibly on another
+// stream or concurrently with itself.
+bool capturing(hipStream_t s)
+{
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return st != hipStreamCaptureStatusNone;
+}
+
+// The ticket-counter set of stream s (nullptr: the static-walk kernel runs).  A set is shared by
+// every launch on its stream, which is safe only because launches on one stream are ordered.  A
+// launch captured into a graph gets no set: its replays may run on other streams or overlap each
+// other (two kernels on one set would skip or repeat tiles).  The 17th distinct stream of a
+// context also falls back (slots are not recycled: a slot's stream may still be running a kernel
+// on it); ppfs_ecc_stream_kernel_name reports which path a stream gets.
 uint32_t* ctr_for(ppfs_ecc_ctx* c, hipStream_t s)
 {
-    if (!c->d_ctr)
+    if (!c->d_ctr || capturing(s))
         return nullptr;
     for (int i = 0; i < c->tk_n; ++i)
         if (c->tk_stream[i] == s)
@@ -520,7 +552,35 @@ uint32_t* dec_ctr(uint32_t* set)
 {
     return set ? set + ppfs_ecc_ctx::kTkSetWords / 2 : nullptr;
 }
+
+// After a device entry point queued work on caller stream s: (re-)record s's completion event.
+// Captured work is the graph's: the caller keeps the context alive while graphs that use it exist.
+void note_caller_stream(ppfs_ecc_ctx* c, hipStream_t s)
+{
+    if (s == c->hs[0] || s == c->hs[1] || capturing(s)) // the context's own streams: destroy drains them
+        return;
+    int i = 0;
+    while (i < c->ev_n && c->ev_stream[i] != s)
+        ++i;
+    if (i == c->ev_n) {
+        if (c->ev_n == ppfs_ecc_ctx::kEvSlots
+            || hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
+            (void)hipGetLastError();
+            c->ev_overflow = true;
+            return;
+        }
+        c->ev_stream[i] = s;
+        c->ev_n++;
+    }
+    if (hipEventRecord(c->ev[i], s) != hipSuccess) {
+        (void)hipGetLastError();
+        c->ev_overflow = true;
+    }
+}
 } // namespace
+
+// every copy the engine queues (checked in PPFS_ECC_DEBUG builds; defined with host_pinned below)
+static hipError_t dma_async(void* dst, const void* src, size_t n, hipMemcpyKind kind, hipStream_t s);
 
 extern "C" uint64_t ppfs_ecc_crc_implicit_to_explicit(uint64_t implicit_poly) { return (implicit_poly << 1) + 1; }
 
@@ -638,9 +698,19 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
         }
     }
     if (!tables.empty()) {
+        // through a page-locked bounce buffer: the engine never hands pageable memory to a copy
+        uint8_t* bounce = nullptr;
         e = hipMalloc(&c->d_tables, tables.size());
         if (e == hipSuccess)
-            e = hipMemcpy(c->d_tables, tables.data(), tables.size(), hipMemcpyHostToDevice);
+            e = hipHostMalloc((void**)&bounce, tables.size(), hipHostMallocDefault);
+        if (e == hipSuccess) {
+            std::memcpy(bounce, tables.data(), tables.size());
+            e = dma_async(c->d_tables, bounce, tables.size(), hipMemcpyHostToDevice, nullptr);
+            if (e == hipSuccess)
+                e = hipStreamSynchronize(nullptr);
+        }
+        if (bounce)
+            (void)hipHostFree(bounce);
         if (e != hipSuccess) {
             ppfs_ecc_destroy(c);
             return fail(PPFS_ECC_EHIP, "table upload", e);
@@ -650,29 +720,69 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
     return 0;
 }
 
+// Ask the resident server launch to leave and wait for it, bounded: it polls `stop` every few
+// microseconds, so a launch still running after kSrvStopMs has stopped polling (a hung or
+// faulted kernel).  Never blocks past the deadline; false = the launch did not leave.
+constexpr int kSrvStopMs = 2000;
+static bool server_halt(ppfs_ecc_ctx* c)
+{
+    if (!c->srv_launched)
+        return true;
+    __atomic_store_n(&c->h_box->stop, 1u, __ATOMIC_RELEASE);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t e = hipStreamQuery(c->srv_stream);
+        if (e != hipErrorNotReady) {
+            (void)hipGetLastError();
+            c->srv_launched = false;
+            return true;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(kSrvStopMs)) {
+            c->srv_stuck = true;
+            c->srv_ok = 0;
+            return false;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
 extern "C" void ppfs_ecc_destroy(ppfs_ecc_ctx* c)
 {
     if (!c)
         return;
     DeviceGuard guard(c->device);
-    // the resident server leaves at `stop` (it polls every few microseconds) before anything it
-    // reads is freed
-    if (c->srv_launched) {
-        __atomic_store_n(&c->h_box->stop, 1u, __ATOMIC_RELEASE);
-        (void)hipStreamSynchronize(c->srv_stream);
-    }
-    if (c->srv_stream)
+    // the resident server leaves at `stop` before anything it reads is freed
+    const bool srv_gone = !c->srv_stuck && server_halt(c);
+    if (c->srv_stream && srv_gone)
         (void)hipStreamDestroy(c->srv_stream);
-    // Nothing the context queued may outlive it: its own streams drain before they are destroyed
-    // and before the staging buffers their copies and kernels use are freed.  Work the caller
-    // queued on its own streams (device entry points) is the caller's to order; the device-wide
-    // synchronize below covers it for the buffers this context owns (tables, scratch).
+    // Nothing the context queued may outlive it, and destroy waits for nothing else:
+    //  - its own streams (host paths) drain before they are destroyed and before the staging
+    //    buffers their copies and kernels use are freed;
+    //  - work it queued on caller streams (device entry points: it reads the tables, ticket
+    //    counters and scratch freed below) is waited for through the per-stream completion events
+    //    note_caller_stream recorded after every call;
+    //  - only when more caller streams were used than there are event slots does destroy fall back
+    //    to a device-wide synchronize.
+    // Other contexts' resident servers and unrelated streams are not waited for.
     for (int i = 0; i < 2; ++i)
         if (c->hs[i])
             (void)hipStreamSynchronize(c->hs[i]);
-    if (c->d_tables || c->d_scratch)
+    for (int i = 0; i < c->ev_n; ++i) {
+        (void)hipEventSynchronize(c->ev[i]);
+        (void)hipEventDestroy(c->ev[i]);
+    }
+    if (c->ev_overflow && (c->d_tables || c->d_scratch || c->d_ctr))
         (void)hipDeviceSynchronize();
     (void)hipGetLastError();
+    if (!srv_gone) {
+        // a launch that ignored `stop` may still read the tables and the mailbox / zero-copy
+        // buffers: leak those rather than free memory under a running kernel
+        std::fprintf(stderr, "ppfs_ecc_destroy: resident server did not stop within %d ms; its buffers are leaked\n",
+            kSrvStopMs);
+        c->d_tables = nullptr;
+        c->h_zc = nullptr;
+        c->h_box = nullptr;
+    }
     for (int i = 0; i < 2; ++i) {
         if (c->hs[i])
             (void)hipStreamDestroy(c->hs[i]);
@@ -764,7 +874,7 @@ static int ppfs_ecc_encode_device_impl(ppfs_ecc_ctx* c, const uint8_t* d_data, u
     hipStream_t s = (hipStream_t)stream;
     switch (c->p.ecc_type) {
     case PPFS_ECC_NONE:
-        return check_hip(hipMemcpyAsync(d_raw, d_data, nblocks * c->raw, hipMemcpyDeviceToDevice, s), "copy");
+        return check_hip(dma_async(d_raw, d_data, nblocks * c->raw, hipMemcpyDeviceToDevice, s), "copy");
     case PPFS_ECC_REED_SOLOMON:
         if (c->rs_fast && aligned16(d_data) && aligned16(d_raw))
             return check_hip(ppfs_rs_fast_encode(c->rs_t2, d_data, d_raw, nblocks, c->d_tables, s, ctr_for(c, s)), "rs encode");
@@ -805,7 +915,7 @@ static int ppfs_ecc_decode_device_impl(ppfs_ecc_ctx* c, uint8_t* d_raw, uint8_t*
                 return r;
         }
         if (d_data)
-            return check_hip(hipMemcpyAsync(d_data, d_raw, nblocks * c->raw, hipMemcpyDeviceToDevice, s), "copy");
+            return check_hip(dma_async(d_data, d_raw, nblocks * c->raw, hipMemcpyDeviceToDevice, s), "copy");
         return 0;
     case PPFS_ECC_REED_SOLOMON:
         if (c->rs_fast) {
@@ -875,7 +985,7 @@ static int ppfs_ecc_write_device_impl(ppfs_ecc_ctx* c, const uint8_t* d_data, ui
     case PPFS_ECC_NONE:
         if (d_status && (r = check_hip(hipMemsetAsync(d_status, 0, nblocks, s), "status")))
             return r;
-        return check_hip(hipMemcpyAsync(d_raw, d_data, nblocks * c->raw, hipMemcpyDeviceToDevice, s), "copy");
+        return check_hip(dma_async(d_raw, d_data, nblocks * c->raw, hipMemcpyDeviceToDevice, s), "copy");
     case PPFS_ECC_REED_SOLOMON:
         // old block decoded for its status (correction event) only; the new codeword does
         // not depend on it (rs_block_device.cpp:61-93)
@@ -902,25 +1012,48 @@ static int ppfs_ecc_write_device_impl(ppfs_ecc_ctx* c, const uint8_t* d_data, ui
     return fail(PPFS_ECC_EINVAL, "bad ctx");
 }
 
+// device entry points: queue, then record the caller stream's completion event (destroy waits
+// on it), then (PPFS_ECC_SYNC_CHECK) report an asynchronous fault under the entry's own name
+static int queued(ppfs_ecc_ctx* c, int r, size_t nblocks, void* stream, const char* what)
+{
+    if (!r && nblocks)
+        note_caller_stream(c, (hipStream_t)stream);
+    return sync_check(r, stream, what);
+}
+
 extern "C" int ppfs_ecc_encode_device(ppfs_ecc_ctx* c, const uint8_t* d_data, uint8_t* d_raw, size_t nblocks,
     void* stream)
 {
-    return sync_check(ppfs_ecc_encode_device_impl(c, d_data, d_raw, nblocks, stream), stream, "encode (async)");
+    return queued(c, ppfs_ecc_encode_device_impl(c, d_data, d_raw, nblocks, stream), nblocks, stream, "encode (async)");
 }
 
 extern "C" int ppfs_ecc_decode_device(ppfs_ecc_ctx* c, uint8_t* d_raw, uint8_t* d_data, uint8_t* d_status,
     size_t nblocks, int write_back, uint8_t* d_spill, void* stream)
 {
-    return sync_check(
-        ppfs_ecc_decode_device_impl(c, d_raw, d_data, d_status, nblocks, write_back, d_spill, stream), stream,
-        "decode (async)");
+    return queued(c, ppfs_ecc_decode_device_impl(c, d_raw, d_data, d_status, nblocks, write_back, d_spill, stream),
+        nblocks, stream, "decode (async)");
 }
 
 extern "C" int ppfs_ecc_write_device(ppfs_ecc_ctx* c, const uint8_t* d_data, uint8_t* d_raw, uint8_t* d_status,
     size_t nblocks, void* stream)
 {
-    return sync_check(ppfs_ecc_write_device_impl(c, d_data, d_raw, d_status, nblocks, stream), stream,
+    return queued(c, ppfs_ecc_write_device_impl(c, d_data, d_raw, d_status, nblocks, stream), nblocks, stream,
         "write (async)");
+}
+
+extern "C" const char* ppfs_ecc_stream_kernel_name(ppfs_ecc_ctx* c, void* stream)
+{
+    if (!c)
+        return "";
+    if (c->d_ctr) { // 2t <= 8: ticket kernels while the stream has (or can get) a counter set
+        const hipStream_t s = (hipStream_t)stream;
+        bool has = false;
+        for (int i = 0; i < c->tk_n; ++i)
+            has = has || c->tk_stream[i] == s;
+        if (capturing(s) || (!has && c->tk_n == ppfs_ecc_ctx::kTkSlots))
+            return "rs255-wg-seg4-lds"; // rs_wg.hpp static walk
+    }
+    return c->kname;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1055,6 +1188,96 @@ static bool host_pinned(const void* p, size_t bytes)
     return true;
 }
 
+// Device memory over the whole range [p, p + n): both ends device memory and, where the runtime
+// keeps an allocation record (hipMalloc; not stream-ordered pool memory), inside one allocation.
+[[maybe_unused]] static bool device_range(const void* p, size_t n)
+{
+    if (!p || !n)
+        return true;
+    auto dev_byte = [](const void* q) {
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        return a.type == hipMemoryTypeDevice;
+    };
+    const uintptr_t a = (uintptr_t)p, last = a + n - 1;
+    if (!dev_byte(p) || !dev_byte((const void*)last))
+        return false;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) == hipSuccess && base && size)
+        return (uintptr_t)base <= a && last < (uintptr_t)base + size;
+    (void)hipGetLastError();
+    return true;
+}
+
+[[maybe_unused]] static std::atomic<long long> g_dma_rejects { 0 };
+
+// Every hipMemcpyAsync of this file.  PPFS_ECC_DEBUG builds check both ends first: a host end
+// must be page-locked over its whole range (host_pinned: the engine's own staging, a hipHostMalloc'd
+// or ppfs_ecc_host_register'd caller buffer), a device end device memory over its whole range
+// (device_range).  A copy that fails the check is refused -- counted (ppfs_ecc_debug_dma_rejects),
+// printed, returned as an error -- never handed to the runtime's pageable-copy path or to the DMA
+// engines.  Normal builds: the copy as is.
+static hipError_t dma_async(void* dst, const void* src, size_t n, hipMemcpyKind kind, hipStream_t s)
+{
+#ifdef PPFS_ECC_DEBUG
+    if (n) {
+        const bool src_dev = kind == hipMemcpyDeviceToHost || kind == hipMemcpyDeviceToDevice;
+        const bool dst_dev = kind == hipMemcpyHostToDevice || kind == hipMemcpyDeviceToDevice;
+        const bool src_ok = src_dev ? device_range(src, n) : host_pinned(src, n);
+        const bool dst_ok = dst_dev ? device_range(dst, n) : host_pinned(dst, n);
+        if (!src_ok || !dst_ok) {
+            const long long k = ++g_dma_rejects;
+            if (k <= 16)
+                std::fprintf(stderr, "PPFS_ECC_DEBUG: refused copy of %zu B %p -> %p (kind %d): %s end not %s over its range\n",
+                    n, src, dst, (int)kind, src_ok ? "destination" : "source",
+                    (src_ok ? dst_dev : src_dev) ? "device memory" : "page-locked");
+            return hipErrorInvalidValue;
+        }
+    }
+#endif
+    return hipMemcpyAsync(dst, src, n, kind, s);
+}
+
+extern "C" long long ppfs_ecc_debug_dma_rejects(void)
+{
+#ifdef PPFS_ECC_DEBUG
+    return g_dma_rejects.load();
+#else
+    return -1;
+#endif
+}
+
+// Positive control of the copy checks: a copy from malloc'd (pageable) memory and one into a range
+// that runs past its device allocation must both be refused.  1 = both refused (the reject counter
+// is restored, so the control does not count as a finding), 0 = a check let one through, -1 in
+// normal builds.
+extern "C" long long ppfs_ecc_debug_dma_selftest(void)
+{
+#ifdef PPFS_ECC_DEBUG
+    const long long before = g_dma_rejects.load();
+    uint8_t* pageable = (uint8_t*)std::malloc(4096);
+    uint8_t* d = nullptr;
+    if (!pageable || hipMalloc(&d, 4096) != hipSuccess) {
+        std::free(pageable);
+        return 0;
+    }
+    const bool r1 = dma_async(d, pageable, 4096, hipMemcpyHostToDevice, nullptr) != hipSuccess;
+    const bool r2 = dma_async(d + 4096 - 16, d, 32, hipMemcpyDeviceToDevice, nullptr) != hipSuccess;
+    (void)hipGetLastError();
+    (void)hipStreamSynchronize(nullptr);
+    (void)hipFree(d);
+    std::free(pageable);
+    g_dma_rejects.store(before);
+    return (r1 && r2) ? 1 : 0;
+#else
+    return -1;
+#endif
+}
+
 static int device_op(ppfs_ecc_ctx* c, HostOp op, uint8_t* d, const Layout& L, size_t nb, int write_back, bool want_data,
     bool want_spill, hipStream_t s)
 {
@@ -1095,15 +1318,13 @@ static bool server_eligible(ppfs_ecc_ctx* c)
     return c->srv_ok == 1;
 }
 
-// stop the resident launch (if any) and wait until it has returned
-static void server_stop(ppfs_ecc_ctx* c)
+// stop the resident launch (if any) and wait until it has returned (bounded, server_halt); an
+// error when it did not: the context is then unusable (srv_stuck)
+static int server_stop(ppfs_ecc_ctx* c)
 {
-    if (!c->srv_launched)
-        return;
-    __atomic_store_n(&c->h_box->stop, 1u, __ATOMIC_RELEASE);
-    (void)hipStreamSynchronize(c->srv_stream);
-    (void)hipGetLastError();
-    c->srv_launched = false;
+    if (server_halt(c))
+        return 0;
+    return fail(PPFS_ECC_EHIP, "small-batch server did not stop: context unusable");
 }
 
 static int server_launch(ppfs_ecc_ctx* c)
@@ -1196,11 +1417,12 @@ static int server_call(ppfs_ecc_ctx* c, HostOp op, const Layout& L, size_t nb, i
                 if (r)
                     return r;
             } else if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
-                server_stop(c);
+                const bool stopped = server_stop(c) == 0; // bounded: never hangs on a launch that stopped polling
                 c->srv_ok = 0; // this context uses the launch path from now on
-                if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq)
+                if (stopped && __atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq)
                     return 0;
-                return fail(PPFS_ECC_EHIP, "small-batch server: no answer within 10 s");
+                return fail(PPFS_ECC_EHIP, stopped ? "small-batch server: no answer within 10 s"
+                                                   : "small-batch server: no answer within 10 s and did not stop: context unusable");
             }
         }
     }
@@ -1213,7 +1435,8 @@ static int host_run_small(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, ui
 {
     const Layout L = layout_for(c, nb);
     if (c->zc_bytes < L.total) {
-        server_stop(c); // it holds the buffer's address
+        if (server_stop(c)) // it holds the buffer's address
+            return PPFS_ECC_EHIP;
         if (c->h_zc && c->hs[0])
             HIP_TRY(hipStreamSynchronize(c->hs[0]), "zero-copy sync");
         if (c->h_zc)
@@ -1271,6 +1494,8 @@ static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t*
 {
     if (!c)
         return fail(PPFS_ECC_EINVAL, "null ctx");
+    if (c->srv_stuck)
+        return fail(PPFS_ECC_EHIP, "context unusable: its resident server launch did not stop");
     if (nblocks == 0)
         return 0;
     DeviceGuard guard(c->device);
@@ -1339,16 +1564,16 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
         }
         if (nchg > nb / kGatherDiv) { // many: the whole range
             uint8_t* o = direct ? raw + b0 * c->raw : h + L.raw;
-            HIP_TRY(hipMemcpyAsync(o, d + L.raw, nb * c->raw, hipMemcpyDeviceToHost, s), "D2H raw");
+            HIP_TRY(dma_async(o, d + L.raw, nb * c->raw, hipMemcpyDeviceToHost, s), "D2H raw");
             HIP_TRY(hipStreamSynchronize(s), "sync");
             if (!direct)
                 par_memcpy(raw + b0 * c->raw, h + L.raw, nb * c->raw);
             return 0;
         }
-        HIP_TRY(hipMemcpyAsync(d + L.idx, ix, nchg * sizeof(uint32_t), hipMemcpyHostToDevice, s), "H2D idx");
+        HIP_TRY(dma_async(d + L.idx, ix, nchg * sizeof(uint32_t), hipMemcpyHostToDevice, s), "H2D idx");
         HIP_TRY(ppfs_gather_rows_launch(d + L.raw, nb, d + L.gat, (const uint32_t*)(d + L.idx), (uint32_t)nchg,
                     (uint32_t)c->raw, s), "gather");
-        HIP_TRY(hipMemcpyAsync(h + L.gat, d + L.gat, nchg * c->raw, hipMemcpyDeviceToHost, s), "D2H gather");
+        HIP_TRY(dma_async(h + L.gat, d + L.gat, nchg * c->raw, hipMemcpyDeviceToHost, s), "D2H gather");
         HIP_TRY(hipStreamSynchronize(s), "sync");
         for (size_t j = 0; j < nchg; ++j)
             std::memcpy(raw + (b0 + ix[j]) * c->raw, h + L.gat + j * c->raw, c->raw);
@@ -1395,10 +1620,10 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
         const bool need_raw = op != OP_ENCODE || raw_is_rmw(c);
         if (direct) {
             if (need_data)
-                HIP_TRY(hipMemcpyAsync(d + L.data, data_in + b0 * c->data, nb * c->data, hipMemcpyHostToDevice, s),
+                HIP_TRY(dma_async(d + L.data, data_in + b0 * c->data, nb * c->data, hipMemcpyHostToDevice, s),
                     "H2D data");
             if (need_raw)
-                HIP_TRY(hipMemcpyAsync(d + L.raw, raw + b0 * c->raw, nb * c->raw, hipMemcpyHostToDevice, s), "H2D raw");
+                HIP_TRY(dma_async(d + L.raw, raw + b0 * c->raw, nb * c->raw, hipMemcpyHostToDevice, s), "H2D raw");
         } else {
             if (need_data)
                 par_memcpy(h + L.data, data_in + b0 * c->data, nb * c->data);
@@ -1406,7 +1631,7 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
                 par_memcpy(h + L.raw, raw + b0 * c->raw, nb * c->raw);
             const size_t in_lo = need_data ? L.data : L.raw;
             const size_t in_hi = need_raw ? L.raw + nb * c->raw : L.data + nb * c->data;
-            HIP_TRY(hipMemcpyAsync(d + in_lo, h + in_lo, in_hi - in_lo, hipMemcpyHostToDevice, s), "H2D");
+            HIP_TRY(dma_async(d + in_lo, h + in_lo, in_hi - in_lo, hipMemcpyHostToDevice, s), "H2D");
         }
         switch (op) {
         case OP_ENCODE:
@@ -1431,7 +1656,7 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
             // instead of up to four -- each copy is a few us of latency on the critical path
             const size_t lo = want_data ? L.data : L.raw;
             const size_t hi = spill ? L.spill + nb * spill_b : (want_st ? L.status + nb : L.raw + nb * c->raw);
-            HIP_TRY(hipMemcpyAsync(h + lo, d + lo, hi - lo, hipMemcpyDeviceToHost, s), "D2H");
+            HIP_TRY(dma_async(h + lo, d + lo, hi - lo, hipMemcpyDeviceToHost, s), "D2H");
             fetched[slot] = true;
         } else {
             fetched[slot] = want_raw;
@@ -1440,13 +1665,13 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
             uint8_t* o_st = (direct && status) ? status + b0 : h + L.status;
             uint8_t* o_sp = direct ? (spill ? spill + b0 * spill_b : nullptr) : h + L.spill;
             if (want_raw)
-                HIP_TRY(hipMemcpyAsync(o_raw, d + L.raw, nb * c->raw, hipMemcpyDeviceToHost, s), "D2H raw");
+                HIP_TRY(dma_async(o_raw, d + L.raw, nb * c->raw, hipMemcpyDeviceToHost, s), "D2H raw");
             if (want_data)
-                HIP_TRY(hipMemcpyAsync(o_data, d + L.data, nb * c->data, hipMemcpyDeviceToHost, s), "D2H data");
+                HIP_TRY(dma_async(o_data, d + L.data, nb * c->data, hipMemcpyDeviceToHost, s), "D2H data");
             if (want_st)
-                HIP_TRY(hipMemcpyAsync(o_st, d + L.status, nb, hipMemcpyDeviceToHost, s), "D2H status");
+                HIP_TRY(dma_async(o_st, d + L.status, nb, hipMemcpyDeviceToHost, s), "D2H status");
             if (spill)
-                HIP_TRY(hipMemcpyAsync(o_sp, d + L.spill, nb * spill_b, hipMemcpyDeviceToHost, s), "D2H spill");
+                HIP_TRY(dma_async(o_sp, d + L.spill, nb * spill_b, hipMemcpyDeviceToHost, s), "D2H spill");
         }
         pending_first[slot] = b0;
         pending_n[slot] = nb;
@@ -1565,8 +1790,13 @@ extern "C" int ppfs_ecc_scrub_device(ppfs_ecc_ctx* c, uint8_t* d_image, size_t i
     const size_t n = c->raw, sb = 256 - std::min<size_t>(n, 255);
     const bool chain = c->p.ecc_type == PPFS_ECC_REED_SOLOMON && c->rs_n < 255;
     uint8_t* d_spill = nullptr;
+    uint8_t* bounce = nullptr; // page-locked: the spill records and patches never DMA pageable memory
     if (chain) {
         HIP_TRY(hipMallocAsync((void**)&d_spill, nblocks * sb, s), "scrub spill alloc");
+        if (hipHostMalloc((void**)&bounce, std::max<size_t>(nblocks * sb, 256), hipHostMallocDefault) != hipSuccess) {
+            (void)hipFreeAsync(d_spill, s);
+            return fail(PPFS_ECC_ENOMEM, "scrub spill bounce");
+        }
     }
     ScrubOps ops;
     ops.decode = [&](size_t b0, size_t nb, int wb, uint8_t* st_host, uint8_t* spill_host) {
@@ -1576,20 +1806,26 @@ extern "C" int ppfs_ecc_scrub_device(ppfs_ecc_ctx* c, uint8_t* d_image, size_t i
             stream);
         if (r || !spill_host)
             return r;
-        HIP_TRY(hipMemcpyAsync(spill_host, d_spill + b0 * sb, nb * sb, hipMemcpyDeviceToHost, s), "scrub spill D2H");
+        HIP_TRY(dma_async(bounce, d_spill + b0 * sb, nb * sb, hipMemcpyDeviceToHost, s), "scrub spill D2H");
         HIP_TRY(hipStreamSynchronize(s), "scrub sync");
+        std::memcpy(spill_host, bounce, nb * sb);
         return 0;
     };
-    ops.put = [&](size_t addr, const uint8_t* src, size_t len) {
-        HIP_TRY(hipMemcpyAsync(d_image + addr, src, len, hipMemcpyHostToDevice, s), "scrub spill H2D");
-        HIP_TRY(hipStreamSynchronize(s), "scrub sync"); // src is a host vector that goes away
+    ops.put = [&](size_t addr, const uint8_t* src, size_t len) { // len <= 255 - n < 256
+        std::memcpy(bounce, src, len);
+        HIP_TRY(dma_async(d_image + addr, bounce, len, hipMemcpyHostToDevice, s), "scrub spill H2D");
+        HIP_TRY(hipStreamSynchronize(s), "scrub sync"); // the bounce is reused by the next call
         return 0;
     };
     // status bytes live on the device; scrub_run only indexes st (never reads it)
     std::vector<uint8_t> dummy(chain ? nblocks : 0);
     const int r = scrub_run(c, image_bytes, nblocks, dummy.data(), ops);
-    if (d_spill)
+    if (d_spill) {
         (void)hipFreeAsync(d_spill, s);
+        (void)hipStreamSynchronize(s); // the bounce's last copy is done before it is freed
+    }
+    if (bounce)
+        (void)hipHostFree(bounce);
     return r;
 }
 
@@ -1659,13 +1895,13 @@ extern "C" int ppfs_vote3_host(int device, const uint8_t* a, const uint8_t* b, c
         std::memcpy(h, a, nbytes);
         std::memcpy(h + nbytes, b, nbytes);
         std::memcpy(h + 2 * nbytes, c, nbytes);
-        e = hipMemcpyAsync(d, h, 3 * nbytes, hipMemcpyHostToDevice, s);
+        e = dma_async(d, h, 3 * nbytes, hipMemcpyHostToDevice, s);
     }
     if (e == hipSuccess)
         e = ppfs_vote3_launch(d, d + nbytes, d + 2 * nbytes, d + 3 * nbytes, rec_bytes, nrec,
             damaged ? (uint32_t*)(d + dmg_off) : nullptr, s);
     if (e == hipSuccess)
-        e = hipMemcpyAsync(h + 3 * nbytes, d + 3 * nbytes, total - 3 * nbytes, hipMemcpyDeviceToHost, s);
+        e = dma_async(h + 3 * nbytes, d + 3 * nbytes, total - 3 * nbytes, hipMemcpyDeviceToHost, s);
     const hipError_t es = hipStreamSynchronize(s);
     if (e == hipSuccess)
         e = es;
@@ -1686,11 +1922,22 @@ extern "C" int ppfs_vote3_host(int device, const uint8_t* a, const uint8_t* b, c
 // ---------------------------------------------------------------------------------------
 // Page-locking of caller memory (a pinned host mirror of the disk image)
 // ---------------------------------------------------------------------------------------
+// Registry of the ranges registered through this ABI (start -> bytes): ppfs_ecc_host_registered
+// lets a caller (tests/conftest.py) check that no engine-registered range outlives its owner --
+// a range still registered after its memory went back to the allocator would let a later,
+// unrelated buffer at the same address be treated as page-locked.
+namespace {
+std::mutex g_reg_mu;
+std::map<uintptr_t, size_t> g_reg;
+} // namespace
+
 extern "C" int ppfs_ecc_host_register(void* ptr, size_t bytes)
 {
     if (!ptr || !bytes)
         return fail(PPFS_ECC_EINVAL, "host_register: bad argument");
+    std::lock_guard<std::mutex> lk(g_reg_mu);
     HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault), "hipHostRegister");
+    g_reg[(uintptr_t)ptr] = bytes;
     return 0;
 }
 
@@ -1698,8 +1945,22 @@ extern "C" int ppfs_ecc_host_unregister(void* ptr)
 {
     if (!ptr)
         return fail(PPFS_ECC_EINVAL, "host_unregister: null pointer");
+    std::lock_guard<std::mutex> lk(g_reg_mu);
     HIP_TRY(hipHostUnregister(ptr), "hipHostUnregister");
+    g_reg.erase((uintptr_t)ptr);
     return 0;
+}
+
+extern "C" long long ppfs_ecc_host_registered(size_t* bytes)
+{
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    if (bytes) {
+        size_t b = 0;
+        for (const auto& kv : g_reg)
+            b += kv.second;
+        *bytes = b;
+    }
+    return (long long)g_reg.size();
 }
 
 // ------------------------------------------------------------------------------------------

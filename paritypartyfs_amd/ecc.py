@@ -82,6 +82,12 @@ class EccEngine:
         self.data_size = int(lib().ppfs_ecc_data_size(h))
         self.kernel_name = lib().ppfs_ecc_kernel_name(h).decode()
 
+    def stream_kernel_name(self, stream=None) -> str:
+        """The kernel path a device call on `stream` (default: torch's current stream) takes
+        (ppfs_ecc_stream_kernel_name): kernel_name, except that RS 2t <= 8 runs its static-walk
+        kernels on a 17th distinct stream and on a stream capturing a graph."""
+        return lib().ppfs_ecc_stream_kernel_name(self._h, _stream_handle(stream)).decode()
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
             lib().ppfs_ecc_destroy(self._h)
@@ -231,8 +237,10 @@ class pinned:
         return self
 
     def __exit__(self, *exc):
-        for a in self._arrays:
-            check(lib().ppfs_ecc_host_unregister(_ptr(a)))
+        # every array is released even when one release fails; the first failure is raised after
+        rcs = [lib().ppfs_ecc_host_unregister(_ptr(a)) for a in self._arrays]
+        for rc in rcs:
+            check(rc)
         return False
 
 

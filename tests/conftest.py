@@ -33,7 +33,10 @@ def _gpu_fault_guard(request):
     is then reported against that test, not at the next unrelated torch call."""
     from paritypartyfs_amd import _native
 
-    before = _native.debug_faults() if request.node.get_closest_marker("gpu") is not None else None
+    gpu = request.node.get_closest_marker("gpu") is not None
+    before = _native.debug_faults() if gpu else None
+    reg_before = _native.host_registered() if gpu else None
+    dma_before = _native.debug_dma_rejects() if gpu else None
     yield
     if request.node.get_closest_marker("gpu") is None:
         return
@@ -53,3 +56,15 @@ def _gpu_fault_guard(request):
     if after is not None and after != (before or 0):
         pytest.fail(f"{after - (before or 0)} out-of-bounds kernel accesses in {request.node.nodeid} "
                     "(PPFS_ECC_DEBUG; details on stdout)", pytrace=False)
+    # PPFS_ECC_DEBUG builds refuse every engine copy with an end that is not page-locked / device
+    # memory over its whole range (api.cpp dma_async): none may have been refused
+    dma_after = _native.debug_dma_rejects()
+    if dma_after is not None and dma_after != (dma_before or 0):
+        pytest.fail(f"{dma_after - (dma_before or 0)} engine copies refused in {request.node.nodeid}: an end was not "
+                    "page-locked / device memory over its range (PPFS_ECC_DEBUG; details on stderr)", pytrace=False)
+    # no range registered through ppfs_ecc_host_register outlives the test that registered it (a stale
+    # registration would make a later buffer at the same address look page-locked to the engine)
+    reg_after = _native.host_registered()
+    if reg_after is not None and reg_after[0] > (reg_before[0] if reg_before else 0):
+        pytest.fail(f"{reg_after[0] - (reg_before[0] if reg_before else 0)} host range(s) registered through "
+                    f"ppfs_ecc_host_register outlived {request.node.nodeid} ({reg_after[1]} B registered)", pytrace=False)

@@ -1,0 +1,195 @@
+"""GPU tests of context lifetime and launch-path bookkeeping (round 3):
+
+- ppfs_ecc_destroy waits for the work its context queued and for nothing else: destroying context A
+  while context B's resident server is busy serving per-block calls takes milliseconds, not B's
+  server lifetime, and B keeps answering correctly (api.cpp note_caller_stream / ppfs_ecc_destroy);
+- a hipGraph captured from encode + decode uses the static-walk kernels, never a stream's
+  ticket-counter set, so replays of two such graphs on two streams at once, and a replay beside
+  eager work on the capture's stream, stay bit-exact (api.cpp ctr_for);
+- ppfs_ecc_stream_kernel_name reports the static walk for a 17th stream and during capture;
+- every range registered through ppfs_ecc_host_register is released by `pinned` (the registry the
+  conftest guard checks after every GPU test);
+- the PPFS_ECC_DEBUG build's copy checks refuse a pageable source (positive control).
+"""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from tests.conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+if gpu_available():
+    import torch
+
+from paritypartyfs_amd import ECC_REED_SOLOMON, EccEngine, _native, pinned
+
+STATIC = "rs255-wg-seg4-lds"
+
+
+def _rs_batch(oracle, nb, seed, bs=512, t=3):
+    n, k, _ = oracle.rs_sizes(bs, t)
+    rng = np.random.default_rng(seed)
+    data = rng.integers(0, 256, nb * k, dtype=np.uint8)
+    return n, k, data, oracle.rs_encode(bs, t, data)
+
+
+def test_destroy_does_not_wait_for_another_contexts_server(oracle):
+    """B serves one-block decodes from its resident launch in a loop (the launch stays up to 1 s); A
+    queues a batch on torch's stream and is destroyed: A's destroy waits for A's batch only."""
+    n, k, data, cw = _rs_batch(oracle, 64, 31)
+    B = EccEngine(ECC_REED_SOLOMON, 512, 3)
+    stop = threading.Event()
+    errors, calls = [], [0]
+
+    def serve():
+        raw = cw[:n].copy()
+        out = np.empty(k, np.uint8)
+        st = np.empty(1, np.uint8)
+        try:
+            while not stop.is_set():
+                bad = raw.copy()
+                bad[calls[0] % n] ^= 0x41
+                B.decode_host(bad, out, st, write_back=True)
+                if not (np.array_equal(out, data[:k]) and st[0] == 1 and np.array_equal(bad, raw)):
+                    errors.append(calls[0])
+                calls[0] += 1
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(repr(e))
+
+    th = threading.Thread(target=serve)
+    th.start()
+    try:
+        time.sleep(0.2)  # B's server is resident and busy
+        nb = 1 << 16
+        _, _, adata, acw = _rs_batch(oracle, nb, 32)
+        d = torch.from_numpy(adata).cuda()
+        r = torch.zeros(nb * n, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        times = []
+        for _ in range(5):
+            A = EccEngine(ECC_REED_SOLOMON, 512, 3)
+            A.encode(d, r)  # queued on torch's stream
+            t0 = time.perf_counter()
+            A.close()
+            times.append(time.perf_counter() - t0)
+            torch.cuda.synchronize()
+            assert np.array_equal(r.cpu().numpy(), acw)  # A's work finished before its tables went away
+            r.zero_()
+        time.sleep(0.1)
+    finally:
+        stop.set()
+        th.join(60)
+    assert not errors, errors[:5]
+    assert calls[0] > 100, calls[0]  # B kept serving throughout
+    # a device-wide synchronize would wait for B's resident launch (up to SRV_LIFETIME_US = 1 s)
+    assert max(times) < 0.25, times
+    B.close()
+
+
+def test_destroy_waits_for_work_on_every_caller_stream(oracle):
+    """Work queued on several caller streams, then destroy at once: every batch is complete and
+    bit-exact afterwards (each stream's completion event was waited for)."""
+    nb = 1 << 15
+    n, k, data, cw = _rs_batch(oracle, nb, 33)
+    d = torch.from_numpy(data).cuda()
+    streams = [torch.cuda.Stream() for _ in range(5)]
+    outs = [torch.zeros(nb * n, dtype=torch.uint8, device="cuda") for _ in streams]
+    torch.cuda.synchronize()
+    eng = EccEngine(ECC_REED_SOLOMON, 512, 3)
+    for s, o in zip(streams, outs):
+        for _ in range(3):
+            eng.encode(d, o, stream=s)
+    eng.close()
+    torch.cuda.synchronize()
+    for o in outs:
+        assert np.array_equal(o.cpu().numpy(), cw)
+
+
+def _capture(eng, data, cw, out, st, nb):
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        assert eng.stream_kernel_name() == STATIC  # no ticket set inside a capture
+        eng.encode(data, cw, nblocks=nb)
+        eng.decode(cw, out, st, write_back=True, nblocks=nb)
+    return g
+
+
+def test_graph_replays_on_two_streams_at_once(oracle):
+    """Two graphs of encode + decode (each its own buffers) replayed concurrently on two streams,
+    and one replayed beside eager launches on its capture's stream: bit-exact every time.  With the
+    capture stream's ticket set baked into the graphs, the concurrent replays would share counters
+    and skip or repeat tiles."""
+    nb = (1 << 18) + 5
+    n, k, data, cw = _rs_batch(oracle, nb, 34)
+    eng = EccEngine(ECC_REED_SOLOMON, 512, 3)
+    assert eng.kernel_name == "rs255-wg-tk-lds"
+    d = torch.from_numpy(data).cuda()
+    bufs = [(torch.zeros(nb * n, dtype=torch.uint8, device="cuda"), torch.zeros(nb * k, dtype=torch.uint8, device="cuda"),
+             torch.zeros(nb, dtype=torch.uint8, device="cuda")) for _ in range(3)]
+    eng.encode(d, bufs[0][0], nblocks=nb)  # eager first: loads the kernels
+    torch.cuda.synchronize()
+    graphs = [_capture(eng, d, c, o, s, nb) for c, o, s in bufs[:2]]
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    want_cw = torch.from_numpy(cw).cuda()
+    for _ in range(3):
+        for c, o, s in bufs:
+            c.zero_(), o.zero_(), s.fill_(9)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(sa):
+            graphs[0].replay()
+        with torch.cuda.stream(sb):
+            graphs[1].replay()
+            eng.encode(d, bufs[2][0], nblocks=nb)  # eager beside the replays (ticket kernels)
+            eng.decode(bufs[2][0], bufs[2][1], bufs[2][2], write_back=True, nblocks=nb)
+        torch.cuda.synchronize()
+        for c, o, s in bufs:
+            assert torch.equal(c, want_cw)
+            assert torch.equal(o, d)
+            assert int(s.max()) == 0
+    assert eng.stream_kernel_name() == "rs255-wg-tk-lds"  # outside a capture: ticket kernels again
+    del graphs
+    eng.close()
+
+
+def test_stream_kernel_name_reports_the_static_walk_past_16_streams():
+    eng = EccEngine(ECC_REED_SOLOMON, 512, 3)
+    d = torch.zeros(64 * 249, dtype=torch.uint8, device="cuda")
+    r = torch.zeros(64 * 255, dtype=torch.uint8, device="cuda")
+    streams = [torch.cuda.Stream() for _ in range(17)]
+    names = []
+    for s in streams:
+        names.append(eng.stream_kernel_name(s))
+        eng.encode(d, r, stream=s)
+    torch.cuda.synchronize()
+    assert names[:16] == ["rs255-wg-tk-lds"] * 16
+    assert eng.stream_kernel_name(streams[16]) == STATIC
+    assert eng.stream_kernel_name(streams[3]) == "rs255-wg-tk-lds"
+    eng.close()
+    hm = EccEngine(ECC_REED_SOLOMON, 4096, 16)  # no ticket kernels: always its own path
+    assert hm.stream_kernel_name(streams[16]) == hm.kernel_name == "rs255-bs-byte-lds"
+    hm.close()
+
+
+def test_pinned_releases_every_registered_range():
+    base = _native.host_registered()
+    base = base[0] if base else 0
+    a = np.zeros(1 << 20, np.uint8)
+    b = np.zeros(3 << 20, np.uint8)
+    with pinned(a, b):
+        cnt, nbytes = _native.host_registered()
+        assert cnt == base + 2 and nbytes >= a.nbytes + b.nbytes
+    assert _native.host_registered()[0] == base
+
+
+def test_debug_copy_checks_positive_control():
+    """PPFS_ECC_DEBUG builds refuse a copy from pageable memory and one past a device allocation;
+    normal builds have no checks (-1)."""
+    L = _native.lib()
+    v = L.ppfs_ecc_debug_dma_selftest()
+    if _native.debug_faults() is None:
+        assert v == -1 and _native.debug_dma_rejects() is None
+    else:
+        assert v == 1, v

@@ -66,6 +66,38 @@ def test_bench_gpus2_launches_two_ranks():
     assert line["ms_per_step"] >= 2.0 * 0.95  # rank 1's stand-in sleeps 2 ms per step
 
 
+def test_bench_gpus2_argv_reaches_every_rank():
+    """The driver's configs[4] form `python bench.py --gpus 2 --block-size 4096 --t 16`: the launcher
+    passes the argv to every rank unchanged (each rank reports what it parsed, all_gather over gloo)."""
+    import json
+    import subprocess
+
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--block-size", "4096", "--t", "16", "--blocks", "12345", "--dry-run-cpu"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][0]
+    ranks = sorted(line["rank_args"], key=lambda a: a["rank"])
+    assert [a["rank"] for a in ranks] == [0, 1]
+    assert all(a["block_size"] == 4096 and a["t"] == 16 and a["blocks"] == 12345 for a in ranks)
+
+
+def test_bench_torchrun_world1_runs_collectives():
+    """Under torchrun at WORLD_SIZE=1 the timed region still runs the barrier and the max-reduce (the
+    code path of the N-GPU run); here with the CPU stand-in over gloo."""
+    import json
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
+           "127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+           "--dry-run-cpu"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=dict(os.environ))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][0]
+    assert line["n_gpus"] == 1 and len(line["rank_args"]) == 1
+
+
 def test_bench_rejects_world_mismatch():
     import subprocess
 

@@ -76,7 +76,7 @@ def test_normal_build_has_no_debug_checks(lib):
 def test_debug_build_exports_its_counters():
     dbg = os.path.join(ROOT, "paritypartyfs_amd", "_lib", "alt", "libppfs_ecc_debug.so")
     if not os.path.exists(dbg):
-        pytest.skip("no PPFS_ECC_DEBUG build (tools/build_alt.sh debug -DPPFS_ECC_DEBUG=1)")
+        pytest.skip("no PPFS_ECC_DEBUG build (tools/build_alt.sh --product debug -DPPFS_ECC_DEBUG=1)")
     out = subprocess.run(["nm", "-D", "--defined-only", dbg], capture_output=True, text=True).stdout
     units = re.findall(r"\bT (ppfs_dbg_faults_\w+)$", out, flags=re.M)
     assert len(units) == 11, units  # 7 RS instantiations, generic RS, bit, bit-fast, vote

@@ -1,8 +1,20 @@
 #!/bin/bash
-# Builds an ablation variant of the engine: tools/build_alt.sh <name> '<extra hipcc flags>'
-#   -> paritypartyfs_amd/_lib/alt/libppfs_ecc_<name>.so (load it with PPFS_ECC_LIB=...)
+# Builds a variant of the engine into paritypartyfs_amd/_lib/alt/libppfs_ecc_<name>.so (load it with
+# PPFS_ECC_LIB=...):
+#   tools/build_alt.sh <name> '<extra hipcc flags>'            ablation build: the RS fast path from
+#       tools/ablations/rs_fast_inst_ablate.hip (every PPFS_* switch of rounds 1-2, the headers in
+#       tools/ablations/)
+#   tools/build_alt.sh --product <name> '<extra hipcc flags>'  the shipped dispatch with extra flags
+#       (e.g. the bounds-checked build: --product debug -DPPFS_ECC_DEBUG=1)
 set -e
+INST=../../tools/ablations/rs_fast_inst_ablate.hip
+INC="-I. -I../../tools/ablations"
+if [ "$1" = "--product" ]; then
+    INST=rs_fast_inst.hip
+    INC=""
+    shift
+fi
 N=$1; shift
 cd "$(dirname "$0")/../paritypartyfs_amd/csrc"
-make -j8 OUT=../_lib/alt/libppfs_ecc_$N.so OBJDIR=../_lib/alt/obj_$N EXTRA="$*" >/dev/null
-echo "built _lib/alt/libppfs_ecc_$N.so ($*)"
+make -j8 OUT=../_lib/alt/libppfs_ecc_$N.so OBJDIR=../_lib/alt/obj_$N RS_INST=$INST EXTRA="$INC $*" >/dev/null
+echo "built _lib/alt/libppfs_ecc_$N.so ($INST $*)"

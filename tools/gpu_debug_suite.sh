@@ -3,7 +3,7 @@
 # bounds-checks its global accesses against the extents its launch implies, counts and skips the
 # ones outside; tests/conftest.py fails a test whose kernels counted any), with PPFS_ECC_SYNC_CHECK=1
 # (every device entry point synchronizes and reports its own asynchronous errors).
-# Build first: tools/build_alt.sh debug -DPPFS_ECC_DEBUG=1
+# Build first: tools/build_alt.sh --product debug -DPPFS_ECC_DEBUG=1
 set -o pipefail
 TAG=${1:-debug}
 mkdir -p gpurun_out
