@@ -33,7 +33,7 @@ extern "C" {
 int ppfs_rs_fast_supported(int n, int t2);
 int ppfs_rs_fast_tables_bytes(int t2);
 hipError_t ppfs_rs_fast_encode(int t2, const uint8_t* d, uint8_t* r, uint64_t nb, const uint8_t* tab, hipStream_t s,
-    uint32_t* ctr);
+    uint32_t* ctr, uint32_t* ctr_clear);
 const char* ppfs_rs_fast_path(int t2);
 hipError_t ppfs_flag_launch(uint32_t* flag, uint32_t v, hipStream_t s);
 hipError_t ppfs_rs_generic_server_launch(int n, int t2, ppfs::SrvBox* box, uint8_t* zc, uint64_t zc_bytes,
@@ -43,7 +43,7 @@ hipError_t ppfs_bit_server_launch(int ecc_type, uint32_t bs, uint32_t ds, uint32
 hipError_t ppfs_rs_server_launch(int t2, ppfs::SrvBox* box, uint8_t* zc, uint64_t zc_bytes, const uint8_t* tab,
     uint32_t gen, uint32_t idle_us, hipStream_t s);
 hipError_t ppfs_rs_fast_decode(int t2, uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, const uint8_t* tab, int wb,
-    hipStream_t s, uint32_t* ctr);
+    hipStream_t s, uint32_t* ctr, uint32_t* ctr_clear);
 hipError_t ppfs_rs_generic_encode(const uint8_t* d, uint8_t* r, uint64_t nb, int n, int t2, const uint8_t* tab,
     hipStream_t s);
 hipError_t ppfs_rs_generic_decode(uint8_t* r, uint8_t* d, uint8_t* st, uint8_t* spill, uint64_t nb, int n, int t2,
@@ -422,7 +422,7 @@ std::vector<uint8_t> build_crc_tables(uint64_t P, int n, uint32_t ds)
 // T[i][v] = (v << 4i) * C mod P for a constant C = x^e mod P.  Maps: x^0, x^32, x^64, x^96 (piece
 // dwords), x^8192 (one lane's pieces, 1 KiB apart), x^(128 2^j) j < 6 (lane tree), then the final
 // factor placing the zero-padded 16-byte grid: encode x^(8 (ds + m - 1024 (NP + 1)) + n - 1) for
-// each payload misalignment m < 16, check x^(8 (ds - bs) + n - 1).
+// each payload misalignment m < 16, check x^(8 (ds - bs) + n - 1); then x^4096.
 std::vector<uint8_t> build_crc_fast_tables(uint64_t P, int n, uint32_t ds, uint32_t bs)
 {
     CrcHost c { P, n, n == 64 ? ~0ull : ((1ull << n) - 1) };
@@ -433,6 +433,7 @@ std::vector<uint8_t> build_crc_fast_tables(uint64_t P, int n, uint32_t ds, uint3
     for (long m = 0; m < 16; ++m)
         ex.push_back(8L * ((long)ds + m - 1024L * (NP + 1)) + n - 1);
     ex.push_back(8L * ((long)ds - (long)bs) + n - 1);
+    ex.push_back(4096); // the 2-blocks-per-wave encode's Horner step (bit_fast.hip CF_K2)
     std::vector<uint8_t> out((size_t)ppfs_crc_fast_tables_bytes(), 0);
     uint32_t* t = (uint32_t*)out.data();
     for (size_t mi = 0; mi < ex.size(); ++mi) {
@@ -472,13 +473,16 @@ struct ppfs_ecc_ctx {
     const char* kname = "";
     // device tables
     uint8_t* d_tables = nullptr;
-    // ticket counters of the dynamic-tile t <= 4 encode and decode (rs_wg_tk.hpp): one 2,560-byte
-    // set per stream that runs them through this context, encode half then decode half (launches on
-    // one stream are ordered and a kernel leaves its half at zero; no two streams share a set);
-    // further streams use the static walk
+    // ticket counters of the dynamic-tile t <= 4 encode and decode (rs_wg_tk.hpp): per stream that
+    // runs them through this context a slot of two 2,560-byte sets (launch parity), each an encode
+    // half then a decode half.  A launch counts on one set and zeroes the other, which the previous
+    // launch of the same kind on the stream used (launches on one stream are ordered; no two streams
+    // share a slot); tk_par = the set the next launch of each kind uses.  Further streams use the
+    // static walk.
     static constexpr int kTkSlots = 16, kTkSetWords = 640; // encode 320 words, decode 320
     uint32_t* d_ctr = nullptr;
     hipStream_t tk_stream[kTkSlots] = {};
+    uint8_t tk_par[kTkSlots][2] = {};
     int tk_n = 0;
     // scratch for write_device status when the caller passes none
     uint8_t* d_scratch = nullptr;
@@ -535,22 +539,39 @@ bool capturing(hipStream_t s)
 // other (two kernels on one set would skip or repeat tiles).  The 17th distinct stream of a
 // context also falls back (slots are not recycled: a slot's stream may still be running a kernel
 // on it); ppfs_ecc_stream_kernel_name reports which path a stream gets.
-uint32_t* ctr_for(ppfs_ecc_ctx* c, hipStream_t s)
+struct TkSets {
+    uint32_t* mine = nullptr;  // the set this launch counts on
+    uint32_t* clear = nullptr; // the set it zeroes (the previous launch's)
+    int slot = -1, op = 0;
+};
+TkSets ctr_for(ppfs_ecc_ctx* c, hipStream_t s, int op /* 0 encode, 1 decode */)
 {
+    TkSets t;
     if (!c->d_ctr || capturing(s))
-        return nullptr;
-    for (int i = 0; i < c->tk_n; ++i)
-        if (c->tk_stream[i] == s)
-            return c->d_ctr + (size_t)i * ppfs_ecc_ctx::kTkSetWords;
-    if (c->tk_n == ppfs_ecc_ctx::kTkSlots)
-        return nullptr;
-    c->tk_stream[c->tk_n] = s;
-    return c->d_ctr + (size_t)(c->tk_n++) * ppfs_ecc_ctx::kTkSetWords;
+        return t;
+    int i = 0;
+    while (i < c->tk_n && c->tk_stream[i] != s)
+        ++i;
+    if (i == c->tk_n) {
+        if (c->tk_n == ppfs_ecc_ctx::kTkSlots)
+            return t;
+        c->tk_stream[c->tk_n++] = s;
+    }
+    const int par = c->tk_par[i][op];
+    uint32_t* base = c->d_ctr + (size_t)i * 2 * ppfs_ecc_ctx::kTkSetWords + (size_t)op * (ppfs_ecc_ctx::kTkSetWords / 2);
+    t.mine = base + (size_t)par * ppfs_ecc_ctx::kTkSetWords;
+    t.clear = base + (size_t)(par ^ 1) * ppfs_ecc_ctx::kTkSetWords;
+    t.slot = i;
+    t.op = op;
+    return t;
 }
-// a set's second half counts the decode's tiles (rs_wg_decode_tk_kernel)
-uint32_t* dec_ctr(uint32_t* set)
+// after a launch with sets t went into the stream: the next launch of its kind uses the other set
+// (a launch that failed to enqueue zeroed nothing and counted on nothing: the parity stays)
+hipError_t tk_commit(ppfs_ecc_ctx* c, const TkSets& t, hipError_t e)
 {
-    return set ? set + ppfs_ecc_ctx::kTkSetWords / 2 : nullptr;
+    if (e == hipSuccess && t.slot >= 0)
+        c->tk_par[t.slot][t.op] ^= 1;
+    return e;
 }
 
 // After a device entry point queued work on caller stream s: (re-)record s's completion event.
@@ -688,7 +709,7 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
         return fail(PPFS_ECC_EHIP, "hipSetDevice", e);
     }
     if (c->rs_fast && c->rs_t2 <= 8) {
-        const size_t cb = sizeof(uint32_t) * ppfs_ecc_ctx::kTkSlots * ppfs_ecc_ctx::kTkSetWords;
+        const size_t cb = sizeof(uint32_t) * ppfs_ecc_ctx::kTkSlots * 2 * ppfs_ecc_ctx::kTkSetWords;
         e = hipMalloc(&c->d_ctr, cb);
         if (e == hipSuccess)
             e = hipMemset(c->d_ctr, 0, cb);
@@ -876,8 +897,12 @@ static int ppfs_ecc_encode_device_impl(ppfs_ecc_ctx* c, const uint8_t* d_data, u
     case PPFS_ECC_NONE:
         return check_hip(dma_async(d_raw, d_data, nblocks * c->raw, hipMemcpyDeviceToDevice, s), "copy");
     case PPFS_ECC_REED_SOLOMON:
-        if (c->rs_fast && aligned16(d_data) && aligned16(d_raw))
-            return check_hip(ppfs_rs_fast_encode(c->rs_t2, d_data, d_raw, nblocks, c->d_tables, s, ctr_for(c, s)), "rs encode");
+        if (c->rs_fast && aligned16(d_data) && aligned16(d_raw)) {
+            const TkSets t = ctr_for(c, s, 0);
+            return check_hip(
+                tk_commit(c, t, ppfs_rs_fast_encode(c->rs_t2, d_data, d_raw, nblocks, c->d_tables, s, t.mine, t.clear)),
+                "rs encode");
+        }
         if (c->rs_fast) {
             // fast tables but unaligned pointers: the generic kernel needs gf block + generator
             return fail(PPFS_ECC_EINVAL, "rs encode: device pointers must be 16-byte aligned");
@@ -926,9 +951,10 @@ static int ppfs_ecc_decode_device_impl(ppfs_ecc_ctx* c, uint8_t* d_raw, uint8_t*
                 if (r)
                     return r;
             }
-            return check_hip(
-                ppfs_rs_fast_decode(c->rs_t2, d_raw, d_data, d_status, nblocks, c->d_tables, write_back, s,
-                    dec_ctr(ctr_for(c, s))),
+            const TkSets t = ctr_for(c, s, 1);
+            return check_hip(tk_commit(c, t,
+                                 ppfs_rs_fast_decode(c->rs_t2, d_raw, d_data, d_status, nblocks, c->d_tables, write_back, s,
+                                     t.mine, t.clear)),
                 "rs decode");
         }
         return check_hip(ppfs_rs_generic_decode(d_raw, d_data, d_status, d_spill, nblocks, c->rs_n, c->rs_t2,

@@ -72,13 +72,15 @@ static uint32_t rs_grid(uint64_t nb)
 }
 #endif
 
+// ctr / ctr_clear: the stream's ticket-counter set for this launch and the one to zero (the previous
+// launch's; api.cpp ctr_for alternates them), or null: the static walk
 extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d, uint8_t* r, uint64_t nb,
-    const uint8_t* tab, hipStream_t s, [[maybe_unused]] uint32_t* ctr)
+    const uint8_t* tab, hipStream_t s, [[maybe_unused]] uint32_t* ctr, [[maybe_unused]] uint32_t* ctr_clear)
 {
 #if PPFS_T2 <= 8
-    if (ctr)
+    if (ctr && ctr_clear)
         hipLaunchKernelGGL((wg::rs_wg_encode_tk_kernel<PPFS_T2, ENC_WPC, 1>), dim3(rs_tile_grid(nb, ENC_WPC)), dim3(256), 0, s,
-            d, r, nb, tab, ctr);
+            d, r, nb, tab, ctr, ctr_clear);
     else
         hipLaunchKernelGGL((wg::rs_wg_encode_kernel<PPFS_T2, ENC_NBUF, ENC_WPC_STATIC, 3, 1, false>), dim3(rs_tile_grid(nb, ENC_WPC_STATIC)),
             dim3(256), 0, s, d, r, nb, tab);
@@ -109,12 +111,12 @@ extern "C" const char* PPFS_CAT(ppfs_rs_fast_path_t, PPFS_T2)()
 }
 
 extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb,
-    const uint8_t* tab, int wb, hipStream_t s, [[maybe_unused]] uint32_t* ctr)
+    const uint8_t* tab, int wb, hipStream_t s, [[maybe_unused]] uint32_t* ctr, [[maybe_unused]] uint32_t* ctr_clear)
 {
 #if PPFS_T2 <= 8
-    if (ctr)
+    if (ctr && ctr_clear)
         hipLaunchKernelGGL((wg::rs_wg_decode_tk_kernel<PPFS_T2, DEC_WPC, 1>), dim3(rs_tile_grid(nb, DEC_WPC)), dim3(256), 0, s,
-            r, d, st, nb, tab, wb, ctr);
+            r, d, st, nb, tab, wb, ctr, ctr_clear);
     else
         hipLaunchKernelGGL((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC, 7, 1>), dim3(rs_tile_grid(nb, DEC_WPC)),
             dim3(256), 0, s, r, d, st, nb, tab, wb);

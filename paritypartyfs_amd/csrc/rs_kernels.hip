@@ -241,9 +241,9 @@ using namespace ppfs;
 
 #define X(T)                                                                                                           \
     extern "C" hipError_t ppfs_rs_fast_encode_t##T(const uint8_t*, uint8_t*, uint64_t, const uint8_t*, hipStream_t,   \
-        uint32_t*);                                                                                                    \
+        uint32_t*, uint32_t*);                                                                                         \
     extern "C" hipError_t ppfs_rs_fast_decode_t##T(uint8_t*, uint8_t*, uint8_t*, uint64_t, const uint8_t*, int,       \
-        hipStream_t, uint32_t*);
+        hipStream_t, uint32_t*, uint32_t*);
 PPFS_RS_CASES(X)
 #undef X
 
@@ -271,12 +271,12 @@ extern "C" int ppfs_rs_fast_tables_bytes(int t2)
 }
 
 extern "C" hipError_t ppfs_rs_fast_encode(int t2, const uint8_t* d, uint8_t* r, uint64_t nb, const uint8_t* tab,
-    hipStream_t s, uint32_t* ctr)
+    hipStream_t s, uint32_t* ctr, uint32_t* ctr_clear)
 {
     switch (t2) {
 #define X(T)                                                                                                           \
     case T:                                                                                                            \
-        return ppfs_rs_fast_encode_t##T(d, r, nb, tab, s, ctr);
+        return ppfs_rs_fast_encode_t##T(d, r, nb, tab, s, ctr, ctr_clear);
         PPFS_RS_CASES(X)
 #undef X
     default:
@@ -302,12 +302,12 @@ extern "C" const char* ppfs_rs_fast_path(int t2)
 }
 
 extern "C" hipError_t ppfs_rs_fast_decode(int t2, uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb,
-    const uint8_t* tab, int wb, hipStream_t s, uint32_t* ctr)
+    const uint8_t* tab, int wb, hipStream_t s, uint32_t* ctr, uint32_t* ctr_clear)
 {
     switch (t2) {
 #define X(T)                                                                                                           \
     case T:                                                                                                            \
-        return ppfs_rs_fast_decode_t##T(r, d, st, nb, tab, wb, s, ctr);
+        return ppfs_rs_fast_decode_t##T(r, d, st, nb, tab, wb, s, ctr, ctr_clear);
         PPFS_RS_CASES(X)
 #undef X
     default:

@@ -388,11 +388,50 @@ __device__ __forceinline__ void stage_bytes(uint8_t* dst, const uint8_t* __restr
         dst[i] = src[i];
 }
 
+#ifndef PPFS_WB_SECTOR
+#define PPFS_WB_SECTOR 1
+#endif
+// Write-back of whole 32-byte sectors (full tiles of a 32-byte aligned codeword buffer): the tile
+// (64 x 255 = 510 x 32 bytes) is sector-aligned, so the sector around a corrected byte lies in the
+// LDS image, which after the corrections holds exactly the bytes the write-back leaves in HBM (the
+// corrected ones, and unchanged ones that equal HBM's).  A full-sector store replaces the 1-byte
+// partial write, which the memory side has to merge into its sector.  Lanes whose
+// fixes share a sector store the same 32 bytes.  sect_off = the tile's first byte in raw_g.
+struct SectorWb {
+    uint32_t s0 = ~0u, s1 = ~0u, s2 = ~0u, s3 = ~0u; // sectors (byte offset in the tile) to store
+    __device__ void add(uint32_t off)
+    {
+        const uint32_t so = off & ~31u;
+        if (so != s0) {
+            s3 = s2;
+            s2 = s1;
+            s1 = s0;
+            s0 = so;
+        }
+    }
+    // after every lane's fixes are in LDS (tile image at LDS byte `img`)
+    __device__ void store(const uint8_t* lds, uint32_t img, uint8_t* __restrict__ tile_g) const
+    {
+        const uint32_t v[4] = { s0, s1, s2, s3 };
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (v[i] == ~0u)
+                continue;
+            const uint4 a = *(const uint4*)(lds + img + v[i]), b = *(const uint4*)(lds + img + v[i] + 16u);
+            *(uint4*)(tile_g + v[i]) = a;
+            *(uint4*)(tile_g + v[i] + 16u) = b;
+        }
+    }
+};
+
 // Decode phase 2 (wave 0, lane = block): the reference correction for blocks with r' != 0.
-// fix(pos, e) patches codeword byte pos of the lane's row (LDS) and, with write-back, in HBM.
+// fix(pos, e) patches codeword byte pos of the lane's row (LDS) and, with write-back, in HBM: the
+// byte itself, or (sect != null, full tiles) the 32-byte sector around it once every lane's fixes
+// are in the LDS image (SectorWb).
 template <int T2>
 __device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, uint32_t par, uint32_t r, bool valid,
-    uint8_t* __restrict__ raw_g, uint64_t blk, bool wb, [[maybe_unused]] uint64_t raw_bytes)
+    uint8_t* __restrict__ raw_g, uint64_t blk, bool wb, [[maybe_unused]] uint64_t raw_bytes,
+    uint8_t* __restrict__ sect_tile = nullptr)
 {
     using L = RsWgLayout<T2>;
     const uint64_t rem = *(const uint64_t*)(lds + par + 8u * r);
@@ -422,12 +461,16 @@ __device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, ui
                 S[i] = (s[i >> 2] >> (8 * (i & 3))) & 0xFFu;
             geo = rs_geometric<T2>(S, gf, gpos, ge);
         }
+        SectorWb sw;
+        const bool sect = wb && sect_tile != nullptr;
         auto fix = [&](uint32_t pos, uint32_t e) {
             if (e == 0)
                 return;
             const uint8_t fixed = (uint8_t)(lds[row + pos] ^ e);
             lds[row + pos] = fixed;
-            if (wb && PPFS_DBG_OK(raw_g + blk * 255u + pos, 1, raw_g, raw_bytes))
+            if (sect)
+                sw.add(255u * r + pos);
+            else if (wb && PPFS_DBG_OK(raw_g + blk * 255u + pos, 1, raw_g, raw_bytes))
                 wb_byte(raw_g + blk * 255u + pos, fixed);
         };
         if (__builtin_amdgcn_ballot_w64(err && !geo)) {
@@ -439,6 +482,11 @@ __device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, ui
             }
         } else if (err && geo) {
             fix(gpos, ge);
+        }
+        if (sect) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // every lane's fixes in the image (one wave)
+            if (PPFS_DBG_OK(sect_tile, (uint64_t)TB * 255u, raw_g, raw_bytes))
+                sw.store(lds, buf + PAD, sect_tile);
         }
     }
     return err ? 1u : 0u;

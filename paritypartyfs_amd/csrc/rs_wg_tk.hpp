@@ -1,28 +1,32 @@
 #pragma once
 // rs_wg_tk.hpp -- the t <= 4 RS encode (rs_wg.hpp's ring of 3 LDS tile buffers, 2 workgroups per
-// CU) with its tiles handed out dynamically: per-XCD ticket counters keep the tiles in flight one
-// window of HBM and let fast workgroups take more tiles (the persistent static walk's copy skeleton
-// measured 96 vs 91.6 us against dynamic tiles).  The counters live in a per-context
-// buffer, one set per stream that runs them through the context (api.cpp ctr_for): launches on one
-// stream are ordered, and the kernel's last workgroup zeroes its set for the next one.
+// CU) and decode (double buffer, 3 per CU) with their tiles handed out dynamically: per-XCD ticket
+// counters keep the tiles in flight one window of HBM and let fast workgroups take more tiles (the
+// persistent static walk's copy skeleton measured 96 vs 91.6 us against dynamic tiles, DESIGN.md
+// 4.1).  The counters live in a per-context buffer, one pair of sets per stream that runs them
+// through the context (api.cpp ctr_for): launches on one stream are ordered.
+//
+// Launch bookkeeping without a tail (round 3): a launch counts on set `ctr` and zeroes `ctr_clear`,
+// the set the previous launch of the same kind on the stream counted on (complete: same stream);
+// the host alternates the two.  So no workgroup has to find out that it is the last one to reset
+// the counters after the grid's final tiles (one more atomic round trip at the end of every launch).
+//
+// Startup (round 3): a workgroup's first two tiles are static (its rank among the workgroups of its
+// XCD, and that plus their number), so the DMA waves issue them first thing, before any table byte
+// or ticket arrives; wave 0 brings the tables into LDS by LDS-DMA meanwhile and takes the first
+// dynamic ticket.  Tickets continue after the 2 G_x static tiles of the XCD.
 #include "rs_wg.hpp"
 
 namespace ppfs {
 namespace wg {
 
-// ------------------------------------------------------------------------------------
-// Dynamic tiles with the ticket in a worker wave: the 4-wave ring encode of rs_wg_encode_kernel
-// (NBUF = 3) with its tile sequence from per-XCD ticket counters, as in the ablation
-// rs_wg_encode_dyn_kernel (rs_wg_ablate.hpp) but without its fifth wave.  Waves 1-3 issue all of a tile's LDS-DMA
-// (at most 6 instructions each: for 2t <= 8 wave 1 issues 6 and waves 2-3 issue 5, which the
-// loop's wait counts tolerate, vm_wait_newer rounding down to a multiple of 4) and wave 0 none, so wave 0's vector-memory queue holds only its stores
-// and the ticket atomics: the compiler's wait for a returned ticket (issued at the top of
-// iteration j, published in LDS at its end) never waits for a tile DMA.  Ticket j is the tile of
-// iteration j + 3 (read at the top of iteration j + 1 for the DMA two tiles ahead); the prologue
-// takes three.  The last workgroup resets the counters for the next launch on the stream.  The
-// loop's ticket is an atomicInc (uinc_wrap), which the compiler's atomic optimizer leaves alone: an
-// optimised atomicAdd would be combined across lanes and waited for at once.
-// ------------------------------------------------------------------------------------
+// DMA instructions one wave of waves 1-3 issues for an NPIECE-piece tile (pieces p = w + 192 k,
+// w = tid - 64): the last, partial round only in the waves whose first lane has a piece
+template <int NPIECE> constexpr uint32_t dma_count(uint32_t wave)
+{
+    return (uint32_t)(NPIECE / 192) + ((NPIECE % 192) > (int)(64u * (wave - 1u)) ? 1u : 0u);
+}
+
 template <int NPIECE>
 __device__ __forceinline__ void dma_tile192(uint8_t* dst, const uint8_t* __restrict__ src, uint32_t tid,
     [[maybe_unused]] const uint8_t* gbase, [[maybe_unused]] uint64_t extent)
@@ -30,17 +34,96 @@ __device__ __forceinline__ void dma_tile192(uint8_t* dst, const uint8_t* __restr
     constexpr int KI = (NPIECE + 191) / 192;
     const uint32_t w = tid - 64u; // waves 1-3
     const uint32_t lbase = __builtin_amdgcn_readfirstlane(lds_addr(dst) + (w & ~63u) * 16u);
+    // the last round is issued only by the waves that have pieces in it (wave-uniform branch), so
+    // every wave's instruction count is exactly dma_count<NPIECE>(wave)
+    const bool last_round = __builtin_amdgcn_readfirstlane(w & ~63u) < (uint32_t)(NPIECE - 192 * (KI - 1));
 #pragma unroll
     for (int k = 0; k < KI; ++k) {
         const uint32_t p = w + 192u * (uint32_t)k;
-        if (((k + 1) * 192 <= NPIECE || p < (uint32_t)NPIECE) && PPFS_DBG_OK(src + (size_t)p * 16, 16, gbase, extent))
-            dma16(src + (size_t)p * 16, __builtin_amdgcn_readfirstlane(lbase + 3072u * (uint32_t)k));
+        if ((k + 1) * 192 <= NPIECE) {
+            if (PPFS_DBG_OK(src + (size_t)p * 16, 16, gbase, extent))
+                dma16(src + (size_t)p * 16, __builtin_amdgcn_readfirstlane(lbase + 3072u * (uint32_t)k));
+        } else if (last_round) {
+            if (p < (uint32_t)NPIECE && PPFS_DBG_OK(src + (size_t)p * 16, 16, gbase, extent))
+                dma16(src + (size_t)p * 16, __builtin_amdgcn_readfirstlane(lbase + 3072u * (uint32_t)k));
+        }
     }
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 15] (exact: the counts below are known per wave)
+__device__ __forceinline__ void vm_wait_exact(uint32_t n)
+{
+    switch (__builtin_amdgcn_readfirstlane(n)) {
+#define PPFS_VMW(N)                                                                                                    \
+    case N:                                                                                                            \
+        asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory");                                                          \
+        break;
+        PPFS_VMW(1) PPFS_VMW(2) PPFS_VMW(3) PPFS_VMW(4) PPFS_VMW(5) PPFS_VMW(6) PPFS_VMW(7) PPFS_VMW(8)
+        PPFS_VMW(9) PPFS_VMW(10) PPFS_VMW(11) PPFS_VMW(12) PPFS_VMW(13) PPFS_VMW(14) PPFS_VMW(15)
+#undef PPFS_VMW
+    default:
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        break;
+    }
+}
+
+// Wave 0 (64 lanes) copies the first BYTES of the table blob into LDS at 0 by LDS-DMA: no register
+// round trip, and its loads never share a queue with the DMA waves' tiles.  Caller: vmcnt(0).
+template <int BYTES>
+__device__ __forceinline__ void dma_tables_w0(uint8_t* lds, const uint8_t* __restrict__ tables, uint32_t lane)
+{
+    static_assert(BYTES % 16 == 0, "16-byte pieces");
+    constexpr int NP = BYTES / 16, KI = (NP + 63) / 64;
+    const uint32_t lbase = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+        const uint32_t p = lane + 64u * (uint32_t)k;
+        if ((k + 1) * 64 <= NP || p < (uint32_t)NP)
+            dma16(tables + 16u * p, lbase + 1024u * (uint32_t)k);
+    }
+}
+
+// XCD-local tile numbering: workgroup b sits on counter xc = b % nx with rank b / nx among the gx
+// workgroups of that counter; local ticket j is tile j * nx + xc
+struct TkGeom {
+    uint32_t nx, xc, gx, rank;
+};
+__device__ __forceinline__ TkGeom tk_geom()
+{
+    TkGeom g;
+    g.nx = gridDim.x < 8u ? gridDim.x : 8u;
+    g.xc = blockIdx.x % g.nx;
+    g.gx = (gridDim.x - g.xc + g.nx - 1u) / g.nx;
+    g.rank = blockIdx.x / g.nx;
+    return g;
+}
+
+#ifndef PPFS_TK_MAPC
+#define PPFS_TK_MAPC 0 // ablation: 1 = each XCD's counter walks a contiguous range of tiles
+#endif
+// the tile of local ticket j on this XCD: interleaved (j nx + xc) or, with PPFS_TK_MAPC, the XCD's
+// contiguous range of per = nfull / nx + 1 tiles (tiles past nfull -> nfull + 1: none)
+__device__ __forceinline__ uint64_t tk_tile(uint64_t j, const TkGeom& g, uint64_t nfull)
+{
+    if constexpr (PPFS_TK_MAPC) {
+        const uint64_t per = nfull / g.nx + 1u, t = (uint64_t)g.xc * per + j;
+        return (j < per && t <= nfull) ? t : nfull + 1u;
+    } else {
+        return j * g.nx + g.xc;
+    }
+}
+
+// block 0, one lane: zero the counter set the previous launch on this stream used
+__device__ __forceinline__ void tk_clear(uint32_t* __restrict__ ctr_clear, uint32_t nx)
+{
+    for (uint32_t x = 0; x < nx; ++x)
+        __hip_atomic_store(ctr_clear + 32u * x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int T2, int WPC = 2, int NTST = 1>
 __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t* __restrict__ data,
-    uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables, uint32_t* __restrict__ ctr)
+    uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables, uint32_t* __restrict__ ctr,
+    uint32_t* __restrict__ ctr_clear)
 {
     constexpr int NBUF = 3;
     using L = RsWgLayout<T2>;
@@ -51,29 +134,19 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
     constexpr int K = L::K;
     constexpr int IN_PIECES = TB * K / 16;
     constexpr int OUT_PIECES = TB * 255 / 16;
-    constexpr uint32_t KD = (IN_PIECES + 191) / 192; // DMA instructions per tile of a DMA wave
-    constexpr uint32_t OFF_TK = D::BYTES;              // 4 ticket slots: slot i & 3 = tile of iteration i
+    constexpr uint32_t OFF_TK = D::BYTES; // 4 ticket slots: slot i & 3 = tile of iteration i
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_ALLOC];
     uint32_t* const s_tk = (uint32_t*)(lds + OFF_TK);
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
     const bool dmaw = wave != 0, tk_lane = wave == 0 && lane == 0;
+    const uint32_t kd = dmaw ? dma_count<IN_PIECES>(wave) : 0u; // this wave's DMA instructions per tile
     const uint32_t row = lane_row(lane);
     const uint64_t nfull = nblocks / TB, ntiles = (nblocks + TB - 1) / TB;
-    const uint32_t nx = gridDim.x < 8u ? gridDim.x : 8u, xc = blockIdx.x % nx;
-    uint32_t* const my_ctr = ctr + 32u * xc; // 128-byte lines
-    for (uint32_t p = tid; p < (uint32_t)D::TBL / 16; p += NTHR)
-        *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
-    if (tid < 128)
-        *(uint64_t*)(lds + D::OFF_PAR + 8 * tid) = 0;
-    if (tk_lane) {
-        const uint32_t base = atomicAdd(my_ctr, 3u);
-#pragma unroll
-        for (uint32_t j = 0; j < 3; ++j)
-            s_tk[j] = (base + j) * nx + xc;
-    }
-    __syncthreads();
-    uint64_t q0 = __builtin_amdgcn_readfirstlane(s_tk[0]), q1 = __builtin_amdgcn_readfirstlane(s_tk[1]);
-    uint32_t cur = 0, pc = 0, hist = 0, iter = 0;
+    const TkGeom g = tk_geom();
+    uint32_t* const my_ctr = ctr + 32u * g.xc; // 128-byte lines
+    // the first two tiles are static: local tickets rank and rank + gx
+    uint64_t q0 = tk_tile(g.rank, g, nfull), q1 = tk_tile(g.rank + g.gx, g, nfull);
+    uint32_t hist = 0;
     if (dmaw) {
         if (q0 < nfull)
             dma_tile192<IN_PIECES>(lds + D::OFF_BUF + PAD, data + q0 * (TB * K), tid, data, nblocks * K);
@@ -81,10 +154,27 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
         if (go)
             dma_tile192<IN_PIECES>(lds + D::OFF_BUF + BUF + PAD, data + q1 * (TB * K), tid, data, nblocks * K);
         hist = go ? 1u : 0u;
-        vm_wait_newer(KD * hist); // tile q0 landed, q1 may fly
+    } else {
+        dma_tables_w0<D::TBL>(lds, tables, lane);
+        *(uint64_t*)(lds + D::OFF_PAR + 8u * lane) = 0; // both parity slot sets (2 x 64 x 8 B)
+        *(uint64_t*)(lds + D::OFF_PAR + 512u + 8u * lane) = 0;
+        if (tk_lane) {
+            if (blockIdx.x == 0)
+                tk_clear(ctr_clear, g.nx);
+            const uint32_t t2 = atomicInc(my_ctr, 0xFFFFFFFFu) + 2u * g.gx; // the tile of iteration 2
+            s_tk[2] = (uint32_t)tk_tile(t2, g, nfull);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // tables landed, ticket returned
     }
+    if (dmaw)
+        vm_wait_exact(kd * hist); // tile q0 landed, q1 may fly
+    barrier_lds();
+    uint32_t cur = 0, pc = 0, iter = 0;
     while (q0 < nfull) {
-        barrier_lds(); // A: tile q0 in LDS, the last emission reads done, the next ticket published
+        // A: tile q0 in LDS, the last emission reads done, the next ticket published (the first
+        // pass: tables, parity slots and the iteration-2 ticket in place)
+        if (iter)
+            barrier_lds();
         const uint64_t ahead = __builtin_amdgcn_readfirstlane(s_tk[(iter + 2u) & 3u]);
         // no initial value: writing the register outside wave 0's branch would make every wave wait
         // for the previous ticket (the compiler tracks its pending write per register)
@@ -111,13 +201,13 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
         }
         ++iter;
         if (dmaw) {
-            // the next tile's DMA (issued an iteration ago) landed; the stores since, and this
-            // iteration's DMA, may fly
+            // the next tile's DMA (issued an iteration ago, or in the prologue) landed; newer: the
+            // last two iterations' stores and this iteration's DMA
             const uint32_t st = 4u * (iter < 2u ? iter : 2u);
-            vm_wait_newer(st + KD * (hist & 1u));
+            vm_wait_exact(st + kd * (hist & 1u));
         }
         if (tk_lane)
-            s_tk[(iter + 2u) & 3u] = tk * nx + xc; // the tile of (iteration iter - 1) + 3
+            s_tk[(iter + 2u) & 3u] = (uint32_t)tk_tile(tk + 2u * g.gx, g, nfull); // the tile of (iteration iter - 1) + 3
         cur = ring_add(cur, 1, NBUF);
         pc ^= 1u;
         q0 = q1;
@@ -146,27 +236,19 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
                 st_bytes(dst + 16u * p, v, nout - 16u * p);
         }
     }
-    if (tk_lane) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this workgroup's last ticket has returned
-        if (atomicAdd(ctr + 32u * 8u, 1u) == gridDim.x - 1) { // every workgroup has taken its last ticket
-            for (uint32_t x = 0; x < nx; ++x)
-                __hip_atomic_store(ctr + 32u * x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(ctr + 32u * 8u, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
 // ------------------------------------------------------------------------------------
 // The t <= 4 decode (rs_wg_decode_kernel, double-buffered, 3 workgroups per CU) on the same
-// ticket scheme: waves 1-3 issue the DMA, wave 0 (the corrector) takes the tickets.  With two
-// buffers ticket j is the tile of iteration j + 2 (read at the top of iteration j + 1 for the DMA
-// one tile ahead); the prologue takes two.  Counter set: the second half of the stream's set
-// (api.cpp ctr_for), so an encode and a decode on one stream never share counters.
+// ticket scheme: waves 1-3 issue the DMA, wave 0 (the corrector) brings the tables and takes the
+// tickets.  With two buffers the first tile is static and ticket j is the tile of iteration j + 1
+// (taken at the top of iteration j - 1, read at the top of iteration j for the DMA one tile ahead).
+// Counter sets: the decode halves of the stream's pair (api.cpp ctr_for).
 // ------------------------------------------------------------------------------------
 template <int T2, int WPC = 3, int NTST = 1>
 __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
     uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables, int write_back,
-    uint32_t* __restrict__ ctr)
+    uint32_t* __restrict__ ctr, uint32_t* __restrict__ ctr_clear)
 {
     constexpr int NBUF = 2;
     using L = RsWgLayout<T2>;
@@ -183,28 +265,31 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
     const bool dmaw = wave != 0, tk_lane = wave == 0 && lane == 0;
     const uint32_t row = lane_row(lane);
     const bool wb = write_back != 0, want = data != nullptr;
+    // full tiles of a 32-byte aligned image write back whole sectors (rs_wg.hpp SectorWb)
+    const bool sect = PPFS_WB_SECTOR && wb && ((uintptr_t)raw & 31u) == 0;
     const uint64_t nfull = nblocks / TB, ntiles = (nblocks + TB - 1) / TB;
-    const uint32_t nx = gridDim.x < 8u ? gridDim.x : 8u, xc = blockIdx.x % nx;
-    uint32_t* const my_ctr = ctr + 32u * xc;
-    for (uint32_t p = tid; p < (uint32_t)D::TBL / 16; p += NTHR)
-        *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
-    if (tid < 128)
-        *(uint64_t*)(lds + D::OFF_PAR + 8 * tid) = 0;
-    if (tk_lane) {
-        const uint32_t base = atomicAdd(my_ctr, 2u);
-        s_tk[0] = base * nx + xc;
-        s_tk[1] = (base + 1u) * nx + xc;
-    }
-    __syncthreads();
-    uint64_t q0 = __builtin_amdgcn_readfirstlane(s_tk[0]);
-    uint32_t cur = 0, pc = 0, iter = 0;
+    const TkGeom g = tk_geom();
+    uint32_t* const my_ctr = ctr + 32u * g.xc;
+    uint64_t q0 = tk_tile(g.rank, g, nfull); // static first tile
     if (dmaw) {
         if (q0 < nfull)
             dma_tile192<IN_PIECES>(lds + D::OFF_BUF + PAD, raw + q0 * (TB * 255), tid, raw, nblocks * 255u);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        dma_tables_w0<D::TBL>(lds, tables, lane);
+        *(uint64_t*)(lds + D::OFF_PAR + 8u * lane) = 0;
+        *(uint64_t*)(lds + D::OFF_PAR + 512u + 8u * lane) = 0;
+        if (tk_lane) {
+            if (blockIdx.x == 0)
+                tk_clear(ctr_clear, g.nx);
+            s_tk[1] = (uint32_t)tk_tile(atomicInc(my_ctr, 0xFFFFFFFFu) + g.gx, g, nfull); // the tile of iteration 1
+        }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // tile q0 / tables and the ticket landed
+    barrier_lds();
+    uint32_t cur = 0, pc = 0, iter = 0;
     while (q0 < nfull) {
-        barrier_lds(); // A: tile q0 in LDS, the last emission reads done, the next ticket published
+        if (iter)
+            barrier_lds(); // A: tile q0 in LDS, the last emission reads done, the next ticket published
         const uint64_t q1 = __builtin_amdgcn_readfirstlane(s_tk[(iter + 1u) & 3u]);
         uint32_t tk; // no initial value (see the encode)
         if (tk_lane)
@@ -218,7 +303,8 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         phase_remainder<T2, 255>(lds, buf, par, wave, row);
         barrier_lds(); // B: remainders complete
         if (wave == 0) {
-            const uint32_t st = phase_correct<T2>(lds, buf, par, row, true, raw, q0 * TB + row, wb, nblocks * 255u);
+            const uint32_t st = phase_correct<T2>(lds, buf, par, row, true, raw, q0 * TB + row, wb, nblocks * 255u,
+                sect ? raw + q0 * (TB * 255) : nullptr);
             if (status && PPFS_DBG_OK(status + q0 * TB + row, 1, status, nblocks))
                 status[q0 * TB + row] = (uint8_t)st;
         }
@@ -241,7 +327,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         if (tk_lane)
-            s_tk[(iter + 1u) & 3u] = tk * nx + xc; // the tile of (iteration iter - 1) + 2
+            s_tk[(iter + 1u) & 3u] = (uint32_t)tk_tile(tk + g.gx, g, nfull); // the tile of (iteration iter - 1) + 2
         cur ^= 1u;
         pc ^= 1u;
         q0 = q1;
@@ -276,14 +362,6 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
                 else
                     st_bytes(dst + 16u * p, v, nout - 16u * p);
             }
-        }
-    }
-    if (tk_lane) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (atomicAdd(ctr + 32u * 8u, 1u) == gridDim.x - 1) {
-            for (uint32_t x = 0; x < nx; ++x)
-                __hip_atomic_store(ctr + 32u * x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(ctr + 32u * 8u, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }

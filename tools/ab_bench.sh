@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 for r in 1 2; do
 for v in new ${VARIANTS}; do
   if [ $v = new ]; then L=$PWD/paritypartyfs_amd/_lib/libppfs_ecc.so; else L=$PWD/paritypartyfs_amd/_lib/alt/libppfs_ecc_$v.so; fi
-  PPFS_ECC_LIB=$L timeout -k 10 150 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive \
+  PPFS_ECC_LIB=$L timeout -k 10 150 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive --no-configs \
       --standalone-launches 20 --prewarm-s 0.5 "$@" > gpurun_out/${TAG}_${v}_$r.json 2> gpurun_out/${TAG}_${v}_$r.err || { tail -5 gpurun_out/${TAG}_${v}_$r.err; exit 1; }
   python3 - gpurun_out/${TAG}_${v}_$r.json $v $r <<'PY'
 import json, sys

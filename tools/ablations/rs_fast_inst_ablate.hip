@@ -240,7 +240,7 @@ constexpr int SOLO_NW = PPFS_SOLO_NW, SOLO_WPC = PPFS_SOLO_WPC;
 #endif
 
 extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d, uint8_t* r, uint64_t nb,
-    const uint8_t* tab, hipStream_t s, [[maybe_unused]] uint32_t* ctr)
+    const uint8_t* tab, hipStream_t s, [[maybe_unused]] uint32_t* ctr, [[maybe_unused]] uint32_t* ctr_clear)
 {
 #if PPFS_T2 <= 8
 #if PPFS_WG_RP
@@ -262,7 +262,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
 #endif
     if ((PPFS_WG_TK & 1) && ctr && PPFS_ENC_MODE == 3 && !WG_FULL && !PPFS_WG_ENC_IMG && !(PPFS_WG_W1 & 1))
         hipLaunchKernelGGL((wg::rs_wg_encode_tk_kernel<PPFS_T2, 2, PPFS_ENC_NTST>), dim3(rs_tile_grid(nb, 2)), dim3(256), 0, s, d,
-            r, nb, tab, ctr);
+            r, nb, tab, ctr, ctr_clear);
     else if constexpr (PPFS_WG_W1 & 1)
         hipLaunchKernelGGL((w1::rs_w1_encode_kernel<PPFS_T2, PPFS_W1_NW, PPFS_W1_NBUF, PPFS_ENC_MODE, PPFS_ENC_NTST>),
             dim3(rs_tile_grid(nb, 1, w1::TB * PPFS_W1_NW)), dim3(64 * PPFS_W1_NW), 0, s, d, r, nb, tab);
@@ -310,7 +310,7 @@ extern "C" const char* PPFS_CAT(ppfs_rs_fast_path_t, PPFS_T2)()
 }
 
 extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb,
-    const uint8_t* tab, int wb, hipStream_t s, [[maybe_unused]] uint32_t* ctr)
+    const uint8_t* tab, int wb, hipStream_t s, [[maybe_unused]] uint32_t* ctr, [[maybe_unused]] uint32_t* ctr_clear)
 {
 #if PPFS_T2 <= 8
 #if PPFS_WG_RP
@@ -323,7 +323,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
 #else
     if ((PPFS_WG_TK & 2) && ctr && PPFS_DEC_MODE == 7 && !DEC_FULL && DEC_NBUF == 2 && DEC_WPC == 3 && !(PPFS_WG_W1 & 2))
         hipLaunchKernelGGL((wg::rs_wg_decode_tk_kernel<PPFS_T2, 3, PPFS_DEC_NTST>), dim3(rs_tile_grid(nb, 3)), dim3(256), 0, s,
-            r, d, st, nb, tab, wb, ctr);
+            r, d, st, nb, tab, wb, ctr, ctr_clear);
     else if constexpr (PPFS_WG_W1 & 2)
         hipLaunchKernelGGL((w1::rs_w1_decode_kernel<PPFS_T2, PPFS_W1_DEC_NW, PPFS_W1_DEC_NBUF, PPFS_DEC_NTST>),
             dim3(rs_tile_grid(nb, 1, w1::TB * PPFS_W1_DEC_NW)), dim3(64 * PPFS_W1_DEC_NW), 0, s, r, d, st, nb, tab, wb);
