@@ -252,16 +252,24 @@ class HipEvents:
             self.L.hipEventDestroy(e)
 
 
-def timed_steps(step, steps, world, sync, device=None):
+def timed_steps(step, steps, world, sync, device=None, pre=None):
     """Time exactly `steps` calls of step() between barrier + sync on both sides; returns the
     MAX elapsed seconds over ranks (every rank gets the same value).  The barrier and the
-    max-reduce are the only collectives: nothing on the data path."""
+    max-reduce are the only collectives: nothing on the data path.
+
+    pre(): untimed work queued BEFORE the barrier (warm-up steps), so that the GPU is busy while
+    the ranks meet -- an RCCL barrier idles the host for long enough that an idle GPU drops its
+    clocks, and the first timed steps then ran ~15 % slow (r3c: 0.2675 vs 0.2294 ms per step under
+    torchrun at WORLD_SIZE=1 with the barrier on an idle GPU).  The synchronize after the barrier
+    drains pre()'s work; the region starts from a busy, clocked-up GPU."""
     import torch
     import torch.distributed as dist
 
     # under torchrun the collectives run whenever a process group exists, also at WORLD_SIZE=1:
     # `torchrun --nproc-per-node 1 bench.py` then executes exactly the RCCL code of the 8-GPU run
     coll = world > 1 or (dist.is_available() and dist.is_initialized())
+    if pre is not None:
+        pre()
     if coll:
         dist.barrier()
     sync()
@@ -463,15 +471,17 @@ def main(argv=None):
             torch.cuda.synchronize()
 
     rewarm(args.prewarm_s)
-    # The W warmup steps run straight into the timed region: no host-side work between them
-    # other than the synchronize the region starts with (an idle GPU drops its clocks within a
-    # millisecond or two and the next steps run slower while they ramp back: r2c, 0.311 ms per step
-    # after a host-side check vs 0.25 back to back).  The self-check runs after the region.
-    run_steps(args.warmup)
-    elapsed = timed_steps(lambda: run_steps(args.steps), 1, world, torch.cuda.synchronize, red_dev)
+    # The W warmup steps are queued right before the barrier and run straight into the timed
+    # region: nothing but the barrier (while they run) and the synchronize the region starts with
+    # lies between them (an idle GPU drops its clocks within a millisecond or two and the next steps
+    # run slower while they ramp back: r2c, 0.311 ms per step after a host-side check vs 0.25 back
+    # to back).  The self-check runs after the region.
+    elapsed = timed_steps(lambda: run_steps(args.steps), 1, world, torch.cuda.synchronize, red_dev,
+                          pre=lambda: run_steps(args.warmup))
     # the same timed region again, 3 times (reported beside the measurement, never as `value`):
     # shows whether the measured region was representative of back-to-back regions
-    repeats = [timed_steps(lambda: run_steps(args.steps), 1, world, torch.cuda.synchronize, red_dev) / args.steps * 1e3
+    repeats = [timed_steps(lambda: run_steps(args.steps), 1, world, torch.cuda.synchronize, red_dev,
+                           pre=lambda: run_steps(max(2, args.warmup))) / args.steps * 1e3
                for _ in range(3)]
     # device-side self-check of the last timed step: every block corrected, payload restored
     ok = bool(torch.equal(out, data)) and int(status.min()) == 1 and int(status.max()) == 1

@@ -518,9 +518,124 @@ struct ppfs_ecc_ctx {
     hipEvent_t ev[kEvSlots] = {};
     int ev_n = 0;
     bool ev_overflow = false;
+    // the context's own stream for its stream-ordered device allocations (mem_alloc / mem_free)
+    hipStream_t ms = nullptr;
+    size_t pin_bytes = 0; // bytes of each h_pin[] buffer (pin cache key)
 };
 
 namespace {
+// ---------------------------------------------------------------------------------------
+// Memory that never synchronizes the device when it is freed.  hipFree and hipHostFree wait for
+// every stream of the device, so a context destroyed (or resizing its staging) beside another
+// context's resident server, or beside a long kernel of the caller's, waited for them -- 1 to 51 s
+// in r3d's destroy test.  Device buffers come from the stream-ordered pool on the context's own
+// stream (hipFreeAsync after the work that reads them is known complete); page-locked host
+// buffers go back to a process-wide cache (exact size and flags) instead of hipHostFree.
+// ---------------------------------------------------------------------------------------
+#ifdef PPFS_ECC_DEBUG
+// PPFS_ECC_DEBUG: the engine's stream-ordered device allocations, for dma_async's range check
+// (the runtime keeps no address-range record for pool memory)
+std::mutex g_pool_mu;
+std::map<uintptr_t, size_t> g_pool;
+void pool_note(void* p, size_t n)
+{
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (n)
+        g_pool[(uintptr_t)p] = n;
+    else
+        g_pool.erase((uintptr_t)p);
+}
+bool pool_covers(const void* p, size_t n)
+{
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    auto it = g_pool.upper_bound((uintptr_t)p);
+    if (it == g_pool.begin())
+        return false;
+    --it;
+    return (uintptr_t)p >= it->first && (uintptr_t)p + n <= it->first + it->second;
+}
+#else
+inline void pool_note(void*, size_t) {}
+#endif
+// hipMallocAsync on stream s (recorded for the debug build's copy checks)
+hipError_t pool_alloc(void** p, size_t n, hipStream_t s)
+{
+    const hipError_t e = hipMallocAsync(p, n, s);
+    if (e == hipSuccess)
+        pool_note(*p, n);
+    return e;
+}
+void pool_free(void* p, hipStream_t s)
+{
+    if (!p)
+        return;
+    pool_note(p, 0);
+    (void)hipFreeAsync(p, s);
+}
+
+hipError_t mem_alloc(ppfs_ecc_ctx* c, void** p, size_t n)
+{
+    *p = nullptr;
+    if (!c->ms) {
+        const hipError_t e = hipStreamCreateWithFlags(&c->ms, hipStreamNonBlocking);
+        if (e != hipSuccess)
+            return e;
+    }
+    hipError_t e = pool_alloc(p, n, c->ms);
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(c->ms); // usable from any stream from here on
+    return e;
+}
+// caller: nothing still queued reads p
+void mem_free(ppfs_ecc_ctx* c, void* p)
+{
+    pool_free(p, c->ms);
+}
+
+struct PinCache {
+    std::mutex mu;
+    std::multimap<std::pair<size_t, unsigned>, void*> idle;
+    size_t idle_bytes = 0;
+    static constexpr size_t kMaxIdle = 512ull << 20;
+};
+PinCache& pin_cache()
+{
+    static PinCache* pc = new PinCache(); // never destroyed: buffers may be returned at process exit
+    return *pc;
+}
+hipError_t pin_alloc(void** p, size_t n, unsigned flags)
+{
+    PinCache& pc = pin_cache();
+    {
+        std::lock_guard<std::mutex> lk(pc.mu);
+        auto it = pc.idle.find({ n, flags });
+        if (it != pc.idle.end()) {
+            *p = it->second;
+            pc.idle.erase(it);
+            pc.idle_bytes -= n;
+            return hipSuccess;
+        }
+    }
+    return hipHostMalloc(p, n, flags);
+}
+// caller: nothing still queued reads or writes p
+void pin_free(void* p, size_t n, unsigned flags)
+{
+    if (!p)
+        return;
+    PinCache& pc = pin_cache();
+    {
+        std::lock_guard<std::mutex> lk(pc.mu);
+        if (pc.idle_bytes + n <= PinCache::kMaxIdle) {
+            pc.idle.insert({ { n, flags }, p });
+            pc.idle_bytes += n;
+            return;
+        }
+    }
+    (void)hipHostFree(p); // beyond the cache: the synchronizing free
+}
+constexpr unsigned kPinStage = hipHostMallocDefault, kPinMapped = hipHostMallocMapped | hipHostMallocCoherent;
+
 // Is s capturing a hipGraph?  Work queued then runs later, once per replay, possibly on another
 // stream or concurrently with itself.
 bool capturing(hipStream_t s)
@@ -710,9 +825,11 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
     }
     if (c->rs_fast && c->rs_t2 <= 8) {
         const size_t cb = sizeof(uint32_t) * ppfs_ecc_ctx::kTkSlots * 2 * ppfs_ecc_ctx::kTkSetWords;
-        e = hipMalloc(&c->d_ctr, cb);
+        e = mem_alloc(c, (void**)&c->d_ctr, cb);
         if (e == hipSuccess)
-            e = hipMemset(c->d_ctr, 0, cb);
+            e = hipMemsetAsync(c->d_ctr, 0, cb, c->ms);
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(c->ms);
         if (e != hipSuccess) {
             ppfs_ecc_destroy(c);
             return fail(PPFS_ECC_EHIP, "ticket counters", e);
@@ -721,17 +838,17 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
     if (!tables.empty()) {
         // through a page-locked bounce buffer: the engine never hands pageable memory to a copy
         uint8_t* bounce = nullptr;
-        e = hipMalloc(&c->d_tables, tables.size());
+        e = mem_alloc(c, (void**)&c->d_tables, tables.size());
         if (e == hipSuccess)
-            e = hipHostMalloc((void**)&bounce, tables.size(), hipHostMallocDefault);
+            e = pin_alloc((void**)&bounce, tables.size(), kPinStage);
         if (e == hipSuccess) {
             std::memcpy(bounce, tables.data(), tables.size());
-            e = dma_async(c->d_tables, bounce, tables.size(), hipMemcpyHostToDevice, nullptr);
+            e = dma_async(c->d_tables, bounce, tables.size(), hipMemcpyHostToDevice, c->ms);
             if (e == hipSuccess)
-                e = hipStreamSynchronize(nullptr);
+                e = hipStreamSynchronize(c->ms);
         }
-        if (bounce)
-            (void)hipHostFree(bounce);
+        if (bounce && e == hipSuccess)
+            pin_free(bounce, tables.size(), kPinStage);
         if (e != hipSuccess) {
             ppfs_ecc_destroy(c);
             return fail(PPFS_ECC_EHIP, "table upload", e);
@@ -804,24 +921,20 @@ extern "C" void ppfs_ecc_destroy(ppfs_ecc_ctx* c)
         c->h_zc = nullptr;
         c->h_box = nullptr;
     }
+    // frees that never synchronize the device (mem_free, pin_free)
     for (int i = 0; i < 2; ++i) {
         if (c->hs[i])
             (void)hipStreamDestroy(c->hs[i]);
-        if (c->h_pin[i])
-            (void)hipHostFree(c->h_pin[i]);
-        if (c->d_stage[i])
-            (void)hipFree(c->d_stage[i]);
+        pin_free(c->h_pin[i], c->pin_bytes, kPinStage);
+        mem_free(c, c->d_stage[i]);
     }
-    if (c->d_tables)
-        (void)hipFree(c->d_tables);
-    if (c->d_ctr)
-        (void)hipFree(c->d_ctr);
-    if (c->d_scratch)
-        (void)hipFree(c->d_scratch);
-    if (c->h_zc)
-        (void)hipHostFree(c->h_zc);
-    if (c->h_box) // after the streams drained: the launch path's flag kernels write it
-        (void)hipHostFree(c->h_box);
+    mem_free(c, c->d_tables);
+    mem_free(c, c->d_ctr);
+    mem_free(c, c->d_scratch);
+    pin_free(c->h_zc, c->zc_bytes, kPinMapped);
+    pin_free(c->h_box, sizeof(ppfs::SrvBox), kPinMapped); // after the streams drained: flag kernels write it
+    if (c->ms)
+        (void)hipStreamDestroy(c->ms); // its frees complete first
     delete c;
 }
 
@@ -982,11 +1095,11 @@ static int ensure_scratch(ppfs_ecc_ctx* c, size_t bytes, hipStream_t s)
     if (c->d_scratch) {
         // an earlier write on this stream may still read the old scratch status
         HIP_TRY(hipStreamSynchronize(s), "scratch sync");
-        (void)hipFree(c->d_scratch);
+        mem_free(c, c->d_scratch);
     }
     c->d_scratch = nullptr;
     c->scratch_bytes = 0;
-    HIP_TRY(hipMalloc(&c->d_scratch, bytes), "scratch alloc");
+    HIP_TRY(mem_alloc(c, (void**)&c->d_scratch, bytes), "scratch alloc");
     c->scratch_bytes = bytes;
     return 0;
 }
@@ -1093,16 +1206,18 @@ static int ensure_staging(ppfs_ecc_ctx* c, size_t bytes)
         if (c->hs[i])
             HIP_TRY(hipStreamSynchronize(c->hs[i]), "staging sync");
     for (int i = 0; i < 2; ++i) {
-        if (c->h_pin[i])
-            (void)hipHostFree(c->h_pin[i]);
-        if (c->d_stage[i])
-            (void)hipFree(c->d_stage[i]);
+        pin_free(c->h_pin[i], c->pin_bytes, kPinStage);
+        mem_free(c, c->d_stage[i]);
         c->h_pin[i] = nullptr;
         c->d_stage[i] = nullptr;
+    }
+    c->stage_bytes = c->pin_bytes = 0;
+    for (int i = 0; i < 2; ++i) {
         if (!c->hs[i])
             HIP_TRY(hipStreamCreateWithFlags(&c->hs[i], hipStreamNonBlocking), "stream");
-        HIP_TRY(hipHostMalloc(&c->h_pin[i], bytes, hipHostMallocDefault), "pinned alloc");
-        HIP_TRY(hipMalloc(&c->d_stage[i], bytes), "stage alloc");
+        HIP_TRY(pin_alloc((void**)&c->h_pin[i], bytes, kPinStage), "pinned alloc");
+        c->pin_bytes = bytes;
+        HIP_TRY(mem_alloc(c, (void**)&c->d_stage[i], bytes), "stage alloc");
     }
     c->stage_bytes = bytes;
     return 0;
@@ -1220,6 +1335,10 @@ static bool host_pinned(const void* p, size_t bytes)
 {
     if (!p || !n)
         return true;
+#ifdef PPFS_ECC_DEBUG
+    if (pool_covers(p, n)) // the engine's own stream-ordered allocations
+        return true;
+#endif
     auto dev_byte = [](const void* q) {
         hipPointerAttribute_t a;
         if (hipPointerGetAttributes(&a, q) != hipSuccess) {
@@ -1378,8 +1497,7 @@ static int ensure_box(ppfs_ecc_ctx* c)
 {
     if (c->h_box)
         return 0;
-    HIP_TRY(hipHostMalloc((void**)&c->h_box, sizeof(ppfs::SrvBox), hipHostMallocMapped | hipHostMallocCoherent),
-        "mailbox");
+    HIP_TRY(pin_alloc((void**)&c->h_box, sizeof(ppfs::SrvBox), kPinMapped), "mailbox");
     std::memset((void*)c->h_box, 0, sizeof(ppfs::SrvBox));
     HIP_TRY(hipHostGetDevicePointer((void**)&c->d_box, c->h_box, 0), "mailbox map");
     return 0;
@@ -1465,12 +1583,11 @@ static int host_run_small(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, ui
             return PPFS_ECC_EHIP;
         if (c->h_zc && c->hs[0])
             HIP_TRY(hipStreamSynchronize(c->hs[0]), "zero-copy sync");
-        if (c->h_zc)
-            (void)hipHostFree(c->h_zc);
+        pin_free(c->h_zc, c->zc_bytes, kPinMapped);
         c->h_zc = c->d_zc = nullptr;
         c->zc_bytes = 0;
         const size_t bytes = std::max(L.total, layout_for(c, kSmallBlocks).total);
-        HIP_TRY(hipHostMalloc((void**)&c->h_zc, bytes, hipHostMallocMapped | hipHostMallocCoherent), "zero-copy alloc");
+        HIP_TRY(pin_alloc((void**)&c->h_zc, bytes, kPinMapped), "zero-copy alloc");
         HIP_TRY(hipHostGetDevicePointer((void**)&c->d_zc, c->h_zc, 0), "zero-copy map");
         c->zc_bytes = bytes;
     }
@@ -1818,9 +1935,9 @@ extern "C" int ppfs_ecc_scrub_device(ppfs_ecc_ctx* c, uint8_t* d_image, size_t i
     uint8_t* d_spill = nullptr;
     uint8_t* bounce = nullptr; // page-locked: the spill records and patches never DMA pageable memory
     if (chain) {
-        HIP_TRY(hipMallocAsync((void**)&d_spill, nblocks * sb, s), "scrub spill alloc");
-        if (hipHostMalloc((void**)&bounce, std::max<size_t>(nblocks * sb, 256), hipHostMallocDefault) != hipSuccess) {
-            (void)hipFreeAsync(d_spill, s);
+        HIP_TRY(pool_alloc((void**)&d_spill, nblocks * sb, s), "scrub spill alloc");
+        if (pin_alloc((void**)&bounce, std::max<size_t>(nblocks * sb, 256), kPinStage) != hipSuccess) {
+            pool_free(d_spill, s);
             return fail(PPFS_ECC_ENOMEM, "scrub spill bounce");
         }
     }
@@ -1847,11 +1964,11 @@ extern "C" int ppfs_ecc_scrub_device(ppfs_ecc_ctx* c, uint8_t* d_image, size_t i
     std::vector<uint8_t> dummy(chain ? nblocks : 0);
     const int r = scrub_run(c, image_bytes, nblocks, dummy.data(), ops);
     if (d_spill) {
-        (void)hipFreeAsync(d_spill, s);
+        pool_free(d_spill, s);
         (void)hipStreamSynchronize(s); // the bounce's last copy is done before it is freed
     }
     if (bounce)
-        (void)hipHostFree(bounce);
+        pin_free(bounce, std::max<size_t>(nblocks * sb, 256), kPinStage);
     return r;
 }
 
@@ -1914,9 +2031,10 @@ extern "C" int ppfs_vote3_host(int device, const uint8_t* a, const uint8_t* b, c
     HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "vote3 stream");
     uint8_t *d = nullptr, *h = nullptr;
     const size_t dmg_off = (4 * nbytes + 255) & ~(size_t)255, total = dmg_off + nrec * sizeof(uint32_t);
-    hipError_t e = hipMalloc(&d, total);
+    // stream-ordered device memory and the page-locked cache: nothing here synchronizes the device
+    hipError_t e = pool_alloc((void**)&d, total, s);
     if (e == hipSuccess)
-        e = hipHostMalloc((void**)&h, total, hipHostMallocDefault);
+        e = pin_alloc((void**)&h, total, kPinStage);
     if (e == hipSuccess) {
         std::memcpy(h, a, nbytes);
         std::memcpy(h + nbytes, b, nbytes);
@@ -1938,9 +2056,11 @@ extern "C" int ppfs_vote3_host(int device, const uint8_t* a, const uint8_t* b, c
     }
     const int r = e != hipSuccess ? fail(PPFS_ECC_EHIP, "vote3", e) : 0;
     if (h)
-        (void)hipHostFree(h);
-    if (d)
-        (void)hipFree(d);
+        pin_free(h, total, kPinStage);
+    if (d) {
+        pool_free(d, s);
+        (void)hipStreamSynchronize(s);
+    }
     (void)hipStreamDestroy(s);
     return r;
 }

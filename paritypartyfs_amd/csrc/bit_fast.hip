@@ -1097,7 +1097,10 @@ extern "C" hipError_t ppfs_crc_fast_encode(const uint8_t* d, uint8_t* r, const u
     const bf::CrcFast a { bs, ds, n, bs - ds, (uint32_t)mask, nb * (uint64_t)ds };
     if ((nb + 4ull * bf::CRC_BPW - 1) / (4ull * bf::CRC_BPW) > (1ull << 30))
         return hipErrorInvalidValue;
-    if (bs - ds == 4) { // 4-byte field: two blocks per wave from payload-aligned pieces
+#ifndef PPFS_CRC_ENC2
+#define PPFS_CRC_ENC2 1
+#endif
+    if (PPFS_CRC_ENC2 && bs - ds == 4) { // 4-byte field: two blocks per wave from payload-aligned pieces
         const uint64_t per_wg = 2ull * bf::WAVES * bf::CRC_BPW;
         const dim3 grid((uint32_t)((nb + per_wg - 1) / per_wg));
         switch (bs) {

@@ -145,3 +145,12 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_server_launch_t, PPFS_T2)(ppfs::SrvBox* b
 #endif
     return hipGetLastError();
 }
+
+#if defined(PPFS_TK_TRACE) && PPFS_T2 <= 8
+// profiling builds: the encode's per-phase cycle sums (rs_wg_tk.hpp g_tk_trace) into host memory
+extern "C" hipError_t PPFS_CAT(ppfs_tk_trace_read_t, PPFS_T2)(void* dst, size_t bytes)
+{
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(wg::g_tk_trace), bytes < sizeof(wg::g_tk_trace) ? bytes : sizeof(wg::g_tk_trace), 0,
+        hipMemcpyDeviceToHost);
+}
+#endif

@@ -120,6 +120,22 @@ __device__ __forceinline__ void tk_clear(uint32_t* __restrict__ ctr_clear, uint3
         __hip_atomic_store(ctr_clear + 32u * x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// PPFS_TK_TRACE (profiling builds only, tools/build_alt.sh --product trace -DPPFS_TK_TRACE=1): waves 0
+// and 1 of every encode workgroup sum s_memtime cycles per loop phase into g_tk_trace, read back by
+// ppfs_tk_trace_read_t<2t> (tools/tk_trace.py).  Normal builds: nothing.
+#ifdef PPFS_TK_TRACE
+constexpr int TK_TRACE_N = 10; // prologue, issue, remainder, barrier B, emission, vm wait, barrier A, epilogue, iterations, end
+__device__ uint64_t g_tk_trace[4096 * 2 * TK_TRACE_N];
+#define PPFS_TK_MARK(i)                                                                                                \
+    do {                                                                                                               \
+        const uint64_t now_ = clock64();                                                                               \
+        tr_[i] += now_ - tlast_;                                                                                       \
+        tlast_ = now_;                                                                                                 \
+    } while (0)
+#else
+#define PPFS_TK_MARK(i) ((void)0)
+#endif
+
 template <int T2, int WPC = 2, int NTST = 1>
 __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t* __restrict__ data,
     uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables, uint32_t* __restrict__ ctr,
@@ -144,6 +160,11 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
     const uint64_t nfull = nblocks / TB, ntiles = (nblocks + TB - 1) / TB;
     const TkGeom g = tk_geom();
     uint32_t* const my_ctr = ctr + 32u * g.xc; // 128-byte lines
+#ifdef PPFS_TK_TRACE
+    uint64_t tr_[TK_TRACE_N] = {};
+    uint64_t tlast_ = clock64();
+    const uint64_t t0_ = tlast_;
+#endif
     // the first two tiles are static: local tickets rank and rank + gx
     uint64_t q0 = tk_tile(g.rank, g, nfull), q1 = tk_tile(g.rank + g.gx, g, nfull);
     uint32_t hist = 0;
@@ -169,12 +190,15 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
     if (dmaw)
         vm_wait_exact(kd * hist); // tile q0 landed, q1 may fly
     barrier_lds();
+    PPFS_TK_MARK(0);
     uint32_t cur = 0, pc = 0, iter = 0;
     while (q0 < nfull) {
         // A: tile q0 in LDS, the last emission reads done, the next ticket published (the first
         // pass: tables, parity slots and the iteration-2 ticket in place)
-        if (iter)
+        if (iter) {
             barrier_lds();
+            PPFS_TK_MARK(6);
+        }
         const uint64_t ahead = __builtin_amdgcn_readfirstlane(s_tk[(iter + 2u) & 3u]);
         // no initial value: writing the register outside wave 0's branch would make every wave wait
         // for the previous ticket (the compiler tracks its pending write per register)
@@ -187,10 +211,13 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
             dma_tile192<IN_PIECES>(lds + D::OFF_BUF + ring_add(cur, NBUF - 1, NBUF) * BUF + PAD, data + ahead * (TB * K),
                 tid, data, nblocks * K);
         hist = (hist << 1) | (go ? 1u : 0u);
+        PPFS_TK_MARK(1);
         if (wave == 0)
             *(uint64_t*)(lds + D::OFF_PAR + (pc ^ 1u) * 512u + 8u * lane) = 0;
         phase_remainder<T2, K, D::NMAP>(lds, buf, par, wave, row);
+        PPFS_TK_MARK(2);
         barrier_lds(); // B: parity slots complete
+        PPFS_TK_MARK(3);
         uint8_t* dst = raw + q0 * (TB * 255);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -200,6 +227,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
                 st_nt<NTST>(dst + 16u * p, o);
         }
         ++iter;
+        PPFS_TK_MARK(4);
         if (dmaw) {
             // the next tile's DMA (issued an iteration ago, or in the prologue) landed; newer: the
             // last two iterations' stores and this iteration's DMA
@@ -208,6 +236,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
         }
         if (tk_lane)
             s_tk[(iter + 2u) & 3u] = (uint32_t)tk_tile(tk + 2u * g.gx, g, nfull); // the tile of (iteration iter - 1) + 3
+        PPFS_TK_MARK(5);
         cur = ring_add(cur, 1, NBUF);
         pc ^= 1u;
         q0 = q1;
@@ -236,6 +265,15 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
                 st_bytes(dst + 16u * p, v, nout - 16u * p);
         }
     }
+#ifdef PPFS_TK_TRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PPFS_TK_MARK(7);
+    tr_[8] = iter;
+    tr_[9] = clock64() - t0_;
+    if (wave < 2 && lane == 0 && blockIdx.x < 4096)
+        for (int i = 0; i < TK_TRACE_N; ++i)
+            g_tk_trace[(blockIdx.x * 2 + wave) * TK_TRACE_N + i] = tr_[i];
+#endif
 }
 
 // ------------------------------------------------------------------------------------
@@ -265,8 +303,6 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
     const bool dmaw = wave != 0, tk_lane = wave == 0 && lane == 0;
     const uint32_t row = lane_row(lane);
     const bool wb = write_back != 0, want = data != nullptr;
-    // full tiles of a 32-byte aligned image write back whole sectors (rs_wg.hpp SectorWb)
-    const bool sect = PPFS_WB_SECTOR && wb && ((uintptr_t)raw & 31u) == 0;
     const uint64_t nfull = nblocks / TB, ntiles = (nblocks + TB - 1) / TB;
     const TkGeom g = tk_geom();
     uint32_t* const my_ctr = ctr + 32u * g.xc;
@@ -303,8 +339,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         phase_remainder<T2, 255>(lds, buf, par, wave, row);
         barrier_lds(); // B: remainders complete
         if (wave == 0) {
-            const uint32_t st = phase_correct<T2>(lds, buf, par, row, true, raw, q0 * TB + row, wb, nblocks * 255u,
-                sect ? raw + q0 * (TB * 255) : nullptr);
+            const uint32_t st = phase_correct<T2>(lds, buf, par, row, true, raw, q0 * TB + row, wb, nblocks * 255u);
             if (status && PPFS_DBG_OK(status + q0 * TB + row, 1, status, nblocks))
                 status[q0 * TB + row] = (uint8_t)st;
         }

@@ -69,8 +69,12 @@ def test_destroy_does_not_wait_for_another_contexts_server(oracle):
         r = torch.zeros(nb * n, dtype=torch.uint8, device="cuda")
         torch.cuda.synchronize()
         times = []
+        hdata = adata[: 200 * k].copy()
+        hraw = np.zeros(200 * n, np.uint8)
         for _ in range(5):
             A = EccEngine(ECC_REED_SOLOMON, 512, 3)
+            A.encode_host(hdata, hraw)  # A's own streams and staging (chunked host path)
+            assert np.array_equal(hraw, acw[: 200 * n])
             A.encode(d, r)  # queued on torch's stream
             t0 = time.perf_counter()
             A.close()
@@ -84,7 +88,8 @@ def test_destroy_does_not_wait_for_another_contexts_server(oracle):
         th.join(60)
     assert not errors, errors[:5]
     assert calls[0] > 100, calls[0]  # B kept serving throughout
-    # a device-wide synchronize would wait for B's resident launch (up to SRV_LIFETIME_US = 1 s)
+    # a device-wide synchronize -- hipDeviceSynchronize, or a hipFree / hipHostFree, which wait for
+    # every stream of the device -- would wait for B's resident launch (up to SRV_LIFETIME_US = 1 s)
     assert max(times) < 0.25, times
     B.close()
 
