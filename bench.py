@@ -252,7 +252,7 @@ class HipEvents:
             self.L.hipEventDestroy(e)
 
 
-def timed_steps(step, steps, world, sync, device=None, pre=None):
+def timed_steps(step, steps, world, sync, device=None, pre=None, bar_group=None):
     """Time exactly `steps` calls of step() between barrier + sync on both sides; returns the
     MAX elapsed seconds over ranks (every rank gets the same value).  The barrier and the
     max-reduce are the only collectives: nothing on the data path.
@@ -261,7 +261,10 @@ def timed_steps(step, steps, world, sync, device=None, pre=None):
     the ranks meet -- an RCCL barrier idles the host for long enough that an idle GPU drops its
     clocks, and the first timed steps then ran ~15 % slow (r3c: 0.2675 vs 0.2294 ms per step under
     torchrun at WORLD_SIZE=1 with the barrier on an idle GPU).  The synchronize after the barrier
-    drains pre()'s work; the region starts from a busy, clocked-up GPU."""
+    drains pre()'s work; the region starts from a busy, clocked-up GPU.  bar_group: the process group
+    of the barriers (a gloo group beside RCCL: an RCCL barrier's kernel waits for the work queued on
+    the current stream, so the host reached the region's synchronize only after the GPU had drained
+    and idled -- r3e, 0.2553 vs 0.2258 ms per step of device time under torchrun at WORLD_SIZE=1)."""
     import torch
     import torch.distributed as dist
 
@@ -271,7 +274,7 @@ def timed_steps(step, steps, world, sync, device=None, pre=None):
     if pre is not None:
         pre()
     if coll:
-        dist.barrier()
+        dist.barrier(group=bar_group)
     sync()
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -279,7 +282,7 @@ def timed_steps(step, steps, world, sync, device=None, pre=None):
     sync()
     elapsed = time.perf_counter() - t0
     if coll:
-        dist.barrier()
+        dist.barrier(group=bar_group)
         tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
@@ -379,6 +382,8 @@ def main(argv=None):
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
+    # the timed region's barriers over gloo (CPU) beside RCCL, which keeps the max-reduce (timed_steps)
+    bar_group = dist.new_group(backend="gloo") if dist.is_initialized() and dist.get_backend() == "nccl" else None
     dev = torch.device("cuda", torch.cuda.current_device())
     red_dev = red_dev or dev
     # Every launch of the run goes to one created stream, not the legacy null stream (which orders
@@ -477,11 +482,11 @@ def main(argv=None):
     # run slower while they ramp back: r2c, 0.311 ms per step after a host-side check vs 0.25 back
     # to back).  The self-check runs after the region.
     elapsed = timed_steps(lambda: run_steps(args.steps), 1, world, torch.cuda.synchronize, red_dev,
-                          pre=lambda: run_steps(args.warmup))
+                          pre=lambda: run_steps(args.warmup), bar_group=bar_group)
     # the same timed region again, 3 times (reported beside the measurement, never as `value`):
     # shows whether the measured region was representative of back-to-back regions
     repeats = [timed_steps(lambda: run_steps(args.steps), 1, world, torch.cuda.synchronize, red_dev,
-                           pre=lambda: run_steps(max(2, args.warmup))) / args.steps * 1e3
+                           pre=lambda: run_steps(max(2, args.warmup)), bar_group=bar_group) / args.steps * 1e3
                for _ in range(3)]
     # device-side self-check of the last timed step: every block corrected, payload restored
     ok = bool(torch.equal(out, data)) and int(status.min()) == 1 and int(status.max()) == 1
@@ -742,7 +747,7 @@ def main(argv=None):
             "roofline_frac_of_device_copy": round(achieved / copy_gbs, 4) if copy_gbs else None,
             "host_inclusive": host_incl,
             "kernel_path": eng.stream_kernel_name(stream),
-            "collectives": ("rccl" if dist.is_initialized() and dist.get_backend() == "nccl"
+            "collectives": ("rccl max-reduce, gloo barriers" if dist.is_initialized() and dist.get_backend() == "nccl"
                             else "gloo" if dist.is_initialized() else "none (single process, no torchrun)"),
             "launch": f"hipGraph of {group} steps" if graph is not None else "eager",
             "host_issue_us_per_eager_step": round(t_issue * 1e6, 1),

@@ -422,7 +422,7 @@ std::vector<uint8_t> build_crc_tables(uint64_t P, int n, uint32_t ds)
 // T[i][v] = (v << 4i) * C mod P for a constant C = x^e mod P.  Maps: x^0, x^32, x^64, x^96 (piece
 // dwords), x^8192 (one lane's pieces, 1 KiB apart), x^(128 2^j) j < 6 (lane tree), then the final
 // factor placing the zero-padded 16-byte grid: encode x^(8 (ds + m - 1024 (NP + 1)) + n - 1) for
-// each payload misalignment m < 16, check x^(8 (ds - bs) + n - 1); then x^4096.
+// each payload misalignment m < 16, check x^(8 (ds - bs) + n - 1).
 std::vector<uint8_t> build_crc_fast_tables(uint64_t P, int n, uint32_t ds, uint32_t bs)
 {
     CrcHost c { P, n, n == 64 ? ~0ull : ((1ull << n) - 1) };
@@ -433,7 +433,7 @@ std::vector<uint8_t> build_crc_fast_tables(uint64_t P, int n, uint32_t ds, uint3
     for (long m = 0; m < 16; ++m)
         ex.push_back(8L * ((long)ds + m - 1024L * (NP + 1)) + n - 1);
     ex.push_back(8L * ((long)ds - (long)bs) + n - 1);
-    ex.push_back(4096); // the 2-blocks-per-wave encode's Horner step (bit_fast.hip CF_K2)
+
     std::vector<uint8_t> out((size_t)ppfs_crc_fast_tables_bytes(), 0);
     uint32_t* t = (uint32_t*)out.data();
     for (size_t mi = 0; mi < ex.size(); ++mi) {
@@ -990,7 +990,7 @@ static bool sync_check_enabled()
 
 static int sync_check(int r, void* stream, const char* what)
 {
-    if (r || !sync_check_enabled())
+    if (r || !sync_check_enabled() || capturing((hipStream_t)stream)) // a capture runs nothing yet
         return r;
     hipError_t e = hipStreamSynchronize((hipStream_t)stream);
     if (e == hipSuccess)

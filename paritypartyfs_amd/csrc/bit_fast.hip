@@ -694,10 +694,8 @@ __global__ __launch_bounds__(256) void parity_fast_check_kernel(const uint8_t* _
 //   payload's real position (e < 0 uses x^-1: P(0) = 1).
 // ------------------------------------------------------------------------------------
 constexpr int CF_MAP = 512;                      // 8 nibbles x 16 entries x u32
-// maps: x^0, x^32, x^64, x^96 | x^8192 | x^(128 2^j), j < 6 | encode placement x 16 | check
-// placement | x^4096 (Horner step of the 2-blocks-per-wave encode: 32 lanes x 16 B)
-constexpr int CF_M0 = 0, CF_K = 4, CF_L = 5, CF_FENC = 11, CF_FCHK = 27, CF_K2 = 28, CF_NMAPS = 29;
-constexpr int CF_BYTES = CF_NMAPS * CF_MAP;     // 14.5 KiB
+constexpr int CF_M0 = 0, CF_K = 4, CF_L = 5, CF_FENC = 11, CF_FCHK = 27, CF_NMAPS = 28;
+constexpr int CF_BYTES = CF_NMAPS * CF_MAP;     // 14 KiB
 // Blocks per wave of the CRC kernels: a workgroup stages the 14 KiB of maps once and then walks
 // CRC_BPW consecutive 4-block groups (one contiguous range, so the full grid keeps its address
 // order); with one group per workgroup the map staging read as much L2 as the blocks themselves.
@@ -860,92 +858,6 @@ __global__ __launch_bounds__(256) void crc_fast_encode_kernel(const uint8_t* __r
     }
 }
 
-// ------------------------------------------------------------------------------------
-// CRC encode, two blocks per wave, for a 4-byte field (ds = bs - 4, ds % 4 == 0: n in [25, 32];
-// cfg4's 0x9960034c is n = 32).  Lanes 32 h + i take block 2 p + h, piece j = 32 k + i of the
-// PAYLOAD (bytes [16 j, 16 j + 16) at its own 4-byte alignment -- unaligned loads), so raw piece j =
-// payload piece j for every j but the last, which holds the payload's last 12 bytes and the field:
-// no neighbour-lane shifts to build the output, and 64 NP pieces instead of the aligned superset's
-// 64 NP + 1.  The CRC is the check kernel's over the raw grid (crc_fast_check_kernel: the field
-// bytes masked to zero, placement CF_FCHK), with a lane's 2 NP pieces 4096 bits apart (Horner with
-// x^4096) and a 5-level tree per 32-lane half: per block 3 maps per piece-round pair and 2.5 tree
-// maps where the one-block-per-wave kernel spends 3 x 5 + 4 and 6.
-// ------------------------------------------------------------------------------------
-typedef uint32_t bf_u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-typedef uint32_t bf_u32x3a4 __attribute__((ext_vector_type(3), aligned(4)));
-
-template <int NP>
-__global__ __launch_bounds__(256) void crc_fast_encode2_kernel(const uint8_t* __restrict__ data,
-    uint8_t* __restrict__ raw, const uint8_t* __restrict__ skip, uint64_t nblocks_all, CrcFast a,
-    const uint8_t* __restrict__ tables)
-{
-    constexpr int R = 2 * NP;             // piece rounds per lane
-    constexpr uint32_t LAST = 64 * NP - 1; // the 12-byte piece
-    __shared__ __attribute__((aligned(16))) uint8_t tbl[CF_BYTES];
-    for (uint32_t p = threadIdx.x; p < CF_BYTES / 16; p += 256)
-        *(uint4*)(tbl + 16 * p) = *(const uint4*)(tables + 16 * p);
-    __syncthreads();
-    const uint32_t lane = lane_id(), wave = wave_id(), h = lane >> 5, i = lane & 31u;
-    const bool n32 = a.n == 32;
-    const uint64_t wg0 = (uint64_t)blockIdx.x * (2 * WAVES * CRC_BPW);
-    const uint64_t wend = nblocks_all < wg0 + 2 * WAVES * CRC_BPW ? nblocks_all : wg0 + 2 * WAVES * CRC_BPW;
-    for (uint64_t b0 = wg0 + 2u * wave; b0 < wend; b0 += 2 * WAVES) {
-        const uint64_t blk = b0 + h;
-        const bool valid = blk < wend;
-        const uint8_t* src = data + blk * a.ds;
-        uint8_t* rb = raw + blk * a.bs;
-        uint4 v[R];
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            const uint32_t j = 32u * k + i;
-            v[k] = make_uint4(0, 0, 0, 0);
-            if (valid && (k < R - 1 || j < LAST)) {
-                if (PPFS_DBG_OK(src + 16u * j, 16, data, a.data_bytes)) {
-                    const bf_u32x4a4 u = *(const bf_u32x4a4*)(src + 16u * j);
-                    v[k] = make_uint4(u.x, u.y, u.z, u.w);
-                }
-            } else if (valid && PPFS_DBG_OK(src + 16u * j, 12, data, a.data_bytes)) { // the payload's last 12 bytes
-                const bf_u32x3a4 u = *(const bf_u32x3a4*)(src + 16u * j);
-                v[k] = make_uint4(u.x, u.y, u.z, 0u);
-            }
-        }
-        const bool write = valid && !(skip && PPFS_DBG_OK(skip + blk, 1, skip, nblocks_all) && skip[blk] == 5);
-        if (write) {
-#pragma unroll
-            for (int k = 0; k < R; ++k) {
-                const uint32_t j = 32u * k + i;
-                if ((k < R - 1 || j < LAST) && PPFS_DBG_OK(rb + 16u * j, 16, raw, nblocks_all * a.bs))
-                    gst16_raw(rb + 16u * j, v[k]);
-            }
-        }
-        uint32_t acc = 0;
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-            const uint32_t pv = crc_piece(tbl, v[k], 0u, (k == R - 1 && i == 31u) ? 12u : 16u, n32);
-            acc = k == 0 ? pv : (cmap(tbl + CF_K2 * CF_MAP, acc) ^ pv);
-        }
-#pragma unroll
-        for (int t = 0; t < 5; ++t) { // lanes 0 and 32: their half's sum of acc_i x^(128 (31 - i))
-            const uint32_t other = __shfl_down(acc, 1 << t, 64);
-            acc = cmap(tbl + (CF_L + t) * CF_MAP, acc) ^ other;
-        }
-        const uint32_t s0 = (uint32_t)__builtin_amdgcn_readlane((int)acc, 0);
-        const uint32_t s1 = (uint32_t)__builtin_amdgcn_readlane((int)acc, 32);
-        const uint32_t V = cmap(tbl + CF_FCHK * CF_MAP, h ? s1 : s0);
-        const uint32_t st = (V << 1) & a.mask;
-        if (write && i == 31u) {
-            // raw bytes [ds, ds + 4): the n CRC bits MSB first (n < 32: the last byte keeps its old
-            // low 32 - n bits)
-            uint32_t f = st << (32u - a.n);
-            if (a.n < 32u && PPFS_DBG_OK(rb + a.ds + 3u, 1, raw, nblocks_all * a.bs))
-                f |= (uint32_t)rb[a.ds + 3u] & ((1u << (32u - a.n)) - 1u);
-            const uint4 o = make_uint4(v[R - 1].x, v[R - 1].y, v[R - 1].z, bswap(f));
-            if (PPFS_DBG_OK(rb + 16u * LAST, 16, raw, nblocks_all * a.bs))
-                gst16_raw(rb + 16u * LAST, o);
-        }
-    }
-}
-
 template <int NP>
 __global__ __launch_bounds__(256) void crc_fast_check_kernel(const uint8_t* __restrict__ raw,
     uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks_all, CrcFast a,
@@ -1097,25 +1009,6 @@ extern "C" hipError_t ppfs_crc_fast_encode(const uint8_t* d, uint8_t* r, const u
     const bf::CrcFast a { bs, ds, n, bs - ds, (uint32_t)mask, nb * (uint64_t)ds };
     if ((nb + 4ull * bf::CRC_BPW - 1) / (4ull * bf::CRC_BPW) > (1ull << 30))
         return hipErrorInvalidValue;
-#ifndef PPFS_CRC_ENC2
-#define PPFS_CRC_ENC2 1
-#endif
-    if (PPFS_CRC_ENC2 && bs - ds == 4) { // 4-byte field: two blocks per wave from payload-aligned pieces
-        const uint64_t per_wg = 2ull * bf::WAVES * bf::CRC_BPW;
-        const dim3 grid((uint32_t)((nb + per_wg - 1) / per_wg));
-        switch (bs) {
-        case 1024:
-            hipLaunchKernelGGL(bf::crc_fast_encode2_kernel<1>, grid, dim3(256), 0, s, d, r, skip, nb, a, tab);
-            break;
-        case 2048:
-            hipLaunchKernelGGL(bf::crc_fast_encode2_kernel<2>, grid, dim3(256), 0, s, d, r, skip, nb, a, tab);
-            break;
-        default:
-            hipLaunchKernelGGL(bf::crc_fast_encode2_kernel<4>, grid, dim3(256), 0, s, d, r, skip, nb, a, tab);
-            break;
-        }
-        return hipGetLastError();
-    }
     PPFS_NP_DISPATCH(bs, bf::crc_fast_encode_kernel, (nb + bf::CRC_BPW - 1) / bf::CRC_BPW, s, d, r, skip, nb, a, tab)
     return hipGetLastError();
 }

@@ -221,13 +221,10 @@ __device__ __noinline__ void bs_correct_general(uint8_t* lds, uint32_t goff, uin
 // Decode correction for the pair's block: rs_pair.hpp pair_correct (single error: X = S_2/S_1,
 // e = S_1/X, confirmed iff c mod g == e * (x^p mod g); else the general path), with S_1 and S_2
 // read from the S12 byte table -- 16 lookups per lane where the log / exp forms took 48.
-// sect (full tiles of a 32-byte aligned image): the single-error fix only patches the LDS row and
-// returns its tile byte offset in sect_off (the caller stores the 32-byte sector once every lane's
-// fixes are in the image, rs_wg.hpp SectorWb); the rare general path writes its bytes back itself.
 template <int T2>
 __device__ __forceinline__ uint32_t bs_correct(uint8_t* lds, uint32_t goff, uint32_t s12off, const uint8_t* __restrict__ xp,
     uint32_t row, uint32_t c, const uint32_t (&s)[4], bool valid, uint8_t* __restrict__ raw_g, uint64_t gblk,
-    bool wb, uint64_t raw_bytes, bool sect = false, uint32_t tile_row = 0, uint32_t* sect_off = nullptr)
+    bool wb, uint64_t raw_bytes)
 {
     const bool err = valid && pair::pair_or<1>(s[0] | s[1] | s[2] | s[3]) != 0u;
     if (!__builtin_amdgcn_ballot_w64(err))
@@ -256,11 +253,8 @@ __device__ __forceinline__ uint32_t bs_correct(uint8_t* lds, uint32_t goff, uint
         bad |= ev != rb ? 1u : 0u;
     }
     const bool geo = err && pair::pair_or<1>(bad) == 0u;
-    if (geo && c == 0) {
-        col::col_fix(lds, row, raw_g, gblk, wb && !sect, lx, gf.exp(le), raw_bytes);
-        if (sect && wb)
-            *sect_off = tile_row + lx;
-    }
+    if (geo && c == 0)
+        col::col_fix(lds, row, raw_g, gblk, wb, lx, gf.exp(le), raw_bytes);
     if (err && !geo)
         bs_correct_general<T2>(lds, goff, row, c, s[0], s[1], s[2], s[3], raw_g, gblk, wb, raw_bytes);
     return err ? 1u : 0u;
@@ -465,8 +459,6 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
     constexpr int KO = (OUT_PIECES + 63) / 64;
     __shared__ __attribute__((aligned(16))) uint8_t lds[D::BYTES];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
-    // full tiles (8,160 = 255 x 32 bytes) of a 32-byte aligned image write back whole sectors
-    const bool sect = PPFS_WB_SECTOR && write_back != 0 && ((uintptr_t)raw & 31u) == 0;
     for (uint32_t p = tid; p < (uint32_t)TAB_BYTES / 16; p += 64u * NW)
         *(uint4*)(lds + OFF_TAB + 16 * p) = *(const uint4*)(tables + L::OFF_BS + 16 * p);
     for (uint32_t p = tid; p < (uint32_t)GF_BYTES / 16; p += 64u * NW)
@@ -504,20 +496,11 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
         uint32_t s[4];
         bs_cmodg(s, lds, row, Ln);
         const uint64_t gblk = t * TBW + Ln.blk;
-        uint32_t so = ~0u;
         const uint32_t st = bs_correct<T2>(
-            lds, D::OFF_GF, D::OFF_S12, xpm, row, Ln.c, s, true, raw, gblk, wb, nblocks * 255u, sect, 255u * Ln.blk, &so);
+            lds, D::OFF_GF, D::OFF_S12, xpm, row, Ln.c, s, true, raw, gblk, wb, nblocks * 255u);
         if (status && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
             status[gblk] = (uint8_t)st;
         wave_fence(); // corrections patched into the image rows
-        if (so != ~0u) { // this lane's single-error fix: its whole 32-byte sector (rs_wg.hpp SectorWb)
-            so &= ~31u;
-            uint8_t* const tg = raw + t * (TBW * 255);
-            if (PPFS_DBG_OK(tg + so, 32, raw, nblocks * 255u)) {
-                *(uint4*)(tg + so) = *(const uint4*)(lds + img + so);
-                *(uint4*)(tg + so + 16u) = *(const uint4*)(lds + img + so + 16u);
-            }
-        }
         if (want) {
             uint8_t* dst = data + t * (TBW * K);
 #pragma unroll

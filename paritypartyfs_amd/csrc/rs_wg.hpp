@@ -275,6 +275,37 @@ __device__ __forceinline__ M128 range_mask(uint32_t lo, uint32_t hi)
 }
 __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 
+// The emission's unaligned LDS window: the n dwords at LDS byte S & ~3 (S any byte).  Read as
+// 8-byte aligned ds_read_b64 pairs: consecutive lanes read windows 16 bytes apart, so n dword reads
+// put lanes l, l + 8, l + 16, l + 24 on one bank (4-way conflicts, 8 LDS cycles each) where the
+// b64 pairs conflict 2-way (the trace build showed the emission at 23 % of the encode's cycles).
+#ifndef PPFS_EMIT_B64
+#define PPFS_EMIT_B64 1
+#endif
+template <int N> __device__ __forceinline__ void lds_window(uint32_t (&d)[N], const uint8_t* lds, uint32_t S)
+{
+    if constexpr (PPFS_EMIT_B64) {
+        constexpr int NP = (N + 2) / 2; // 8-byte pairs covering N dwords from any 4-byte start
+        const uint2* w2 = (const uint2*)(lds + (S & ~7u));
+        uint32_t w[2 * NP];
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+            const uint2 v = w2[i];
+            w[2 * i] = v.x;
+            w[2 * i + 1] = v.y;
+        }
+        const bool odd = (S & 4u) != 0;
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            d[i] = odd ? w[i + 1] : w[i];
+    } else {
+        const uint32_t* w = (const uint32_t*)(lds + (S & ~3u));
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            d[i] = w[i];
+    }
+}
+
 // Encode emission: 16 bytes of the codeword tile at piece p, from the LDS payload rows and the
 // combined parity slots.  Codeword byte j of block b = j / 255 (off = j % 255): parity byte off if
 // off < 2t, else payload byte K b + off - 2t.  A piece may run into block b+1 (off > 239).
@@ -284,12 +315,9 @@ __device__ __forceinline__ uint4 enc_piece(const uint8_t* lds, uint32_t buf, uin
     constexpr uint32_t K = 255 - T2;
     const uint32_t j0 = p * 16u, b = j0 / 255u, off = j0 - 255u * b;
     const uint32_t S = buf + PAD + K * b + off - T2; // LDS byte of output byte 0's payload source
-    const uint32_t* w = (const uint32_t*)(lds + (S & ~3u));
     const uint32_t sh = (S & 3u) * 8u;
     uint32_t d[5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i)
-        d[i] = w[i];
+    lds_window(d, lds, S);
     uint32_t X[4], Y[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m)
@@ -335,12 +363,9 @@ template <int T2> __device__ __forceinline__ uint4 dec_piece(const uint8_t* lds,
     constexpr uint32_t K = 255 - T2;
     const uint32_t j0 = p * 16u, b = j0 / K, off = j0 - K * b;
     const uint32_t S = buf + PAD + 255u * b + T2 + off;
-    const uint32_t* w = (const uint32_t*)(lds + (S & ~3u));
     const uint32_t sh = (S & 3u) * 8u;
     uint32_t d[7];
-#pragma unroll
-    for (int i = 0; i < 7; ++i)
-        d[i] = w[i];
+    lds_window(d, lds, S);
     uint32_t X[6];
 #pragma unroll
     for (int m = 0; m < 6; ++m)
@@ -388,50 +413,11 @@ __device__ __forceinline__ void stage_bytes(uint8_t* dst, const uint8_t* __restr
         dst[i] = src[i];
 }
 
-#ifndef PPFS_WB_SECTOR
-#define PPFS_WB_SECTOR 1
-#endif
-// Write-back of whole 32-byte sectors (full tiles of a 32-byte aligned codeword buffer): the tile
-// (64 x 255 = 510 x 32 bytes) is sector-aligned, so the sector around a corrected byte lies in the
-// LDS image, which after the corrections holds exactly the bytes the write-back leaves in HBM (the
-// corrected ones, and unchanged ones that equal HBM's).  A full-sector store replaces the 1-byte
-// partial write, which the memory side has to merge into its sector.  Lanes whose
-// fixes share a sector store the same 32 bytes.  sect_off = the tile's first byte in raw_g.
-struct SectorWb {
-    uint32_t s0 = ~0u, s1 = ~0u, s2 = ~0u, s3 = ~0u; // sectors (byte offset in the tile) to store
-    __device__ void add(uint32_t off)
-    {
-        const uint32_t so = off & ~31u;
-        if (so != s0) {
-            s3 = s2;
-            s2 = s1;
-            s1 = s0;
-            s0 = so;
-        }
-    }
-    // after every lane's fixes are in LDS (tile image at LDS byte `img`)
-    __device__ void store(const uint8_t* lds, uint32_t img, uint8_t* __restrict__ tile_g) const
-    {
-        const uint32_t v[4] = { s0, s1, s2, s3 };
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (v[i] == ~0u)
-                continue;
-            const uint4 a = *(const uint4*)(lds + img + v[i]), b = *(const uint4*)(lds + img + v[i] + 16u);
-            *(uint4*)(tile_g + v[i]) = a;
-            *(uint4*)(tile_g + v[i] + 16u) = b;
-        }
-    }
-};
-
 // Decode phase 2 (wave 0, lane = block): the reference correction for blocks with r' != 0.
-// fix(pos, e) patches codeword byte pos of the lane's row (LDS) and, with write-back, in HBM: the
-// byte itself, or (sect != null, full tiles) the 32-byte sector around it once every lane's fixes
-// are in the LDS image (SectorWb).
+// fix(pos, e) patches codeword byte pos of the lane's row (LDS) and, with write-back, in HBM.
 template <int T2>
 __device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, uint32_t par, uint32_t r, bool valid,
-    uint8_t* __restrict__ raw_g, uint64_t blk, bool wb, [[maybe_unused]] uint64_t raw_bytes,
-    uint8_t* __restrict__ sect_tile = nullptr)
+    uint8_t* __restrict__ raw_g, uint64_t blk, bool wb, [[maybe_unused]] uint64_t raw_bytes)
 {
     using L = RsWgLayout<T2>;
     const uint64_t rem = *(const uint64_t*)(lds + par + 8u * r);
@@ -461,16 +447,12 @@ __device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, ui
                 S[i] = (s[i >> 2] >> (8 * (i & 3))) & 0xFFu;
             geo = rs_geometric<T2>(S, gf, gpos, ge);
         }
-        SectorWb sw;
-        const bool sect = wb && sect_tile != nullptr;
         auto fix = [&](uint32_t pos, uint32_t e) {
             if (e == 0)
                 return;
             const uint8_t fixed = (uint8_t)(lds[row + pos] ^ e);
             lds[row + pos] = fixed;
-            if (sect)
-                sw.add(255u * r + pos);
-            else if (wb && PPFS_DBG_OK(raw_g + blk * 255u + pos, 1, raw_g, raw_bytes))
+            if (wb && PPFS_DBG_OK(raw_g + blk * 255u + pos, 1, raw_g, raw_bytes))
                 wb_byte(raw_g + blk * 255u + pos, fixed);
         };
         if (__builtin_amdgcn_ballot_w64(err && !geo)) {
@@ -482,11 +464,6 @@ __device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, ui
             }
         } else if (err && geo) {
             fix(gpos, ge);
-        }
-        if (sect) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); // every lane's fixes in the image (one wave)
-            if (PPFS_DBG_OK(sect_tile, (uint64_t)TB * 255u, raw_g, raw_bytes))
-                sw.store(lds, buf + PAD, sect_tile);
         }
     }
     return err ? 1u : 0u;

@@ -36,6 +36,7 @@ def _rs_batch(oracle, nb, seed, bs=512, t=3):
     return n, k, data, oracle.rs_encode(bs, t, data)
 
 
+@pytest.mark.timeout(90)
 def test_destroy_does_not_wait_for_another_contexts_server(oracle):
     """B serves one-block decodes from its resident launch in a loop (the launch stays up to 1 s); A
     queues a batch on torch's stream and is destroyed: A's destroy waits for A's batch only."""
@@ -59,33 +60,43 @@ def test_destroy_does_not_wait_for_another_contexts_server(oracle):
         except Exception as e:  # noqa: BLE001 -- reported below
             errors.append(repr(e))
 
+    # The main thread never synchronizes the device while B serves: a device-wide wait can starve as
+    # long as B keeps relaunching its server (hipDeviceSynchronize waits for the device to go idle).
+    nb = 1 << 16
+    _, _, adata, acw = _rs_batch(oracle, nb, 32)
+    ms = torch.cuda.Stream()
+    with torch.cuda.stream(ms):
+        d = torch.from_numpy(adata).cuda()
+        r = torch.zeros(nb * n, dtype=torch.uint8, device="cuda")
+    ms.synchronize()
+    hdata = adata[: 200 * k].copy()
+    hraw = np.zeros(200 * n, np.uint8)
+    times = []
     th = threading.Thread(target=serve)
     th.start()
     try:
         time.sleep(0.2)  # B's server is resident and busy
-        nb = 1 << 16
-        _, _, adata, acw = _rs_batch(oracle, nb, 32)
-        d = torch.from_numpy(adata).cuda()
-        r = torch.zeros(nb * n, dtype=torch.uint8, device="cuda")
-        torch.cuda.synchronize()
-        times = []
-        hdata = adata[: 200 * k].copy()
-        hraw = np.zeros(200 * n, np.uint8)
+        t_end = time.perf_counter() + 20.0
         for _ in range(5):
+            if time.perf_counter() > t_end:  # a hang here would be the bug under test: fail, do not wait
+                break
             A = EccEngine(ECC_REED_SOLOMON, 512, 3)
             A.encode_host(hdata, hraw)  # A's own streams and staging (chunked host path)
             assert np.array_equal(hraw, acw[: 200 * n])
-            A.encode(d, r)  # queued on torch's stream
+            A.encode(d, r, stream=ms)  # queued on a caller stream
             t0 = time.perf_counter()
             A.close()
             times.append(time.perf_counter() - t0)
-            torch.cuda.synchronize()
-            assert np.array_equal(r.cpu().numpy(), acw)  # A's work finished before its tables went away
-            r.zero_()
+            ms.synchronize()
+            with torch.cuda.stream(ms):
+                got = r.cpu().numpy()
+                r.zero_()
+            assert np.array_equal(got, acw)  # A's work finished before its tables went away
         time.sleep(0.1)
     finally:
         stop.set()
         th.join(60)
+    assert len(times) == 5, times
     assert not errors, errors[:5]
     assert calls[0] > 100, calls[0]  # B kept serving throughout
     # a device-wide synchronize -- hipDeviceSynchronize, or a hipFree / hipHostFree, which wait for

@@ -285,9 +285,7 @@ def test_rs_generic_spill_matches_oracle(oracle):
 # ------------------------------------------------------------------------------------
 # bs 1024/2048/4096 with a degree <= 32 polynomial run the streaming kernels of bit_fast.hip
 # (0xc1acf: degree 20, a partial last CRC byte whose low bits keep the old contents)
-# A 4-byte field (degree 25..32) at bs >= 1024 encodes two blocks per wave from payload-aligned
-# pieces (bit_fast.hip crc_fast_encode2_kernel); degrees 29 and 25 keep old low bits in the last
-# field byte; odd block counts leave the last wave's second block empty.
+# Degrees 29 and 25 at bs >= 1024: a 4-byte field whose last byte keeps old low bits.
 CRC_CASES = [(0xea, 256), (0xc1acf, 512), (0x9960034c, 512), (0x9960034c, 4096), (0x5, 64), (0x3, 256),
              (0x42F0E1EBA9EA3693 >> 1, 1024), (0x1021 >> 1, 4096), (0x9960034c, 1024), (0x9960034c, 2048),
              (0xea, 2048), (0xc1acf, 1024), (0xc1acf, 4096), (0x1EDC6F41, 1024), (0x1000003, 4096),

@@ -4,10 +4,10 @@
 set -o pipefail
 TAG=${1:-r3d}
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu > gpurun_out/${TAG}_gputest.log 2>&1
-rc=$?; tail -3 gpurun_out/${TAG}_gputest.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error" gpurun_out/${TAG}_gputest.log | head -20; exit $rc; }
+[ -n "$SKIP_SUITE" ] || { timeout -k 10 600 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu > gpurun_out/${TAG}_gputest.log 2>&1
+rc=$?; tail -3 gpurun_out/${TAG}_gputest.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error" gpurun_out/${TAG}_gputest.log | head -20; exit $rc; }; }
 timeout -k 10 600 bash tools/gpu_debug_suite.sh ${TAG}_debug || exit 1
-for v in new crc1 new crc1; do
+for v in new crc1 crc1nf bfpf r3base new crc1 crc1nf bfpf r3base; do
   if [ $v = new ]; then L=$PWD/paritypartyfs_amd/_lib/libppfs_ecc.so; else L=$PWD/paritypartyfs_amd/_lib/alt/libppfs_ecc_$v.so; fi
   PPFS_ECC_LIB=$L timeout -k 10 120 python tools/bench_configs.py --only crc >> gpurun_out/${TAG}_crc_$v.jsonl 2>> gpurun_out/${TAG}_crc.err || exit 1
 done
