@@ -153,4 +153,9 @@ extern "C" hipError_t PPFS_CAT(ppfs_tk_trace_read_t, PPFS_T2)(void* dst, size_t 
     return hipMemcpyFromSymbol(dst, HIP_SYMBOL(wg::g_tk_trace), bytes < sizeof(wg::g_tk_trace) ? bytes : sizeof(wg::g_tk_trace), 0,
         hipMemcpyDeviceToHost);
 }
+extern "C" hipError_t PPFS_CAT(ppfs_tk_trace_dec_read_t, PPFS_T2)(void* dst, size_t bytes)
+{
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(wg::g_tk_trace_dec),
+        bytes < sizeof(wg::g_tk_trace_dec) ? bytes : sizeof(wg::g_tk_trace_dec), 0, hipMemcpyDeviceToHost);
+}
 #endif

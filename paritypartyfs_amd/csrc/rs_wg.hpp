@@ -280,7 +280,7 @@ __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { re
 // put lanes l, l + 8, l + 16, l + 24 on one bank (4-way conflicts, 8 LDS cycles each) where the
 // b64 pairs conflict 2-way (the trace build showed the emission at 23 % of the encode's cycles).
 #ifndef PPFS_EMIT_B64
-#define PPFS_EMIT_B64 1
+#define PPFS_EMIT_B64 0
 #endif
 template <int N> __device__ __forceinline__ void lds_window(uint32_t (&d)[N], const uint8_t* lds, uint32_t S)
 {
@@ -294,10 +294,13 @@ template <int N> __device__ __forceinline__ void lds_window(uint32_t (&d)[N], co
             w[2 * i] = v.x;
             w[2 * i + 1] = v.y;
         }
-        const bool odd = (S & 4u) != 0;
+        // a bit select, not a ?: on the array: the compiler turns w[i + odd] into an LDS-promoted
+        // private array (a ds_write of the window and a re-read per piece) -- r3f: 2x the emission
+        uint32_t m = (S & 4u) ? ~0u : 0u;
+        asm("" : "+v"(m));
 #pragma unroll
         for (int i = 0; i < N; ++i)
-            d[i] = odd ? w[i + 1] : w[i];
+            d[i] = bfi(m, w[i + 1], w[i]);
     } else {
         const uint32_t* w = (const uint32_t*)(lds + (S & ~3u));
 #pragma unroll

@@ -126,6 +126,9 @@ __device__ __forceinline__ void tk_clear(uint32_t* __restrict__ ctr_clear, uint3
 #ifdef PPFS_TK_TRACE
 constexpr int TK_TRACE_N = 10; // prologue, issue, remainder, barrier B, emission, vm wait, barrier A, epilogue, iterations, end
 __device__ uint64_t g_tk_trace[4096 * 2 * TK_TRACE_N];
+// decode: prologue, issue, remainder, barrier B, correction (+ barrier C), emission, vm wait, barrier A,
+// iterations, end
+__device__ uint64_t g_tk_trace_dec[4096 * 2 * TK_TRACE_N];
 #define PPFS_TK_MARK(i)                                                                                                \
     do {                                                                                                               \
         const uint64_t now_ = clock64();                                                                               \
@@ -306,6 +309,11 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
     const uint64_t nfull = nblocks / TB, ntiles = (nblocks + TB - 1) / TB;
     const TkGeom g = tk_geom();
     uint32_t* const my_ctr = ctr + 32u * g.xc;
+#ifdef PPFS_TK_TRACE
+    uint64_t tr_[TK_TRACE_N] = {};
+    uint64_t tlast_ = clock64();
+    const uint64_t t0_ = tlast_;
+#endif
     uint64_t q0 = tk_tile(g.rank, g, nfull); // static first tile
     if (dmaw) {
         if (q0 < nfull)
@@ -322,10 +330,13 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // tile q0 / tables and the ticket landed
     barrier_lds();
+    PPFS_TK_MARK(0);
     uint32_t cur = 0, pc = 0, iter = 0;
     while (q0 < nfull) {
-        if (iter)
+        if (iter) {
             barrier_lds(); // A: tile q0 in LDS, the last emission reads done, the next ticket published
+            PPFS_TK_MARK(7);
+        }
         const uint64_t q1 = __builtin_amdgcn_readfirstlane(s_tk[(iter + 1u) & 3u]);
         uint32_t tk; // no initial value (see the encode)
         if (tk_lane)
@@ -334,16 +345,20 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         if (dmaw && q1 < nfull)
             dma_tile192<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, raw + q1 * (TB * 255), tid, raw,
                 nblocks * 255u);
+        PPFS_TK_MARK(1);
         if (wave == 0)
             *(uint64_t*)(lds + D::OFF_PAR + (pc ^ 1u) * 512u + 8u * lane) = 0;
         phase_remainder<T2, 255>(lds, buf, par, wave, row);
+        PPFS_TK_MARK(2);
         barrier_lds(); // B: remainders complete
+        PPFS_TK_MARK(3);
         if (wave == 0) {
             const uint32_t st = phase_correct<T2>(lds, buf, par, row, true, raw, q0 * TB + row, wb, nblocks * 255u);
             if (status && PPFS_DBG_OK(status + q0 * TB + row, 1, status, nblocks))
                 status[q0 * TB + row] = (uint8_t)st;
         }
         barrier_lds(); // C: corrections patched into the LDS rows
+        PPFS_TK_MARK(4);
         if (want) {
             uint8_t* dst = data + q0 * (TB * K);
 #pragma unroll
@@ -355,6 +370,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
             }
         }
         ++iter;
+        PPFS_TK_MARK(5);
         if (dmaw) { // the next tile's DMA landed; this tile's stores may fly
             if (want)
                 asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -363,6 +379,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         }
         if (tk_lane)
             s_tk[(iter + 1u) & 3u] = (uint32_t)tk_tile(tk + g.gx, g, nfull); // the tile of (iteration iter - 1) + 2
+        PPFS_TK_MARK(6);
         cur ^= 1u;
         pc ^= 1u;
         q0 = q1;
@@ -399,6 +416,14 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
             }
         }
     }
+#ifdef PPFS_TK_TRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tr_[8] = iter;
+    tr_[9] = clock64() - t0_;
+    if (wave < 2 && lane == 0 && blockIdx.x < 4096)
+        for (int i = 0; i < TK_TRACE_N; ++i)
+            g_tk_trace_dec[(blockIdx.x * 2 + wave) * TK_TRACE_N + i] = tr_[i];
+#endif
 }
 
 } // namespace wg

@@ -20,6 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 PHASES = ["prologue", "issue", "remainder", "barrier_B", "emission", "vm_wait", "barrier_A", "epilogue"]
+PHASES_DEC = ["prologue", "issue", "remainder", "barrier_B", "correction", "emission", "vm_wait", "barrier_A"]
 N = 10
 
 
@@ -58,28 +59,36 @@ def main():
         for _ in range(8):
             step()
         torch.cuda.synchronize()
-    # the last launch's trace: end with an encode so its sums are what the buffer holds
+    # the last launches' traces: the encode's and (in-step) the decode's sums of the final step
     for _ in range(3):
         step()
-    eng.encode(data, cw, nblocks=nb)
     torch.cuda.synchronize()
     L = _native.lib()
-    fn = L.ppfs_tk_trace_read_t6
-    fn.restype = ctypes.c_int
-    fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
-    buf = np.zeros(4096 * 2 * N, np.uint64)
-    rc = fn(buf.ctypes.data, buf.nbytes)
-    assert rc == 0, rc
-    grid = 2 * torch.cuda.get_device_properties(0).multi_processor_count
-    tr = buf.reshape(4096, 2, N)[:grid].astype(np.float64)
-    res = {"blocks": nb, "grid": grid, "mode": "standalone" if a.standalone else "in-step"}
-    for w, name in ((0, "wave0_ticket"), (1, "wave1_dma")):
-        t = tr[:, w, :]
-        tot = t[:, 9].mean()
-        res[name] = {"total_cycles": round(tot), "iterations": round(t[:, 8].mean(), 2),
-                     **{p: round(t[:, i].mean()) for i, p in enumerate(PHASES)},
-                     "share": {p: round(t[:, i].mean() / tot, 3) for i, p in enumerate(PHASES)},
-                     "per_iter": {p: round(t[:, i].sum() / max(1.0, t[:, 8].sum())) for i, p in enumerate(PHASES[1:7], 1)}}
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    res = {"blocks": nb, "mode": "standalone" if a.standalone else "in-step"}
+
+    def read(fname, wpc, phases, key):
+        fn = getattr(L, fname)
+        fn.restype = ctypes.c_int
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        buf = np.zeros(4096 * 2 * N, np.uint64)
+        rc = fn(buf.ctypes.data, buf.nbytes)
+        assert rc == 0, rc
+        grid = wpc * cus
+        tr = buf.reshape(4096, 2, N)[:grid].astype(np.float64)
+        out = {"grid": grid}
+        for w, name in ((0, "wave0"), (1, "wave1_dma")):
+            t = tr[:, w, :]
+            tot = t[:, 9].mean()
+            out[name] = {"total_cycles": round(tot), "iterations": round(t[:, 8].mean(), 2),
+                         "share": {p: round(t[:, i].mean() / tot, 3) for i, p in enumerate(phases)},
+                         "per_iter": {p: round(t[:, i].sum() / max(1.0, t[:, 8].sum())) for i, p in enumerate(phases)
+                                      if i > 0}}
+        res[key] = out
+
+    read("ppfs_tk_trace_read_t6", 2, PHASES, "encode")
+    if not a.standalone:
+        read("ppfs_tk_trace_dec_read_t6", 3, PHASES_DEC, "decode")
     print(json.dumps(res), flush=True)
 
 
