@@ -227,43 +227,12 @@ __device__ __forceinline__ void phase_remainder(uint8_t* lds, uint32_t buf, uint
 }
 
 // the same for a LEN-byte row at LDS byte `row` (any row layout)
-// NMAP = 7 (the ticket encode, round 3): the x^(32 m) maps (MAP32 copied to OFF_MAP), and each lane
-// runs its 64-byte segment as two independent 32-byte chains of 4 slicing steps (bytes 64 w + [0, 32)
-// and + [32, 64)) moved by their own maps: 5 dependent table rounds instead of 9, for 12 more lookups
-template <int T2, int LEN, int W>
-__device__ __forceinline__ void seg_remainder_ilp2(uint32_t (&s)[2], const uint8_t* lds, uint32_t row)
-{
-    uint32_t a[2], b[2];
-    seg_remainder<T2, LEN, 2 * W, 32>(a, lds, row);
-    seg_remainder<T2, LEN, 2 * W + 1, 32>(b, lds, row);
-    if constexpr (W > 0)
-        seg_map<T2, 2 * W>(a, lds);
-    seg_map<T2, 2 * W + 1>(b, lds);
-    s[0] = a[0] ^ b[0];
-    s[1] = a[1] ^ b[1];
-}
-
 template <int T2, int LEN, int NMAP>
 __device__ __forceinline__ void phase_remainder_row(uint8_t* lds, uint32_t row, uint32_t par, uint32_t wave, uint32_t blk)
 {
-    static_assert(NMAP == 2 || NMAP == 3 || NMAP == 7, "x^(64 s) or x^(32 s) maps");
+    static_assert(NMAP == 2 || NMAP == 3, "x^(64 s) maps");
     uint32_t s[2];
-    if constexpr (NMAP == 7) {
-        switch (wave) {
-        case 0:
-            seg_remainder_ilp2<T2, LEN, 0>(s, lds, row);
-            break;
-        case 1:
-            seg_remainder_ilp2<T2, LEN, 1>(s, lds, row);
-            break;
-        case 2:
-            seg_remainder_ilp2<T2, LEN, 2>(s, lds, row);
-            break;
-        default:
-            seg_remainder_ilp2<T2, LEN, 3>(s, lds, row);
-            break;
-        }
-    } else switch (wave) {
+    switch (wave) {
     case 0:
         seg_remainder<T2, LEN, 0>(s, lds, row);
         break;
@@ -540,12 +509,10 @@ __device__ __forceinline__ void vm_wait_newer(uint32_t n)
 
 // COMPACT (encode only): 2 maps (phase_remainder NMAP = 2) and tile buffers sized for the 64
 // payload rows (PAD + 64 K + 32) instead of 64 codewords, so 3 ring buffers fit 3 workgroups / CU
-// MAPS (encode only): 7 = the x^(32 m) maps at OFF_MAP (phase_remainder NMAP = 7)
-template <int T2, bool DEC, int NBUF, bool COMPACT = false, int MAPS = 0> struct Lds {
+template <int T2, bool DEC, int NBUF, bool COMPACT = false> struct Lds {
     using L = RsWgLayout<T2>;
     static_assert(!(DEC && COMPACT), "compact layout: encode only");
-    static_assert(MAPS == 0 || (MAPS == 7 && !DEC && !COMPACT), "32-byte maps: encode only");
-    static constexpr int NMAP = MAPS ? MAPS : COMPACT ? 2 : 3;
+    static constexpr int NMAP = COMPACT ? 2 : 3;
     static constexpr int TBL = DEC ? L::TABLE_BYTES : L::OFF_MAP + NMAP * L::MAP_STRIDE; // encode: SL + MAP only
     static constexpr int OFF_PAR = TBL;                              // 2 x 64 x 8 B remainder slots
     static constexpr int OFF_BUF = OFF_PAR + 1024 + 64;             // + slack: par[b+1] over-read
