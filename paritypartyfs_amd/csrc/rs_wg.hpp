@@ -275,38 +275,14 @@ __device__ __forceinline__ M128 range_mask(uint32_t lo, uint32_t hi)
 }
 __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 
-// The emission's unaligned LDS window: the n dwords at LDS byte S & ~3 (S any byte).  Read as
-// 8-byte aligned ds_read_b64 pairs: consecutive lanes read windows 16 bytes apart, so n dword reads
-// put lanes l, l + 8, l + 16, l + 24 on one bank (4-way conflicts, 8 LDS cycles each) where the
-// b64 pairs conflict 2-way (the trace build showed the emission at 23 % of the encode's cycles).
-#ifndef PPFS_EMIT_B64
-#define PPFS_EMIT_B64 0
-#endif
+// The emission's unaligned LDS window: the n dwords at LDS byte S & ~3 (S any byte).  (Round 3: 8-byte
+// aligned reads with a dword select measured slower, emission 1,747 vs 1,573 cycles per tile.)
 template <int N> __device__ __forceinline__ void lds_window(uint32_t (&d)[N], const uint8_t* lds, uint32_t S)
 {
-    if constexpr (PPFS_EMIT_B64) {
-        constexpr int NP = (N + 2) / 2; // 8-byte pairs covering N dwords from any 4-byte start
-        const uint2* w2 = (const uint2*)(lds + (S & ~7u));
-        uint32_t w[2 * NP];
+    const uint32_t* w = (const uint32_t*)(lds + (S & ~3u));
 #pragma unroll
-        for (int i = 0; i < NP; ++i) {
-            const uint2 v = w2[i];
-            w[2 * i] = v.x;
-            w[2 * i + 1] = v.y;
-        }
-        // a bit select, not a ?: on the array: the compiler turns w[i + odd] into an LDS-promoted
-        // private array (a ds_write of the window and a re-read per piece) -- r3f: 2x the emission
-        uint32_t m = (S & 4u) ? ~0u : 0u;
-        asm("" : "+v"(m));
-#pragma unroll
-        for (int i = 0; i < N; ++i)
-            d[i] = bfi(m, w[i + 1], w[i]);
-    } else {
-        const uint32_t* w = (const uint32_t*)(lds + (S & ~3u));
-#pragma unroll
-        for (int i = 0; i < N; ++i)
-            d[i] = w[i];
-    }
+    for (int i = 0; i < N; ++i)
+        d[i] = w[i];
 }
 
 // Encode emission: 16 bytes of the codeword tile at piece p, from the LDS payload rows and the
