@@ -177,11 +177,11 @@ __device__ __forceinline__ void bs_cmodg(uint32_t (&s)[4], const uint8_t* lds, u
 // Lane c computes S_i, i = 16c+1 .. 16c+16, over the whole c mod g state (coefficient q has
 // exponent i q); lane 0 then holds S_1..S_32 and runs BM / roots / Forney.
 template <int T2>
-__device__ __noinline__ void bs_correct_general(uint8_t* lds, uint32_t goff, uint32_t row, uint32_t c, uint32_t s0,
+__device__ __noinline__ void bs_correct_general(uint8_t* lds, const uint8_t* gfp, uint32_t row, uint32_t c, uint32_t s0,
     uint32_t s1, uint32_t s2, uint32_t s3, uint8_t* __restrict__ raw_g, uint64_t gblk, bool wb, uint64_t raw_bytes)
 {
     static_assert(T2 == 32, "state byte q = coefficient q");
-    const Gf gf { lds + goff };
+    const Gf gf { gfp };
     const uint32_t own[4] = { s0, s1, s2, s3 };
     uint32_t rw[8];
 #pragma unroll
@@ -221,16 +221,17 @@ __device__ __noinline__ void bs_correct_general(uint8_t* lds, uint32_t goff, uin
 // Decode correction for the pair's block: rs_pair.hpp pair_correct (single error: X = S_2/S_1,
 // e = S_1/X, confirmed iff c mod g == e * (x^p mod g); else the general path), with S_1 and S_2
 // read from the S12 byte table -- 16 lookups per lane where the log / exp forms took 48.
+// gfp, s12p: the GF block and the S12 table, in LDS or (BsLds TLDS) in global memory
 template <int T2>
-__device__ __forceinline__ uint32_t bs_correct(uint8_t* lds, uint32_t goff, uint32_t s12off, const uint8_t* __restrict__ xp,
+__device__ __forceinline__ uint32_t bs_correct(uint8_t* lds, const uint8_t* gfp, const uint8_t* s12p, const uint8_t* __restrict__ xp,
     uint32_t row, uint32_t c, const uint32_t (&s)[4], bool valid, uint8_t* __restrict__ raw_g, uint64_t gblk,
     bool wb, uint64_t raw_bytes)
 {
     const bool err = valid && pair::pair_or<1>(s[0] | s[1] | s[2] | s[3]) != 0u;
     if (!__builtin_amdgcn_ballot_w64(err))
         return 0u;
-    const Gf gf { lds + goff };
-    const uint16_t* t = (const uint16_t*)(lds + s12off + 8192u * c); // state byte u = 16c + k
+    const Gf gf { gfp };
+    const uint16_t* t = (const uint16_t*)(s12p + 8192u * c); // state byte u = 16c + k
     uint32_t s12 = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k)
@@ -256,7 +257,7 @@ __device__ __forceinline__ uint32_t bs_correct(uint8_t* lds, uint32_t goff, uint
     if (geo && c == 0)
         col::col_fix(lds, row, raw_g, gblk, wb, lx, gf.exp(le), raw_bytes);
     if (err && !geo)
-        bs_correct_general<T2>(lds, goff, row, c, s[0], s[1], s[2], s[3], raw_g, gblk, wb, raw_bytes);
+        bs_correct_general<T2>(lds, gfp, row, c, s[0], s[1], s[2], s[3], raw_g, gblk, wb, raw_bytes);
     return err ? 1u : 0u;
 }
 
@@ -316,11 +317,13 @@ __device__ __forceinline__ void put_parity(uint8_t* lds, uint32_t img, const BsL
 
 // LDS plan: [0, 64 KiB) byte-slice tables | (decode: GF block, S12 table) |
 // NW x NBUF wave images | 64 B slack (the rows' last-word reads and the decode emission's second
-// window run past the last image)
-template <int NW, int NBUF, bool DEC> struct BsLds {
+// window run past the last image).  TLDS (decode): 0 = GF block and S12 table in LDS, 1 = the GF
+// block only (S12 read from the global table blob), 2 = neither (both global) -- LDS for more waves.
+template <int NW, int NBUF, bool DEC, int TLDS = 0> struct BsLds {
+    static constexpr bool GF_IN = DEC && TLDS < 2, S12_IN = DEC && TLDS < 1;
     static constexpr int OFF_GF = TAB_BYTES;
-    static constexpr int OFF_S12 = OFF_GF + (DEC ? GF_BYTES : 0);
-    static constexpr int OFF_IMG = OFF_S12 + (DEC ? 32 * 256 * 2 : 0);
+    static constexpr int OFF_S12 = OFF_GF + (GF_IN ? GF_BYTES : 0);
+    static constexpr int OFF_IMG = OFF_S12 + (S12_IN ? 32 * 256 * 2 : 0);
     static constexpr int BYTES = OFF_IMG + NW * (NBUF > 0 ? NBUF : 1) * IMGW + 64;
     static_assert(BYTES <= 163840, "one workgroup per CU: 160 KiB of LDS");
     static_assert(OFF_IMG % 16 == 0 && IMGW % 16 == 0, "aligned images");
@@ -446,14 +449,14 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_encode_kernel(const uint8_t*
 // of line); corrections patch the image row and, with write-back, the codeword byte in HBM; the
 // payload pieces come straight from the image.  Single-buffered: the correction path's XP-row
 // loads are compiler-counted, and their waits would drain a prefetch.
-template <int T2, int NW, int NBUF = 1, int NTST = 1>
+template <int T2, int NW, int NBUF = 1, int NTST = 1, int TLDS = 0>
 __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __restrict__ raw,
     uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables,
     int write_back)
 {
     static_assert(T2 == 32, "byte-slice path: 2t = 32");
     using L = RsPairLayout<T2>;
-    using D = BsLds<NW, NBUF, true>;
+    using D = BsLds<NW, NBUF, true, TLDS>;
     constexpr int K = L::K;
     constexpr int OUT_PIECES = TBW * K / 16; // 446
     constexpr int KO = (OUT_PIECES + 63) / 64;
@@ -461,11 +464,15 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
     for (uint32_t p = tid; p < (uint32_t)TAB_BYTES / 16; p += 64u * NW)
         *(uint4*)(lds + OFF_TAB + 16 * p) = *(const uint4*)(tables + L::OFF_BS + 16 * p);
-    for (uint32_t p = tid; p < (uint32_t)GF_BYTES / 16; p += 64u * NW)
-        *(uint4*)(lds + D::OFF_GF + 16 * p) = *(const uint4*)(tables + L::OFF_GF + 16 * p);
-    for (uint32_t p = tid; p < (uint32_t)L::S12_BYTES / 16; p += 64u * NW)
-        *(uint4*)(lds + D::OFF_S12 + 16 * p) = *(const uint4*)(tables + L::OFF_S12 + 16 * p);
+    if constexpr (D::GF_IN)
+        for (uint32_t p = tid; p < (uint32_t)GF_BYTES / 16; p += 64u * NW)
+            *(uint4*)(lds + D::OFF_GF + 16 * p) = *(const uint4*)(tables + L::OFF_GF + 16 * p);
+    if constexpr (D::S12_IN)
+        for (uint32_t p = tid; p < (uint32_t)L::S12_BYTES / 16; p += 64u * NW)
+            *(uint4*)(lds + D::OFF_S12 + 16 * p) = *(const uint4*)(tables + L::OFF_S12 + 16 * p);
     __syncthreads();
+    const uint8_t* const gfp = D::GF_IN ? lds + D::OFF_GF : tables + L::OFF_GF;
+    const uint8_t* const s12p = D::S12_IN ? lds + D::OFF_S12 : tables + L::OFF_S12;
     const BsLane Ln = bs_lane(lane);
     const bool wb = write_back != 0, want = data != nullptr;
     const uint32_t img = D::OFF_IMG + wave * (uint32_t)IMGW;
@@ -497,7 +504,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
         bs_cmodg(s, lds, row, Ln);
         const uint64_t gblk = t * TBW + Ln.blk;
         const uint32_t st = bs_correct<T2>(
-            lds, D::OFF_GF, D::OFF_S12, xpm, row, Ln.c, s, true, raw, gblk, wb, nblocks * 255u);
+            lds, gfp, s12p, xpm, row, Ln.c, s, true, raw, gblk, wb, nblocks * 255u);
         if (status && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
             status[gblk] = (uint8_t)st;
         wave_fence(); // corrections patched into the image rows
@@ -534,7 +541,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
         const bool valid = Ln.blk < nb;
         const uint64_t gblk = t * TBW + Ln.blk;
         const uint32_t st = bs_correct<T2>(
-            lds, D::OFF_GF, D::OFF_S12, xpm, row, Ln.c, s, valid, raw, gblk, wb, nblocks * 255u);
+            lds, gfp, s12p, xpm, row, Ln.c, s, valid, raw, gblk, wb, nblocks * 255u);
         if (status && valid && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
             status[gblk] = (uint8_t)st;
         wave_fence();

@@ -57,7 +57,13 @@ constexpr int ENC_WPC_STATIC = fit_wpc(wg::lds_bytes<PPFS_T2, false, ENC_NBUF>()
 #elif PPFS_T2 == 32
 // 2t = 32 (rs_bs.hpp): one workgroup per CU, every wave on its own 32-block tiles;
 // encode 12 waves (3 per SIMD), decode 8 (LDS- and register-bound)
-constexpr int BS_ENC_NW = 12, BS_DEC_NW = 8;
+#ifndef PPFS_BS_DEC_NW
+#define PPFS_BS_DEC_NW 8
+#endif
+#ifndef PPFS_BS_DEC_TLDS
+#define PPFS_BS_DEC_TLDS 0
+#endif
+constexpr int BS_ENC_NW = 12, BS_DEC_NW = PPFS_BS_DEC_NW, BS_DEC_TLDS = PPFS_BS_DEC_TLDS;
 #else
 // 8 < 2t <= 16: rs_fast.hpp lane-per-block kernels; 2t = 16 encodes with the solo image kernel
 constexpr bool SOLO_IMG = PPFS_T2 == 16;
@@ -121,7 +127,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
         hipLaunchKernelGGL((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC, 7, 1>), dim3(rs_tile_grid(nb, DEC_WPC)),
             dim3(256), 0, s, r, d, st, nb, tab, wb);
 #elif PPFS_T2 == 32
-    hipLaunchKernelGGL((bs::rs_bs_decode_kernel<PPFS_T2, BS_DEC_NW, 1, 1>), dim3(rs_tile_grid(nb, 1, bs::TBW * BS_DEC_NW)),
+    hipLaunchKernelGGL((bs::rs_bs_decode_kernel<PPFS_T2, BS_DEC_NW, 1, 1, BS_DEC_TLDS>), dim3(rs_tile_grid(nb, 1, bs::TBW * BS_DEC_NW)),
         dim3(64 * BS_DEC_NW), 0, s, r, d, st, nb, tab, wb);
 #else
     hipLaunchKernelGGL(rs255_decode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, r, d, st, nb, tab, wb);
