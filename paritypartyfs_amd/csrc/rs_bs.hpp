@@ -37,6 +37,26 @@ using wg::st_nt;
 #define PPFS_BS_XCHG 0
 #endif
 
+// PPFS_TK_TRACE (profiling builds only): every decode wave sums s_memtime cycles per phase into
+// g_bs_trace (prologue, DMA wait, c mod g, S1/S2 + logs, XP row + confirmation, fix / general path,
+// status, emission, image-free wait + next DMA, iterations, end), read by ppfs_bs_trace_read.
+#ifdef PPFS_TK_TRACE
+constexpr int BS_TRACE_N = 11;
+__device__ uint64_t g_bs_trace[4096 * BS_TRACE_N];
+#define PPFS_BS_MARK(i)                                                                                                \
+    do {                                                                                                               \
+        const uint64_t now_ = clock64();                                                                               \
+        tr_[i] += now_ - tlast_;                                                                                       \
+        tlast_ = now_;                                                                                                 \
+    } while (0)
+#define PPFS_BS_TR_PARAMS , uint64_t (&tr_)[BS_TRACE_N], uint64_t &tlast_
+#define PPFS_BS_TR_ARGS , tr_, tlast_
+#else
+#define PPFS_BS_MARK(i) ((void)0)
+#define PPFS_BS_TR_PARAMS
+#define PPFS_BS_TR_ARGS
+#endif
+
 constexpr int TBW = 32;            // blocks per wave tile
 constexpr int IMGW = TBW * 255;    // 8,160 B: one wave tile's codeword image
 constexpr int IMG_PIECES = IMGW / 16; // 510 16-byte pieces in and out
@@ -225,7 +245,7 @@ __device__ __noinline__ void bs_correct_general(uint8_t* lds, const uint8_t* gfp
 template <int T2>
 __device__ __forceinline__ uint32_t bs_correct(uint8_t* lds, const uint8_t* gfp, const uint8_t* s12p, const uint8_t* __restrict__ xp,
     uint32_t row, uint32_t c, const uint32_t (&s)[4], bool valid, uint8_t* __restrict__ raw_g, uint64_t gblk,
-    bool wb, uint64_t raw_bytes)
+    bool wb, uint64_t raw_bytes PPFS_BS_TR_PARAMS)
 {
     const bool err = valid && pair::pair_or<1>(s[0] | s[1] | s[2] | s[3]) != 0u;
     if (!__builtin_amdgcn_ballot_w64(err))
@@ -243,6 +263,7 @@ __device__ __forceinline__ uint32_t bs_correct(uint8_t* lds, const uint8_t* gfp,
     lx = lx >= 255u ? lx - 255u : lx;
     uint32_t le = l1 + 255u - lx;
     le = le >= 255u ? le - 255u : le;
+    PPFS_BS_MARK(3);
     const uint4 xr = *(const uint4*)(xp + 32u * lx + 16u * c); // XP rows stay in global memory (L2)
     const uint32_t xw[4] = { xr.x, xr.y, xr.z, xr.w };
     uint32_t bad = (s1 == 0u || s2 == 0u) ? 1u : 0u;
@@ -254,10 +275,12 @@ __device__ __forceinline__ uint32_t bs_correct(uint8_t* lds, const uint8_t* gfp,
         bad |= ev != rb ? 1u : 0u;
     }
     const bool geo = err && pair::pair_or<1>(bad) == 0u;
+    PPFS_BS_MARK(4);
     if (geo && c == 0)
         col::col_fix(lds, row, raw_g, gblk, wb, lx, gf.exp(le), raw_bytes);
     if (err && !geo)
         bs_correct_general<T2>(lds, gfp, row, c, s[0], s[1], s[2], s[3], raw_g, gblk, wb, raw_bytes);
+    PPFS_BS_MARK(5);
     return err ? 1u : 0u;
 }
 
@@ -471,6 +494,11 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
         for (uint32_t p = tid; p < (uint32_t)L::S12_BYTES / 16; p += 64u * NW)
             *(uint4*)(lds + D::OFF_S12 + 16 * p) = *(const uint4*)(tables + L::OFF_S12 + 16 * p);
     __syncthreads();
+#ifdef PPFS_TK_TRACE
+    uint64_t tr_[BS_TRACE_N] = {};
+    uint64_t tlast_ = clock64();
+    const uint64_t t0_ = tlast_;
+#endif
     const uint8_t* const gfp = D::GF_IN ? lds + D::OFF_GF : tables + L::OFF_GF;
     const uint8_t* const s12p = D::S12_IN ? lds + D::OFF_S12 : tables + L::OFF_S12;
     const BsLane Ln = bs_lane(lane);
@@ -492,6 +520,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
             dma_wave(base, raw + t * (TBW * 255), lane, src_off, raw, nblocks * 255u);
         }
     }
+    PPFS_BS_MARK(0);
     for (; t < nfull; t += S) {
         const uint64_t nx = t + S;
         if constexpr (NBUF == 0) {
@@ -500,14 +529,20 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        PPFS_BS_MARK(1);
         uint32_t s[4];
         bs_cmodg(s, lds, row, Ln);
+#ifdef PPFS_TK_TRACE
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+        PPFS_BS_MARK(2);
         const uint64_t gblk = t * TBW + Ln.blk;
         const uint32_t st = bs_correct<T2>(
-            lds, gfp, s12p, xpm, row, Ln.c, s, true, raw, gblk, wb, nblocks * 255u);
+            lds, gfp, s12p, xpm, row, Ln.c, s, true, raw, gblk, wb, nblocks * 255u PPFS_BS_TR_ARGS);
         if (status && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
             status[gblk] = (uint8_t)st;
         wave_fence(); // corrections patched into the image rows
+        PPFS_BS_MARK(6);
         if (want) {
             uint8_t* dst = data + t * (TBW * K);
 #pragma unroll
@@ -519,6 +554,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
                 asm volatile("" ::: "memory");
             }
         }
+        PPFS_BS_MARK(7);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (nx < nfull) {
             if constexpr (NBUF == 0)
@@ -526,6 +562,10 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
             else
                 dma_wave(base, raw + nx * (TBW * 255), lane, src_off, raw, nblocks * 255u);
         }
+        PPFS_BS_MARK(8);
+#ifdef PPFS_TK_TRACE
+        tr_[9] += 1;
+#endif
     }
     if (t == nfull && nfull < ntiles) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -541,7 +581,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
         const bool valid = Ln.blk < nb;
         const uint64_t gblk = t * TBW + Ln.blk;
         const uint32_t st = bs_correct<T2>(
-            lds, gfp, s12p, xpm, row, Ln.c, s, valid, raw, gblk, wb, nblocks * 255u);
+            lds, gfp, s12p, xpm, row, Ln.c, s, valid, raw, gblk, wb, nblocks * 255u PPFS_BS_TR_ARGS);
         if (status && valid && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
             status[gblk] = (uint8_t)st;
         wave_fence();
@@ -559,6 +599,13 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
             }
         }
     }
+#ifdef PPFS_TK_TRACE
+    tr_[10] = clock64() - t0_;
+    const uint32_t gw = blockIdx.x * NW + wave;
+    if (lane == 0 && gw < 4096)
+        for (int i = 0; i < BS_TRACE_N; ++i)
+            g_bs_trace[gw * BS_TRACE_N + i] = tr_[i];
+#endif
 }
 
 } // namespace bs

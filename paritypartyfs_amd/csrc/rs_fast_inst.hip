@@ -152,6 +152,14 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_server_launch_t, PPFS_T2)(ppfs::SrvBox* b
     return hipGetLastError();
 }
 
+#if defined(PPFS_TK_TRACE) && PPFS_T2 == 32
+// profiling builds: the 2t = 32 decode's per-wave phase sums (rs_bs.hpp g_bs_trace)
+extern "C" hipError_t ppfs_bs_trace_read(void* dst, size_t bytes)
+{
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(bs::g_bs_trace), bytes < sizeof(bs::g_bs_trace) ? bytes : sizeof(bs::g_bs_trace), 0,
+        hipMemcpyDeviceToHost);
+}
+#endif
 #if defined(PPFS_TK_TRACE) && PPFS_T2 <= 8
 // profiling builds: the encode's per-phase cycle sums (rs_wg_tk.hpp g_tk_trace) into host memory
 extern "C" hipError_t PPFS_CAT(ppfs_tk_trace_read_t, PPFS_T2)(void* dst, size_t bytes)
