@@ -341,12 +341,15 @@ __device__ __forceinline__ void put_parity(uint8_t* lds, uint32_t img, const BsL
 // LDS plan: [0, 64 KiB) byte-slice tables | (decode: GF block, S12 table) |
 // NW x NBUF wave images | 64 B slack (the rows' last-word reads and the decode emission's second
 // window run past the last image).  TLDS (decode): 0 = GF block and S12 table in LDS, 1 = the GF
-// block only (S12 read from the global table blob), 2 = neither (both global) -- LDS for more waves.
+// block only (S12 read from the global table blob), 2 = neither (both global) -- LDS for more waves;
+// 3 = GF, S12 and the XPM rows (x^p mod g, 255 x 32 B) in LDS.
 template <int NW, int NBUF, bool DEC, int TLDS = 0> struct BsLds {
-    static constexpr bool GF_IN = DEC && TLDS < 2, S12_IN = DEC && TLDS < 1;
+    static constexpr bool GF_IN = DEC && TLDS != 1 && TLDS != 2, S12_IN = DEC && (TLDS == 0 || TLDS == 3);
+    static constexpr bool XP_IN = DEC && TLDS == 3;
     static constexpr int OFF_GF = TAB_BYTES;
     static constexpr int OFF_S12 = OFF_GF + (GF_IN ? GF_BYTES : 0);
-    static constexpr int OFF_IMG = OFF_S12 + (S12_IN ? 32 * 256 * 2 : 0);
+    static constexpr int OFF_XP = OFF_S12 + (S12_IN ? 32 * 256 * 2 : 0);
+    static constexpr int OFF_IMG = OFF_XP + (XP_IN ? 256 * 32 : 0);
     static constexpr int BYTES = OFF_IMG + NW * (NBUF > 0 ? NBUF : 1) * IMGW + 64;
     static_assert(BYTES <= 163840, "one workgroup per CU: 160 KiB of LDS");
     static_assert(OFF_IMG % 16 == 0 && IMGW % 16 == 0, "aligned images");
@@ -493,6 +496,9 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
     if constexpr (D::S12_IN)
         for (uint32_t p = tid; p < (uint32_t)L::S12_BYTES / 16; p += 64u * NW)
             *(uint4*)(lds + D::OFF_S12 + 16 * p) = *(const uint4*)(tables + L::OFF_S12 + 16 * p);
+    if constexpr (D::XP_IN)
+        for (uint32_t p = tid; p < 255u * 2u; p += 64u * NW)
+            *(uint4*)(lds + D::OFF_XP + 16 * p) = *(const uint4*)(tables + L::OFF_XPM + 16 * p);
     __syncthreads();
 #ifdef PPFS_TK_TRACE
     uint64_t tr_[BS_TRACE_N] = {};
@@ -506,7 +512,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
     const uint32_t img = D::OFF_IMG + wave * (uint32_t)IMGW;
     const uint32_t base = __builtin_amdgcn_readfirstlane(lds_addr(lds + img));
     const uint32_t row = img + 255u * Ln.blk;
-    const uint8_t* const xpm = tables + L::OFF_XPM;
+    const uint8_t* const xpm = D::XP_IN ? lds + D::OFF_XP : tables + L::OFF_XPM;
     const uint64_t nfull = nblocks / TBW, ntiles = (nblocks + TBW - 1) / TBW;
     const uint64_t S = (uint64_t)gridDim.x * NW;
     uint64_t t = (uint64_t)blockIdx.x * NW + wave;
