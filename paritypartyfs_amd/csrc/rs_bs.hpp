@@ -57,6 +57,10 @@ __device__ uint64_t g_bs_trace[4096 * BS_TRACE_N];
 #define PPFS_BS_TR_ARGS
 #endif
 
+#ifndef PPFS_BS_EMIT_G
+#define PPFS_BS_EMIT_G 1 // decode emission: output pieces read from LDS together
+#endif
+
 constexpr int TBW = 32;            // blocks per wave tile
 constexpr int IMGW = TBW * 255;    // 8,160 B: one wave tile's codeword image
 constexpr int IMG_PIECES = IMGW / 16; // 510 16-byte pieces in and out
@@ -551,12 +555,23 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
         PPFS_BS_MARK(6);
         if (want) {
             uint8_t* dst = data + t * (TBW * K);
+            // PPFS_BS_EMIT_G pieces per group: their LDS reads in flight together, then their stores
 #pragma unroll
-            for (int k = 0; k < KO; ++k) {
-                uint32_t p = lane + 64u * (uint32_t)k;
-                asm volatile("" : "+v"(p)); // one piece live at a time
-                if (((k + 1) * 64 <= OUT_PIECES || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, data, nblocks * K))
-                    st_nt<NTST>(dst + 16u * p, pair::pair_dec_piece<T2>(lds, img - pair::PAD, p));
+            for (int k0 = 0; k0 < KO; k0 += PPFS_BS_EMIT_G) {
+                uint4 v[PPFS_BS_EMIT_G];
+#pragma unroll
+                for (int g = 0; g < PPFS_BS_EMIT_G && k0 + g < KO; ++g) {
+                    uint32_t p = lane + 64u * (uint32_t)(k0 + g);
+                    asm volatile("" : "+v"(p));
+                    v[g] = pair::pair_dec_piece<T2>(lds, img - pair::PAD, p);
+                }
+#pragma unroll
+                for (int g = 0; g < PPFS_BS_EMIT_G && k0 + g < KO; ++g) {
+                    const int k = k0 + g;
+                    const uint32_t p = lane + 64u * (uint32_t)k;
+                    if (((k + 1) * 64 <= OUT_PIECES || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, data, nblocks * K))
+                        st_nt<NTST>(dst + 16u * p, v[g]);
+                }
                 asm volatile("" ::: "memory");
             }
         }
