@@ -57,6 +57,12 @@ __device__ uint64_t g_bs_trace[4096 * BS_TRACE_N];
 #define PPFS_BS_TR_ARGS
 #endif
 
+#ifndef PPFS_BS_LOGCHK
+#define PPFS_BS_LOGCHK 0 // decode: single-error confirmation in the log domain
+#endif
+#ifndef PPFS_BS_DEC_IDMA
+#define PPFS_BS_DEC_IDMA 0 // decode: next tile's DMA interleaved with the emission rounds
+#endif
 #ifndef PPFS_BS_EMIT_G
 #define PPFS_BS_EMIT_G 1 // decode emission: output pieces read from LDS together
 #endif
@@ -256,6 +262,14 @@ __device__ __forceinline__ uint32_t bs_correct(uint8_t* lds, const uint8_t* gfp,
         return 0u;
     const Gf gf { gfp };
     const uint16_t* t = (const uint16_t*)(s12p + 8192u * c); // state byte u = 16c + k
+#if PPFS_BS_LOGCHK
+    // LOG of the lane's 16 state bytes, issued beside the S12 lookups (independent of S1, S2): the
+    // confirmation below then compares logs, with no lookup after the XP row arrives
+    uint32_t lr[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        lr[k] = gf.log((s[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+#endif
     uint32_t s12 = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k)
@@ -275,8 +289,16 @@ __device__ __forceinline__ uint32_t bs_correct(uint8_t* lds, const uint8_t* gfp,
     for (int k = 0; k < 16; ++k) {
         const uint32_t x = (xw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
         const uint32_t rb = (s[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+#if PPFS_BS_LOGCHK
+        // rb == e alpha^(log x) <=> (x zero and rb zero) or (rb nonzero and log rb == le + x mod 255)
+        uint32_t lsum = le + x;
+        lsum = lsum >= 255u ? lsum - 255u : lsum;
+        const bool ok = x == 0xFFu ? rb == 0u : (rb != 0u && lr[k] == lsum);
+        bad |= ok ? 0u : 1u;
+#else
         const uint32_t ev = x == 0xFFu ? 0u : gf.exp(le + x);
         bad |= ev != rb ? 1u : 0u;
+#endif
     }
     const bool geo = err && pair::pair_or<1>(bad) == 0u;
     PPFS_BS_MARK(4);
@@ -302,6 +324,29 @@ __device__ __forceinline__ void dma_wave(uint32_t img_base, const uint8_t* __res
             dma16(src + so, __builtin_amdgcn_readfirstlane(img_base + 1024u * (uint32_t)k));
     }
 }
+
+// One wave-instruction k of dma_wave (image pieces lane + 64 k)
+template <typename F>
+__device__ __forceinline__ void dma_wave_k(uint32_t img_base, const uint8_t* __restrict__ src, uint32_t lane, F src_off,
+    int k, [[maybe_unused]] const uint8_t* gbase, [[maybe_unused]] uint64_t extent)
+{
+    const uint32_t i = lane + 64u * (uint32_t)k;
+    const int so = src_off(i);
+    if (((k + 1) * 64 <= IMG_PIECES || i < (uint32_t)IMG_PIECES) && so >= 0 && PPFS_DBG_OK(src + so, 16, gbase, extent))
+        dma16(src + so, __builtin_amdgcn_readfirstlane(img_base + 1024u * (uint32_t)k));
+}
+
+// Decode emission of 2t = 32 (pair_dec_piece: payload piece p of the tile reads image bytes
+// [16 p + 32 (b + 1), +48), b = 16 p / 223): the lowest image byte that output round k (pieces
+// 64 k .. 64 k + 63) reads, and so the number of tile DMA instructions (1 KiB image windows) that
+// may be issued for the NEXT tile once rounds 0..k have read the image
+constexpr int bs_emit_minread(int k) { return 1024 * k + 32 * ((1024 * k) / 223 + 1); }
+constexpr int bs_dma_free_after(int k, int ko)
+{
+    return k + 1 >= ko ? KP : (bs_emit_minread(k + 1) / 1024 < KP ? bs_emit_minread(k + 1) / 1024 : KP);
+}
+static_assert(bs_dma_free_after(0, 7) == 1 && bs_dma_free_after(5, 7) == 6 && bs_dma_free_after(6, 7) == KP,
+    "one DMA window per emission round, the last two after the last round");
 
 // Register prefetch of a wave tile (NBUF = 0): piece i = lane + 64 k into pf[k] with plain
 // 16-byte loads (compiler-counted), written into the image once the previous tile's emission has
@@ -553,6 +598,10 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
             status[gblk] = (uint8_t)st;
         wave_fence(); // corrections patched into the image rows
         PPFS_BS_MARK(6);
+        // PPFS_BS_DEC_IDMA (NBUF = 1): the next tile's DMA windows go out between the emission's
+        // rounds as soon as no later round reads them, so the DMA flies while the wave emits
+        const bool idma = PPFS_BS_DEC_IDMA && NBUF == 1 && want && nx < nfull;
+        int dma_done = 0;
         if (want) {
             uint8_t* dst = data + t * (TBW * K);
             // PPFS_BS_EMIT_G pieces per group: their LDS reads in flight together, then their stores
@@ -573,11 +622,19 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
                         st_nt<NTST>(dst + 16u * p, v[g]);
                 }
                 asm volatile("" ::: "memory");
+                if (idma) { // the stores consumed the group's LDS reads
+                    const int kl = k0 + PPFS_BS_EMIT_G < KO ? k0 + PPFS_BS_EMIT_G - 1 : KO - 1;
+#pragma unroll
+                    for (int j = 0; j < KP; ++j)
+                        if (j >= dma_done && j < bs_dma_free_after(kl, KO))
+                            dma_wave_k(base, raw + nx * (TBW * 255), lane, src_off, j, raw, nblocks * 255u);
+                    dma_done = bs_dma_free_after(kl, KO);
+                }
             }
         }
         PPFS_BS_MARK(7);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (nx < nfull) {
+        if (nx < nfull && !idma) {
             if constexpr (NBUF == 0)
                 put_wave(lds, img, pf, lane, src_off);
             else
