@@ -70,11 +70,11 @@ __device__ __forceinline__ void vm_wait_exact(uint32_t n)
 // Wave 0 (64 lanes) copies the first BYTES of the table blob into LDS at 0 by LDS-DMA: no register
 // round trip, and its loads never share a queue with the DMA waves' tiles.  Caller: vmcnt(0).
 template <int BYTES>
-__device__ __forceinline__ void dma_tables_w0(uint8_t* lds, const uint8_t* __restrict__ tables, uint32_t lane)
+__device__ __forceinline__ void dma_tables_w0(uint8_t* dst, const uint8_t* __restrict__ tables, uint32_t lane)
 {
     static_assert(BYTES % 16 == 0, "16-byte pieces");
     constexpr int NP = BYTES / 16, KI = (NP + 63) / 64;
-    const uint32_t lbase = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+    const uint32_t lbase = __builtin_amdgcn_readfirstlane(lds_addr(dst));
 #pragma unroll
     for (int k = 0; k < KI; ++k) {
         const uint32_t p = lane + 64u * (uint32_t)k;
@@ -139,6 +139,9 @@ __device__ uint64_t g_tk_trace_dec[4096 * 2 * TK_TRACE_N];
 #define PPFS_TK_MARK(i) ((void)0)
 #endif
 
+#ifndef PPFS_ENC_ILP2
+#define PPFS_ENC_ILP2 0 // 1: remainder as two 32-byte chains per lane (phase_remainder NMAP = 7)
+#endif
 template <int T2, int WPC = 2, int NTST = 1>
 __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t* __restrict__ data,
     uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables, uint32_t* __restrict__ ctr,
@@ -146,7 +149,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
 {
     constexpr int NBUF = 3;
     using L = RsWgLayout<T2>;
-    using D = Lds<T2, false, NBUF, false>;
+    using D = Lds<T2, false, NBUF, false, PPFS_ENC_ILP2 ? 7 : 0>;
     constexpr int BUF = D::BUFB;
     constexpr int LDS_ALLOC = lds_alloc<D::BYTES + 64, WPC>();
     static_assert(WPC * LDS_ALLOC <= 163840, "LDS for WPC workgroups per CU");
@@ -179,7 +182,12 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
             dma_tile192<IN_PIECES>(lds + D::OFF_BUF + BUF + PAD, data + q1 * (TB * K), tid, data, nblocks * K);
         hist = go ? 1u : 0u;
     } else {
-        dma_tables_w0<D::TBL>(lds, tables, lane);
+        if constexpr (D::NMAP == 7) { // SL, then MAP32 in the place of MAP
+            dma_tables_w0<L::OFF_MAP>(lds, tables, lane);
+            dma_tables_w0<7 * L::MAP_STRIDE>(lds + L::OFF_MAP, tables + L::OFF_MAP32, lane);
+        } else {
+            dma_tables_w0<D::TBL>(lds, tables, lane);
+        }
         *(uint64_t*)(lds + D::OFF_PAR + 8u * lane) = 0; // both parity slot sets (2 x 64 x 8 B)
         *(uint64_t*)(lds + D::OFF_PAR + 512u + 8u * lane) = 0;
         if (tk_lane) {

@@ -13,7 +13,7 @@ if [ -n "$AB" ]; then
   VARIANTS="$AB" timeout -k 10 900 bash tools/ab_bench.sh ${TAG}_ab $ABARGS > gpurun_out/${TAG}_ab.txt 2>&1 || { tail gpurun_out/${TAG}_ab.txt; exit 1; }
   cat gpurun_out/${TAG}_ab.txt
 fi
-for TR in trace trace64; do
+for TR in trace trace0; do
   [ -f paritypartyfs_amd/_lib/alt/libppfs_ecc_$TR.so ] || continue
   PPFS_ECC_LIB=$PWD/paritypartyfs_amd/_lib/alt/libppfs_ecc_$TR.so timeout -k 10 120 python tools/tk_trace.py > gpurun_out/${TAG}_$TR.jsonl 2>/dev/null || { tail gpurun_out/${TAG}_$TR.jsonl; exit 1; }
   python3 -c "
