@@ -18,7 +18,11 @@ namespace ppfs {
 
 enum : uint32_t { SRV_ENCODE = 0, SRV_DECODE = 1, SRV_WRITE = 2 };
 constexpr uint32_t SRV_EXITED = 0x80000000u;
-constexpr uint64_t SRV_LIFETIME_US = 1000000; // one launch serves at most 1 s
+// One launch serves at most 20 ms.  HIP maps a process's streams onto GPU_MAX_HW_QUEUES (4) hardware
+// queues, so another stream (another context's, the caller's) can sit behind the resident launch on
+// its queue: the lifetime bounds that wait (round 3: 1 s stalled a second context's creation and
+// first copies for seconds while the first one served per-block calls).  A relaunch costs ~10 us.
+constexpr uint64_t SRV_LIFETIME_US = 20000;
 constexpr uint32_t SRV_MAX_BLOCKS = 64;
 
 // cmd word: bits 0-6 block count (1..64), 12-13 op, 14 write-back, 15 want data, 16-31 sequence
