@@ -256,6 +256,13 @@ template <int T2> std::vector<uint8_t> build_rs_wg_tables_t()
                 for (int v = 0; v < 16; ++v)
                     put(L::OFF_MAP32 + m * L::MAP_STRIDE, 2 * q + h, v, xq, (uint8_t)(v << (4 * h)));
         }
+    for (int m = 1; m <= 3; ++m)
+        for (int i = 0; i < 8; ++i) {
+            const std::vector<uint8_t> xi = rs_xpow_mod(T2 + i + 64 * m, g, T2);
+            for (int h = 0; h < 2; ++h)
+                for (int v = 0; v < 16; ++v)
+                    put(L::OFF_SLX + (m - 1) * 16 * L::TBL, 2 * i + h, v, xi, (uint8_t)(v << (4 * h)));
+        }
     for (int q = 0; q < T2; ++q)
         for (int h = 0; h < 2; ++h)
             for (int v = 0; v < 16; ++v)

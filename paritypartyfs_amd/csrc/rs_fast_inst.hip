@@ -11,6 +11,7 @@
 #include "rs_wg_tk.hpp"
 #include "rs_pair.hpp"
 #include "rs_bs.hpp"
+#include "rs_wq.hpp"
 
 #ifndef PPFS_T2
 #error "compile with -DPPFS_T2=<2t>"
@@ -54,6 +55,14 @@ static uint32_t rs_tile_grid(uint64_t nb, int wpc, int tb = 64)
 constexpr int fit_wpc(int bytes, int most) { return 163840 / bytes < most ? 163840 / bytes : most; }
 constexpr int ENC_NBUF = 3, ENC_WPC = 2, DEC_NBUF = 2, DEC_WPC = 3;
 constexpr int ENC_WPC_STATIC = fit_wpc(wg::lds_bytes<PPFS_T2, false, ENC_NBUF>(), 4);
+// PPFS_WG_WQ (round 3): the barrier-free wave-quarter encode (rs_wq.hpp) for every launch
+#ifndef PPFS_WG_WQ
+#define PPFS_WG_WQ 0
+#endif
+#ifndef PPFS_WQ_NBUF
+#define PPFS_WQ_NBUF 3
+#endif
+constexpr int WQ_NBUF = PPFS_WQ_NBUF, WQ_WPC = PPFS_WQ_NBUF >= 3 ? 2 : 3;
 #elif PPFS_T2 == 32
 // 2t = 32 (rs_bs.hpp): one workgroup per CU, every wave on its own 32-block tiles;
 // encode 12 waves (3 per SIMD), decode 8 (LDS- and register-bound)
@@ -84,7 +93,10 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
     const uint8_t* tab, hipStream_t s, [[maybe_unused]] uint32_t* ctr, [[maybe_unused]] uint32_t* ctr_clear)
 {
 #if PPFS_T2 <= 8
-    if (ctr && ctr_clear)
+    if (PPFS_WG_WQ)
+        hipLaunchKernelGGL((wq::rs_wq_encode_kernel<PPFS_T2, WQ_WPC, WQ_NBUF, 1>), dim3(rs_tile_grid(nb, WQ_WPC, 4 * wq::QB)),
+            dim3(256), 0, s, d, r, nb, tab);
+    else if (ctr && ctr_clear)
         hipLaunchKernelGGL((wg::rs_wg_encode_tk_kernel<PPFS_T2, ENC_WPC, 1>), dim3(rs_tile_grid(nb, ENC_WPC)), dim3(256), 0, s,
             d, r, nb, tab, ctr, ctr_clear);
     else

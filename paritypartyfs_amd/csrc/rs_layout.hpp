@@ -34,7 +34,12 @@ template <int T2> struct RsWgLayout {
     // CTR: zeroed tile-ticket counters of the dynamic-tile kernels (rs_wg.hpp): encode at +0,
     // decode at +2048; in each, 8 counters (one per XCD) and the workgroups-done count, one
     // 128-byte line each.  Each launch leaves them at zero.
-    static constexpr int OFF_CTR = OFF_MAP32 + 7 * MAP_STRIDE;
+    // SLX (round 3): the slicing tables of segment m = 1..3 with x^(64 m) folded in, 16 nibble
+    // tables each: table 2i+h, value v -> (v << 4h) * x^(2t+i+64m) mod g, read by the LAST slicing
+    // step of segment m, which then needs no x^(64 m) map (rs_wg.hpp seg_remainder)
+    static constexpr int OFF_SLX = OFF_MAP32 + 7 * MAP_STRIDE;
+    static constexpr int SLX_BYTES = 3 * 16 * TBL;
+    static constexpr int OFF_CTR = OFF_SLX + SLX_BYTES;
     static constexpr int CTR_BYTES = 4096;
     static constexpr int BLOB_BYTES = OFF_CTR + CTR_BYTES;
     static_assert(TABLE_BYTES % 16 == 0 && BLOB_BYTES % 16 == 0, "tables are copied in 16-byte pieces");
@@ -42,7 +47,7 @@ template <int T2> struct RsWgLayout {
 
 constexpr int rs_wg_table_bytes(int t2)
 {
-    return 16 * 128 + 3 * 2 * t2 * 128 + 2 * t2 * 128 + GF_BYTES + 7 * 2 * t2 * 128 + 4096;
+    return 16 * 128 + 3 * 2 * t2 * 128 + 2 * t2 * 128 + GF_BYTES + 7 * 2 * t2 * 128 + 3 * 16 * 128 + 4096;
 }
 
 // Pair RS path (rs_pair.hpp), 16 < 2t <= 32: the same 32-byte top-aligned state, two lanes per

@@ -50,7 +50,7 @@ __device__ __forceinline__ void dma_tile192(uint8_t* dst, const uint8_t* __restr
     }
 }
 
-// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 15] (exact: the counts below are known per wave)
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 31] (exact: the counts below are known per wave)
 __device__ __forceinline__ void vm_wait_exact(uint32_t n)
 {
     switch (__builtin_amdgcn_readfirstlane(n)) {
@@ -60,6 +60,8 @@ __device__ __forceinline__ void vm_wait_exact(uint32_t n)
         break;
         PPFS_VMW(1) PPFS_VMW(2) PPFS_VMW(3) PPFS_VMW(4) PPFS_VMW(5) PPFS_VMW(6) PPFS_VMW(7) PPFS_VMW(8)
         PPFS_VMW(9) PPFS_VMW(10) PPFS_VMW(11) PPFS_VMW(12) PPFS_VMW(13) PPFS_VMW(14) PPFS_VMW(15)
+        PPFS_VMW(16) PPFS_VMW(17) PPFS_VMW(18) PPFS_VMW(19) PPFS_VMW(20) PPFS_VMW(21) PPFS_VMW(22) PPFS_VMW(23)
+        PPFS_VMW(24) PPFS_VMW(25) PPFS_VMW(26) PPFS_VMW(27) PPFS_VMW(28) PPFS_VMW(29) PPFS_VMW(30) PPFS_VMW(31)
 #undef PPFS_VMW
     default:
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -142,6 +144,9 @@ __device__ uint64_t g_tk_trace_dec[4096 * 2 * TK_TRACE_N];
 #ifndef PPFS_ENC_ILP2
 #define PPFS_ENC_ILP2 0 // 1: remainder as two 32-byte chains per lane (phase_remainder NMAP = 7)
 #endif
+#ifndef PPFS_WG_SLX
+#define PPFS_WG_SLX 0 // 1: SLX last-step tables instead of the x^(64 s) maps (rs_wg.hpp seg_remainder)
+#endif
 template <int T2, int WPC = 2, int NTST = 1>
 __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t* __restrict__ data,
     uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables, uint32_t* __restrict__ ctr,
@@ -149,7 +154,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
 {
     constexpr int NBUF = 3;
     using L = RsWgLayout<T2>;
-    using D = Lds<T2, false, NBUF, false, PPFS_ENC_ILP2 ? 7 : 0>;
+    using D = Lds<T2, false, NBUF, false, PPFS_ENC_ILP2 ? 7 : PPFS_WG_SLX ? 1 : 0>;
     constexpr int BUF = D::BUFB;
     constexpr int LDS_ALLOC = lds_alloc<D::BYTES + 64, WPC>();
     static_assert(WPC * LDS_ALLOC <= 163840, "LDS for WPC workgroups per CU");
@@ -185,6 +190,9 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
         if constexpr (D::NMAP == 7) { // SL, then MAP32 in the place of MAP
             dma_tables_w0<L::OFF_MAP>(lds, tables, lane);
             dma_tables_w0<7 * L::MAP_STRIDE>(lds + L::OFF_MAP, tables + L::OFF_MAP32, lane);
+        } else if constexpr (D::NMAP == 1) { // SL, then SLX in the place of MAP
+            dma_tables_w0<L::OFF_MAP>(lds, tables, lane);
+            dma_tables_w0<L::SLX_BYTES>(lds + D::OFF_SLX, tables + L::OFF_SLX, lane);
         } else {
             dma_tables_w0<D::TBL>(lds, tables, lane);
         }
@@ -225,7 +233,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
         PPFS_TK_MARK(1);
         if (wave == 0)
             *(uint64_t*)(lds + D::OFF_PAR + (pc ^ 1u) * 512u + 8u * lane) = 0;
-        phase_remainder<T2, K, D::NMAP>(lds, buf, par, wave, row);
+        phase_remainder<T2, K, D::NMAP, D::OFF_SLX>(lds, buf, par, wave, row);
         PPFS_TK_MARK(2);
         barrier_lds(); // B: parity slots complete
         PPFS_TK_MARK(3);
@@ -262,7 +270,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
         if (PPFS_DBG_OK(data + t * (TB * K), nb * K, data, nblocks * K))
             stage_bytes(lds + buf + PAD, data + t * (TB * K), nb * K, tid);
         barrier_lds();
-        phase_remainder<T2, K, D::NMAP>(lds, buf, par, wave, row);
+        phase_remainder<T2, K, D::NMAP, D::OFF_SLX>(lds, buf, par, wave, row);
         barrier_lds();
         uint8_t* dst = raw + t * (TB * 255);
         const uint32_t nout = nb * 255u;
@@ -301,7 +309,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
 {
     constexpr int NBUF = 2;
     using L = RsWgLayout<T2>;
-    using D = Lds<T2, true, NBUF>;
+    using D = Lds<T2, true, NBUF, false, PPFS_WG_SLX ? 1 : 0>;
     constexpr int LDS_ALLOC = lds_alloc<D::BYTES + 64, WPC>();
     static_assert(WPC * LDS_ALLOC <= 163840, "LDS for WPC workgroups per CU");
     constexpr int K = L::K;
@@ -327,7 +335,12 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         if (q0 < nfull)
             dma_tile192<IN_PIECES>(lds + D::OFF_BUF + PAD, raw + q0 * (TB * 255), tid, raw, nblocks * 255u);
     } else {
-        dma_tables_w0<D::TBL>(lds, tables, lane);
+        if constexpr (D::NMAP == 1) { // the decode tables, then SLX after them
+            dma_tables_w0<L::TABLE_BYTES>(lds, tables, lane);
+            dma_tables_w0<L::SLX_BYTES>(lds + D::OFF_SLX, tables + L::OFF_SLX, lane);
+        } else {
+            dma_tables_w0<D::TBL>(lds, tables, lane);
+        }
         *(uint64_t*)(lds + D::OFF_PAR + 8u * lane) = 0;
         *(uint64_t*)(lds + D::OFF_PAR + 512u + 8u * lane) = 0;
         if (tk_lane) {
@@ -356,7 +369,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         PPFS_TK_MARK(1);
         if (wave == 0)
             *(uint64_t*)(lds + D::OFF_PAR + (pc ^ 1u) * 512u + 8u * lane) = 0;
-        phase_remainder<T2, 255>(lds, buf, par, wave, row);
+        phase_remainder<T2, 255, D::NMAP, D::OFF_SLX>(lds, buf, par, wave, row);
         PPFS_TK_MARK(2);
         barrier_lds(); // B: remainders complete
         PPFS_TK_MARK(3);
@@ -401,7 +414,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         if (PPFS_DBG_OK(raw + t * (TB * 255), nb * 255u, raw, nblocks * 255u))
             stage_bytes(lds + buf + PAD, raw + t * (TB * 255), nb * 255u, tid);
         barrier_lds();
-        phase_remainder<T2, 255>(lds, buf, par, wave, row);
+        phase_remainder<T2, 255, D::NMAP, D::OFF_SLX>(lds, buf, par, wave, row);
         barrier_lds();
         if (wave == 0) {
             const bool valid = row < nb;

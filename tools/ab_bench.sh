@@ -4,7 +4,7 @@
 set -o pipefail
 TAG=$1; shift
 mkdir -p gpurun_out
-for r in 1 2; do
+for r in $(seq 1 ${ROUNDS:-2}); do
 for v in new ${VARIANTS}; do
   if [ $v = new ]; then L=$PWD/paritypartyfs_amd/_lib/libppfs_ecc.so; else L=$PWD/paritypartyfs_amd/_lib/alt/libppfs_ecc_$v.so; fi
   PPFS_ECC_LIB=$L timeout -k 10 150 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive --no-configs \
