@@ -486,7 +486,7 @@ struct ppfs_ecc_ctx {
     // launch of the same kind on the stream used (launches on one stream are ordered; no two streams
     // share a slot); tk_par = the set the next launch of each kind uses.  Further streams use the
     // static walk.
-    static constexpr int kTkSlots = 16, kTkSetWords = 640; // encode 320 words, decode 320
+    static constexpr int kTkSlots = 16, kTkSetWords = 1024; // encode 512 words (rs_wq: 32 counters 64 B apart), decode 512
     uint32_t* d_ctr = nullptr;
     hipStream_t tk_stream[kTkSlots] = {};
     uint8_t tk_par[kTkSlots][2] = {};

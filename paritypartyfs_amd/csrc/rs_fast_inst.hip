@@ -11,7 +11,6 @@
 #include "rs_wg_tk.hpp"
 #include "rs_pair.hpp"
 #include "rs_bs.hpp"
-#include "rs_wq.hpp"
 
 #ifndef PPFS_T2
 #error "compile with -DPPFS_T2=<2t>"
@@ -55,14 +54,6 @@ static uint32_t rs_tile_grid(uint64_t nb, int wpc, int tb = 64)
 constexpr int fit_wpc(int bytes, int most) { return 163840 / bytes < most ? 163840 / bytes : most; }
 constexpr int ENC_NBUF = 3, ENC_WPC = 2, DEC_NBUF = 2, DEC_WPC = 3;
 constexpr int ENC_WPC_STATIC = fit_wpc(wg::lds_bytes<PPFS_T2, false, ENC_NBUF>(), 4);
-// PPFS_WG_WQ (round 3): the barrier-free wave-quarter encode (rs_wq.hpp) for every launch
-#ifndef PPFS_WG_WQ
-#define PPFS_WG_WQ 0
-#endif
-#ifndef PPFS_WQ_NBUF
-#define PPFS_WQ_NBUF 3
-#endif
-constexpr int WQ_NBUF = PPFS_WQ_NBUF, WQ_WPC = PPFS_WQ_NBUF >= 3 ? 2 : 3;
 #elif PPFS_T2 == 32
 // 2t = 32 (rs_bs.hpp): one workgroup per CU, every wave on its own 32-block tiles;
 // encode 12 waves (3 per SIMD), decode 8 (LDS- and register-bound)
@@ -70,9 +61,12 @@ constexpr int WQ_NBUF = PPFS_WQ_NBUF, WQ_WPC = PPFS_WQ_NBUF >= 3 ? 2 : 3;
 #define PPFS_BS_DEC_NW 8
 #endif
 #ifndef PPFS_BS_DEC_TLDS
-#define PPFS_BS_DEC_TLDS 0
+#define PPFS_BS_DEC_TLDS 3 // round 3: XP rows in LDS (with the register prefetch: 139 -> 130 us in the cfg5 step)
 #endif
-constexpr int BS_ENC_NW = 12, BS_DEC_NW = PPFS_BS_DEC_NW, BS_DEC_TLDS = PPFS_BS_DEC_TLDS;
+#ifndef PPFS_BS_DEC_NBUF
+#define PPFS_BS_DEC_NBUF 0 // register prefetch of the next tile (rs_bs.hpp load_wave); 1 = single LDS image
+#endif
+constexpr int BS_ENC_NW = 12, BS_DEC_NW = PPFS_BS_DEC_NW, BS_DEC_TLDS = PPFS_BS_DEC_TLDS, BS_DEC_NBUF = PPFS_BS_DEC_NBUF;
 #else
 // 8 < 2t <= 16: rs_fast.hpp lane-per-block kernels; 2t = 16 encodes with the solo image kernel
 constexpr bool SOLO_IMG = PPFS_T2 == 16;
@@ -93,10 +87,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
     const uint8_t* tab, hipStream_t s, [[maybe_unused]] uint32_t* ctr, [[maybe_unused]] uint32_t* ctr_clear)
 {
 #if PPFS_T2 <= 8
-    if (PPFS_WG_WQ)
-        hipLaunchKernelGGL((wq::rs_wq_encode_kernel<PPFS_T2, WQ_WPC, WQ_NBUF, 1>), dim3(rs_tile_grid(nb, WQ_WPC, 4 * wq::QB)),
-            dim3(256), 0, s, d, r, nb, tab);
-    else if (ctr && ctr_clear)
+    if (ctr && ctr_clear)
         hipLaunchKernelGGL((wg::rs_wg_encode_tk_kernel<PPFS_T2, ENC_WPC, 1>), dim3(rs_tile_grid(nb, ENC_WPC)), dim3(256), 0, s,
             d, r, nb, tab, ctr, ctr_clear);
     else
@@ -139,7 +130,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
         hipLaunchKernelGGL((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC, 7, 1>), dim3(rs_tile_grid(nb, DEC_WPC)),
             dim3(256), 0, s, r, d, st, nb, tab, wb);
 #elif PPFS_T2 == 32
-    hipLaunchKernelGGL((bs::rs_bs_decode_kernel<PPFS_T2, BS_DEC_NW, 1, 1, BS_DEC_TLDS>), dim3(rs_tile_grid(nb, 1, bs::TBW * BS_DEC_NW)),
+    hipLaunchKernelGGL((bs::rs_bs_decode_kernel<PPFS_T2, BS_DEC_NW, BS_DEC_NBUF, 1, BS_DEC_TLDS>), dim3(rs_tile_grid(nb, 1, bs::TBW * BS_DEC_NW)),
         dim3(64 * BS_DEC_NW), 0, s, r, d, st, nb, tab, wb);
 #else
     hipLaunchKernelGGL(rs255_decode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, r, d, st, nb, tab, wb);

@@ -145,7 +145,7 @@ __device__ uint64_t g_tk_trace_dec[4096 * 2 * TK_TRACE_N];
 #define PPFS_ENC_ILP2 0 // 1: remainder as two 32-byte chains per lane (phase_remainder NMAP = 7)
 #endif
 #ifndef PPFS_WG_SLX
-#define PPFS_WG_SLX 0 // 1: SLX last-step tables instead of the x^(64 s) maps (rs_wg.hpp seg_remainder)
+#define PPFS_WG_SLX 1 // SLX last-step tables instead of the x^(64 s) maps (rs_wg.hpp seg_remainder); 0 = maps
 #endif
 template <int T2, int WPC = 2, int NTST = 1>
 __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t* __restrict__ data,

@@ -137,6 +137,17 @@ constexpr int DEC_NBUF = DEC_FULL ? 0 : PPFS_WG_DEC_NBUF;
 #if PPFS_WG_ENC_W8 || PPFS_WG_DYN
 #include "rs_wg_ablate.hpp"
 #endif
+// round 3: the barrier-free wave-quarter encode (rs_wq.hpp): PPFS_WG_WQ = 1 static walk of 16-block
+// wave tiles (ring PPFS_WQ_NBUF), 2 = per-wave ticket counters (ring of 3)
+#ifndef PPFS_WG_WQ
+#define PPFS_WG_WQ 0
+#endif
+#ifndef PPFS_WQ_NBUF
+#define PPFS_WQ_NBUF 3
+#endif
+#if PPFS_T2 <= 8
+#include "rs_wq.hpp"
+#endif
 // wave-independent kernels (rs_w1.hpp): one workgroup of PPFS_W1_NW waves per CU, every wave on
 // its own 64-block tiles; PPFS_W1_NBUF 1 = LDS-DMA, 0 = register prefetch
 #ifndef PPFS_WG_W1
@@ -260,7 +271,13 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
             s, d, r, nb, tab, ctr);
     else
 #endif
-    if ((PPFS_WG_TK & 1) && ctr && PPFS_ENC_MODE == 3 && !WG_FULL && !PPFS_WG_ENC_IMG && !(PPFS_WG_W1 & 1))
+    if (PPFS_WG_WQ == 2 && ctr && ctr_clear)
+        hipLaunchKernelGGL((wq::rs_wq_encode_kernel<PPFS_T2, 2, 3, 1, true>), dim3(rs_tile_grid(nb, 2, 4 * wq::QB)), dim3(256), 0,
+            s, d, r, nb, tab, ctr, ctr_clear);
+    else if (PPFS_WG_WQ)
+        hipLaunchKernelGGL((wq::rs_wq_encode_kernel<PPFS_T2, PPFS_WQ_NBUF >= 3 ? 2 : 3, PPFS_WQ_NBUF, 1>),
+            dim3(rs_tile_grid(nb, PPFS_WQ_NBUF >= 3 ? 2 : 3, 4 * wq::QB)), dim3(256), 0, s, d, r, nb, tab, nullptr, nullptr);
+    else if ((PPFS_WG_TK & 1) && ctr && PPFS_ENC_MODE == 3 && !WG_FULL && !PPFS_WG_ENC_IMG && !(PPFS_WG_W1 & 1))
         hipLaunchKernelGGL((wg::rs_wg_encode_tk_kernel<PPFS_T2, 2, PPFS_ENC_NTST>), dim3(rs_tile_grid(nb, 2)), dim3(256), 0, s, d,
             r, nb, tab, ctr, ctr_clear);
     else if constexpr (PPFS_WG_W1 & 1)

@@ -1,5 +1,9 @@
 #pragma once
-// rs_wq.hpp -- barrier-free t <= 4 RS encode for gfx950 ("wave quarters", round 3).
+// rs_wq.hpp -- barrier-free t <= 4 RS encode for gfx950 ("wave quarters", round 3).  ABLATION, not
+// shipped: correct (94 RS GPU tests, bounds-checked build clean) and 5-8 % faster cache-hot, but
+// 10-12 % slower from HBM and in the bench step than the ticket encode (static walk), 25 % slower
+// with per-wave tickets (65,536 atomics per launch); profiles/r3k_*, r3m_slx_wq_bench_ab.txt.
+// Built by tools/build_alt.sh <name> -DPPFS_WG_WQ=1|2.
 //
 // Reference semantics: lib/blockdevice/src/rs_block_device.cpp _encodeBlock :95-117 (see rs_wg.hpp).
 //
@@ -97,6 +101,19 @@ __device__ __forceinline__ void wq_remainder(uint32_t (&s)[2], const uint8_t* ld
     }
 }
 
+// Ticket atomic issued from inline asm (lane 0; returns the old value): the compiler does not track
+// it, so it never inserts its own (draining) wait for the result.  The caller guarantees completion
+// with its counted vmcnt before the value is read, then ties the register (tk_ready).
+__device__ __forceinline__ void tk_take(uint32_t& tk, uint32_t* ctr)
+{
+    asm volatile("global_atomic_inc %0, %1, %2, off sc0" : "=v"(tk) : "v"(ctr), "v"(0xFFFFFFFFu) : "memory");
+}
+__device__ __forceinline__ uint32_t tk_ready(uint32_t& tk)
+{
+    asm volatile("" : "+v"(tk)); // ordered after the caller's volatile wait: no read of tk moves above it
+    return (uint32_t)__builtin_amdgcn_readfirstlane(tk);
+}
+
 // XOR over the 4 lanes of a quad (the four segments of one block): every lane gets the total
 __device__ __forceinline__ uint32_t quad_xor(uint32_t v)
 {
@@ -154,11 +171,24 @@ template <int NBUF> struct VmRing {
     }
 };
 
-template <int T2, int WPC = 2, int NBUF = 3, int NTST = 1>
+// TK: wave tiles come from ticket counters (rs_wg_tk.hpp's scheme at wave granularity): 32
+// counters, one per (XCD, wave slot), 64 B apart in the stream's set; local ticket k of counter
+// (x, w) is wave tile 4 (k nx + x) + w, so the four quarters of a 64-block range go to the four
+// wave slots of one XCD at about the same time and the tiles in flight stay one window of the
+// payload.  Iterations 0 and 1 take static tickets (the workgroup's rank among its XCD's gx
+// workgroups, and that + gx); the counters hand out the rest from 2 gx on.  The ticket of
+// iteration m is taken (lane 0, an inline-asm atomic the compiler does not track, tk_take) at the
+// top of iteration m - 4, right before the DMA of iteration m - 2's tile, and read at the top of
+// iteration m - 2, after the counted wait for that tile: in-order completion means the ticket has
+// arrived, and no wait drains the ring.  A launch zeroes ctr_clear, the set the previous launch of the same
+// kind on this stream counted on (api.cpp ctr_for alternates them).
+template <int T2, int WPC = 2, int NBUF = 3, int NTST = 1, bool TK = false>
 __global__ __launch_bounds__(256, WPC) void rs_wq_encode_kernel(const uint8_t* __restrict__ data,
-    uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables)
+    uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables, uint32_t* __restrict__ ctr = nullptr,
+    uint32_t* __restrict__ ctr_clear = nullptr)
 {
     static_assert(NBUF >= 2 && NBUF <= 4, "ring of 2 to 4 wave-tile buffers");
+    static_assert(!TK || NBUF == 3, "the ticket lead is sized for a ring of 3");
     using L = RsWgLayout<T2>;
     using D = WqLds<T2, NBUF>;
     constexpr int K = L::K;
@@ -175,6 +205,21 @@ __global__ __launch_bounds__(256, WPC) void rs_wq_encode_kernel(const uint8_t* _
     const uint64_t nfull = nblocks / QB, ntiles = (nblocks + QB - 1) / QB;
     const uint64_t W = (uint64_t)gridDim.x * 4u;
     uint64_t u = (uint64_t)blockIdx.x * 4u + wave;
+    // ticket geometry (TK): counter (xc, wave), this workgroup's rank among the gx of its counter
+    const uint32_t nx = gridDim.x < 8u ? gridDim.x : 8u, xc = blockIdx.x % nx;
+    const uint32_t gx = (gridDim.x - xc + nx - 1u) / nx, rank = blockIdx.x / nx;
+    uint32_t* const my_ctr = TK ? ctr + 16u * (4u * xc + wave) : nullptr;
+    auto tile_of = [&](uint64_t k) -> uint64_t { return 4u * (k * nx + xc) + wave; };
+    uint64_t u1 = u + W;  // the tile of iteration 1
+    uint32_t tka = 0, tkb = 0; // TK: tickets of the iterations two and three ahead (lane 0)
+    if constexpr (TK) {
+        u = tile_of(rank);
+        u1 = tile_of(rank + gx);
+        if (blockIdx.x == 0 && wave == 0 && lane < 32u)
+            __hip_atomic_store(ctr_clear + 16u * lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0)
+            tk_take(tka, my_ctr); // iteration 2
+    }
     const uint32_t par = D::OFF_PAR + wave * PARW;
     const uint32_t buf0 = D::OFF_BUF + wave * (NBUF * D::BUFQ);
     const uint32_t lbase = __builtin_amdgcn_readfirstlane(lds_addr(lds) + buf0 + PAD);
@@ -186,6 +231,9 @@ __global__ __launch_bounds__(256, WPC) void rs_wq_encode_kernel(const uint8_t* _
     // slots 1 .. NBUF - 2
     if (u < nfull)
         dma_qtile<IN_PIECES>(lbase, data + u * (QB * K), lane, data, ext);
+    if constexpr (TK)
+        if (lane == 0)
+            tk_take(tkb, my_ctr); // iteration 3
     for (uint32_t p = tid; p < 2048u / 16u; p += 256u)
         *(uint4*)(lds + 16u * p) = *(const uint4*)(tables + L::OFF_SL + 16u * p);
     for (uint32_t p = tid; p < 3u * 2048u / 16u; p += 256u) {
@@ -194,18 +242,40 @@ __global__ __launch_bounds__(256, WPC) void rs_wq_encode_kernel(const uint8_t* _
     }
     // the table loads' wait covered tile u (issued before them: a wave's loads complete in order)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int r = 1; r <= NBUF - 2; ++r)
-        if (u + (uint64_t)r * W < nfull) {
-            dma_qtile<IN_PIECES>(lbase + (uint32_t)r * D::BUFQ, data + (u + (uint64_t)r * W) * (QB * K), lane, data, ext);
-            vm.dma((uint32_t)r, KI);
+    if constexpr (TK) {
+        if (u1 < nfull) {
+            dma_qtile<IN_PIECES>(lbase + D::BUFQ, data + u1 * (QB * K), lane, data, ext);
+            vm.dma(1u, KI);
         }
+    } else {
+#pragma unroll
+        for (int r = 1; r <= NBUF - 2; ++r)
+            if (u + (uint64_t)r * W < nfull) {
+                dma_qtile<IN_PIECES>(lbase + (uint32_t)r * D::BUFQ, data + (u + (uint64_t)r * W) * (QB * K), lane, data, ext);
+                vm.dma((uint32_t)r, KI);
+            }
+    }
     wg::barrier_lds(); // tables visible to every wave; the only workgroup barrier of the kernel
 
     uint32_t cur = 0;
-    for (; u < nfull; u += W) {
+    // one iteration; tk = the register holding this iteration's ticket two ahead, refilled with the
+    // ticket four ahead (the loop runs two iterations per trip so that the two ticket registers keep
+    // fixed roles: a register copy would make the compiler wait for the atomic one iteration early,
+    // and that wait would also drain the newest tile DMA)
+    auto iteration = [&](uint32_t& tk) {
         const uint32_t buf = buf0 + cur * D::BUFQ;
-        const uint64_t ua = u + (uint64_t)(NBUF - 1) * W; // the tile NBUF - 1 iterations ahead
+        uint64_t ua; // the tile NBUF - 1 iterations ahead
+        if constexpr (TK) {
+            // taken two iterations ago right before the DMA of this iteration's tile, so the wait
+            // for that tile (end of the last iteration, or the prologue's) covered it
+            ua = tile_of((uint64_t)tk_ready(tk) + 2u * gx);
+            if (lane == 0)
+                tk_take(tk, my_ctr); // the iteration four ahead
+            vm.issued(1);
+        } else {
+            (void)tk;
+            ua = u + (uint64_t)(NBUF - 1) * W;
+        }
         const uint32_t sa = wg::ring_add(cur, NBUF - 1, NBUF);
         if (ua < nfull) {
             dma_qtile<IN_PIECES>(lbase + sa * D::BUFQ, data + ua * (QB * K), lane, data, ext);
@@ -228,9 +298,21 @@ __global__ __launch_bounds__(256, WPC) void rs_wq_encode_kernel(const uint8_t* _
         }
         vm.issued(KO);
         cur = wg::ring_add(cur, 1, NBUF);
-        if (u + W < nfull)
+        const uint64_t un = TK ? u1 : u + W; // the next iteration's tile
+        if (un < nfull)
             wg::vm_wait_exact(vm.newer(cur)); // the next tile landed
+        u = un;
+        if constexpr (TK)
+            u1 = ua;
+    };
+    while (u < nfull) {
+        iteration(tka);
+        if (u >= nfull)
+            break;
+        iteration(tkb);
     }
+    // tickets still in flight land in tka / tkb: drain them before those registers can be reused
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(tka), "+v"(tkb)::"memory");
     if (u == nfull && nfull < ntiles) { // the partial wave tile (nblocks % 16 blocks), staged bytewise
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const uint32_t buf = buf0 + cur * D::BUFQ;
