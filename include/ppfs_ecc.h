@@ -219,6 +219,14 @@ int ppfs_ecc_group_decode_host(ppfs_ecc_group* group, uint8_t* raw, uint8_t* dat
 int ppfs_ecc_group_write_host(ppfs_ecc_group* group, const uint8_t* data, uint8_t* raw, uint8_t* status,
     size_t nblocks);
 
+/* Kernel timing hook (bench.py's roofline, tools): the next RS kernel the calling thread launches
+ * through any context records start_event / stop_event (hipEvent_t, created by the caller with
+ * timing enabled) from its own dispatch packet (hipExtLaunchKernel) -- the kernel's execution time
+ * as rocprofv3 measures it, without the launch gap that events recorded on the stream around the
+ * call include.  The hook disarms after one launch; (NULL, NULL) disarms it.  -EINVAL if only one
+ * event is given.  Engine extension, no reference counterpart. */
+int ppfs_ecc_time_next_launch(void* start_event, void* stop_event);
+
 /* Last HIP error string recorded by this thread (diagnostics). */
 const char* ppfs_ecc_last_error(void);
 

@@ -27,6 +27,7 @@ EXPORTED_SYMBOLS = (
     "ppfs_ecc_data_size",
     "ppfs_ecc_kernel_name",
     "ppfs_ecc_stream_kernel_name",
+    "ppfs_ecc_time_next_launch",
     "ppfs_ecc_encode_device",
     "ppfs_ecc_decode_device",
     "ppfs_ecc_write_device",
@@ -103,6 +104,8 @@ def lib() -> ctypes.CDLL:
     L.ppfs_ecc_debug_dma_selftest.argtypes = []
     L.ppfs_ecc_host_registered.restype = c_longlong
     L.ppfs_ecc_host_registered.argtypes = [POINTER(c_size_t)]
+    L.ppfs_ecc_time_next_launch.restype = c_int
+    L.ppfs_ecc_time_next_launch.argtypes = [c_void_p, c_void_p]
     L.ppfs_ecc_stream_kernel_name.restype = c_char_p
     L.ppfs_ecc_stream_kernel_name.argtypes = [c_void_p, c_void_p]
     L.ppfs_ecc_crc_implicit_to_explicit.restype = c_uint64

@@ -26,6 +26,7 @@
 
 #include "../../include/ppfs_ecc.h"
 #include "rs_layout.hpp"
+#include "launch.hpp"
 #include "server_box.hpp"
 
 // kernels (rs_kernels.hip / bit_kernels.hip)
@@ -1185,6 +1186,18 @@ extern "C" int ppfs_ecc_write_device(ppfs_ecc_ctx* c, const uint8_t* d_data, uin
 {
     return queued(c, ppfs_ecc_write_device_impl(c, d_data, d_raw, d_status, nblocks, stream), nblocks, stream,
         "write (async)");
+}
+
+namespace ppfs {
+thread_local TimeHook g_time_hook;
+}
+
+extern "C" int ppfs_ecc_time_next_launch(void* start_event, void* stop_event)
+{
+    if ((start_event == nullptr) != (stop_event == nullptr))
+        return -EINVAL;
+    ppfs::g_time_hook = ppfs::TimeHook { (hipEvent_t)start_event, (hipEvent_t)stop_event };
+    return 0;
 }
 
 extern "C" const char* ppfs_ecc_stream_kernel_name(ppfs_ecc_ctx* c, void* stream)

@@ -11,6 +11,7 @@
 #include "rs_wg_tk.hpp"
 #include "rs_pair.hpp"
 #include "rs_bs.hpp"
+#include "launch.hpp"
 
 #ifndef PPFS_T2
 #error "compile with -DPPFS_T2=<2t>"
@@ -88,20 +89,20 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
 {
 #if PPFS_T2 <= 8
     if (ctr && ctr_clear)
-        hipLaunchKernelGGL((wg::rs_wg_encode_tk_kernel<PPFS_T2, ENC_WPC, 1>), dim3(rs_tile_grid(nb, ENC_WPC)), dim3(256), 0, s,
+        PPFS_LAUNCH((wg::rs_wg_encode_tk_kernel<PPFS_T2, ENC_WPC, 1>), dim3(rs_tile_grid(nb, ENC_WPC)), dim3(256), 0, s,
             d, r, nb, tab, ctr, ctr_clear);
     else
-        hipLaunchKernelGGL((wg::rs_wg_encode_kernel<PPFS_T2, ENC_NBUF, ENC_WPC_STATIC, 3, 1, false>), dim3(rs_tile_grid(nb, ENC_WPC_STATIC)),
+        PPFS_LAUNCH((wg::rs_wg_encode_kernel<PPFS_T2, ENC_NBUF, ENC_WPC_STATIC, 3, 1, false>), dim3(rs_tile_grid(nb, ENC_WPC_STATIC)),
             dim3(256), 0, s, d, r, nb, tab);
 #elif PPFS_T2 == 32
-    hipLaunchKernelGGL((bs::rs_bs_encode_kernel<PPFS_T2, BS_ENC_NW, 1>), dim3(rs_tile_grid(nb, 1, bs::TBW * BS_ENC_NW)),
+    PPFS_LAUNCH((bs::rs_bs_encode_kernel<PPFS_T2, BS_ENC_NW, 1>), dim3(rs_tile_grid(nb, 1, bs::TBW * BS_ENC_NW)),
         dim3(64 * BS_ENC_NW), 0, s, d, r, nb, tab);
 #else
     if constexpr (SOLO_IMG)
-        hipLaunchKernelGGL((pair::rs_solo_encode_img_kernel<PPFS_T2, SOLO_WPC, SOLO_NW>),
+        PPFS_LAUNCH((pair::rs_solo_encode_img_kernel<PPFS_T2, SOLO_WPC, SOLO_NW>),
             dim3(rs_tile_grid(nb, SOLO_WPC, 64 * SOLO_NW)), dim3(64 * SOLO_NW), 0, s, d, r, nb, tab);
     else
-        hipLaunchKernelGGL(rs255_encode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, d, r, nb, tab);
+        PPFS_LAUNCH(rs255_encode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, d, r, nb, tab);
 #endif
     return hipGetLastError();
 }
@@ -124,16 +125,16 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
 {
 #if PPFS_T2 <= 8
     if (ctr && ctr_clear)
-        hipLaunchKernelGGL((wg::rs_wg_decode_tk_kernel<PPFS_T2, DEC_WPC, 1>), dim3(rs_tile_grid(nb, DEC_WPC)), dim3(256), 0, s,
+        PPFS_LAUNCH((wg::rs_wg_decode_tk_kernel<PPFS_T2, DEC_WPC, 1>), dim3(rs_tile_grid(nb, DEC_WPC)), dim3(256), 0, s,
             r, d, st, nb, tab, wb, ctr, ctr_clear);
     else
-        hipLaunchKernelGGL((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC, 7, 1>), dim3(rs_tile_grid(nb, DEC_WPC)),
+        PPFS_LAUNCH((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC, 7, 1>), dim3(rs_tile_grid(nb, DEC_WPC)),
             dim3(256), 0, s, r, d, st, nb, tab, wb);
 #elif PPFS_T2 == 32
-    hipLaunchKernelGGL((bs::rs_bs_decode_kernel<PPFS_T2, BS_DEC_NW, BS_DEC_NBUF, 1, BS_DEC_TLDS>), dim3(rs_tile_grid(nb, 1, bs::TBW * BS_DEC_NW)),
+    PPFS_LAUNCH((bs::rs_bs_decode_kernel<PPFS_T2, BS_DEC_NW, BS_DEC_NBUF, 1, BS_DEC_TLDS>), dim3(rs_tile_grid(nb, 1, bs::TBW * BS_DEC_NW)),
         dim3(64 * BS_DEC_NW), 0, s, r, d, st, nb, tab, wb);
 #else
-    hipLaunchKernelGGL(rs255_decode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, r, d, st, nb, tab, wb);
+    PPFS_LAUNCH(rs255_decode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, r, d, st, nb, tab, wb);
 #endif
     return hipGetLastError();
 }
@@ -145,12 +146,12 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_server_launch_t, PPFS_T2)(ppfs::SrvBox* b
     const uint8_t* tab, uint32_t gen, uint32_t idle_us, hipStream_t s)
 {
 #if PPFS_T2 <= 8
-    hipLaunchKernelGGL((wg::rs_wg_server_kernel<PPFS_T2>), dim3(1), dim3(256), 0, s, box, zc, zc_bytes, tab, gen, idle_us);
+    PPFS_LAUNCH((wg::rs_wg_server_kernel<PPFS_T2>), dim3(1), dim3(256), 0, s, box, zc, zc_bytes, tab, gen, idle_us);
 #elif PPFS_T2 == 32
-    hipLaunchKernelGGL((pair::rs_pair_server_kernel<PPFS_T2, true>), dim3(1), dim3(pair::NTHR), 0, s, box, zc, zc_bytes, tab,
+    PPFS_LAUNCH((pair::rs_pair_server_kernel<PPFS_T2, true>), dim3(1), dim3(pair::NTHR), 0, s, box, zc, zc_bytes, tab,
         gen, idle_us);
 #else
-    hipLaunchKernelGGL((rs255_server_kernel<PPFS_T2>), dim3(1), dim3(64), 0, s, box, zc, zc_bytes, tab, gen, idle_us);
+    PPFS_LAUNCH((rs255_server_kernel<PPFS_T2>), dim3(1), dim3(64), 0, s, box, zc, zc_bytes, tab, gen, idle_us);
 #endif
     return hipGetLastError();
 }
