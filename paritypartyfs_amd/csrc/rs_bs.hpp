@@ -64,7 +64,7 @@ __device__ uint64_t g_bs_trace[4096 * BS_TRACE_N];
 #define PPFS_BS_DEC_IDMA 0 // decode: next tile's DMA interleaved with the emission rounds
 #endif
 #ifndef PPFS_BS_EMIT_G
-#define PPFS_BS_EMIT_G 1 // decode emission: output pieces read from LDS together
+#define PPFS_BS_EMIT_G 4 // decode emission: output pieces read from LDS together (4: +0.5 % cfg5 step, r3p)
 #endif
 
 constexpr int TBW = 32;            // blocks per wave tile
