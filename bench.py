@@ -549,35 +549,44 @@ def main(argv=None):
     L = max(3, args.standalone_launches)
     R = 4
     hs = HipEvents(L + 1)
+    hsk = HipEvents(2 * L)
+    sa_events = {}  # launch-to-launch stream-event intervals, reported beside the kernel times
 
-    def time_launches(fn):
+    def time_launches(fn, key):
+        # kernel durations from the dispatch packets (as in-step above); the stream-event intervals
+        # between consecutive launches also contain the gap between kernels
         for i in range(3):
             fn(i)
         hs.record(0, stream)
         for i in range(L):
+            NL.ppfs_ecc_time_next_launch(hsk.ev[2 * i], hsk.ev[2 * i + 1])
             fn(i)
+            NL.ppfs_ecc_time_next_launch(None, None)
             hs.record(i + 1, stream)
         torch.cuda.synchronize()
-        return [hs.ms(i, i + 1) for i in range(L)]
+        sa_events[key] = round(float(np.median([hs.ms(i, i + 1) for i in range(L)])), 5)
+        return [hsk.ms(2 * i, 2 * i + 1) for i in range(L)]
 
     rewarm(0.3)
-    enc_sa = time_launches(lambda i: eng.encode(data, cw, nblocks=nb))
+    enc_sa = time_launches(lambda i: eng.encode(data, cw, nblocks=nb), "encode_ms_median")
     assert torch.equal(cw, clean_cw), "standalone encode output differs"
     # clean decode (status + write-back enabled, nothing to correct): the read path of a scrub
     rewarm(0.3)
     eng.encode(data, cw, nblocks=nb)
-    dec_sa = time_launches(lambda i: eng.decode(cw, out, status, write_back=True, nblocks=nb))
+    dec_sa = time_launches(lambda i: eng.decode(cw, out, status, write_back=True, nblocks=nb), "clean_decode_ms_median")
     d_rot = [data] + [torch.randint(0, 256, (nb * k,), dtype=torch.uint8, device=dev, generator=gen)
                       for _ in range(R - 1)]
     c_rot = [torch.empty(nb * n, dtype=torch.uint8, device=dev) for _ in range(R)]
     o_rot = [torch.empty(nb * k, dtype=torch.uint8, device=dev) for _ in range(R)]
     rewarm(0.3)
-    enc_cold = time_launches(lambda i: eng.encode(d_rot[i % R], c_rot[i % R], nblocks=nb))
+    enc_cold = time_launches(lambda i: eng.encode(d_rot[i % R], c_rot[i % R], nblocks=nb), "cold_encode_ms_median")
     rewarm(0.3)
-    dec_cold = time_launches(lambda i: eng.decode(c_rot[i % R], o_rot[i % R], status, write_back=True, nblocks=nb))
+    dec_cold = time_launches(lambda i: eng.decode(c_rot[i % R], o_rot[i % R], status, write_back=True, nblocks=nb),
+                             "cold_clean_decode_ms_median")
     assert torch.equal(o_rot[1], d_rot[1]), "standalone decode output differs"
     del d_rot, c_rot, o_rot
     hs.close()
+    hsk.close()
 
     # (3) device copy ceiling: the engine's full-grid 16-byte copy kernel over the bytes of one
     # encode (read k, write n per block), timed like the kernels
@@ -689,7 +698,7 @@ def main(argv=None):
                 continue  # the bench's own workload is measured above
             cfg_lines[want[name]] = run_config(name, typ, cbs, ct, poly, 1 << 20, args.config_reps, stream, dev)
         cfg_lines["note"] = ("BASELINE configs measured outside the timed region: median of back-to-back launches "
-                             "of one kernel over 2^20 blocks (fence-free HIP events), algorithmic bytes (payload + raw "
+                             "of one kernel over 2^20 blocks (each kernel's dispatch-packet start / stop), algorithmic bytes (payload + raw "
                              "per block) / time, fraction of 8 TB/s; 1-error decodes restore the corrupted image by "
                              "an untimed copy before each launch; roundtrip_ok = decode(encode(x)) == x with the "
                              "expected statuses")
@@ -754,10 +763,12 @@ def main(argv=None):
                 "cold_encode_frac": frac(float(np.median(enc_cold))),
                 "cold_clean_decode_ms_median": round(float(np.median(dec_cold)), 5),
                 "cold_clean_decode_frac": frac(float(np.median(dec_cold))),
-                "note": "back-to-back launches of one kernel, fence-free events between them, outside the "
-                        "timed region (north-star: >= 70 % on RS t=3 encode over 1 M blocks); hot = same "
-                        "buffers every launch (input partly Infinity-Cache resident), cold = launches rotate "
-                        f"over {R} buffer sets (input from HBM)",
+                "stream_event_intervals_ms": sa_events,
+                "note": "back-to-back launches of one kernel outside the timed region, each kernel's duration "
+                        "from its dispatch packet (stream_event_intervals_ms: fence-free events between the "
+                        "launches, gaps included) (north-star: >= 70 % on RS t=3 encode over 1 M blocks); hot = "
+                        "same buffers every launch (input partly Infinity-Cache resident), cold = launches "
+                        f"rotate over {R} buffer sets (input from HBM)",
             },
             "device_copy_GBps": round(copy_gbs, 1),
             "device_copy_cold_GBps": round(copy_cold_gbs, 1),

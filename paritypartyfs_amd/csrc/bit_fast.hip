@@ -25,6 +25,7 @@
 
 #include "dbg.hpp"
 #include "gf_common.hpp"
+#include "launch.hpp"
 
 namespace ppfs {
 namespace bf {
@@ -1032,13 +1033,13 @@ extern "C" int ppfs_bitfast_supported(uint32_t bs) { return bs == 1024 || bs == 
 #define PPFS_NP_DISPATCH(bs, KERNEL, nb, ...)                                                                         \
     switch (bs) {                                                                                                      \
     case 1024:                                                                                                         \
-        hipLaunchKernelGGL(KERNEL<1>, dim3(bf_grid(KERNEL<1>, nb)), dim3(256), 0, __VA_ARGS__);                        \
+        PPFS_LAUNCH(KERNEL<1>, dim3(bf_grid(KERNEL<1>, nb)), dim3(256), 0, __VA_ARGS__);                        \
         break;                                                                                                         \
     case 2048:                                                                                                         \
-        hipLaunchKernelGGL(KERNEL<2>, dim3(bf_grid(KERNEL<2>, nb)), dim3(256), 0, __VA_ARGS__);                        \
+        PPFS_LAUNCH(KERNEL<2>, dim3(bf_grid(KERNEL<2>, nb)), dim3(256), 0, __VA_ARGS__);                        \
         break;                                                                                                         \
     default:                                                                                                           \
-        hipLaunchKernelGGL(KERNEL<4>, dim3(bf_grid(KERNEL<4>, nb)), dim3(256), 0, __VA_ARGS__);                        \
+        PPFS_LAUNCH(KERNEL<4>, dim3(bf_grid(KERNEL<4>, nb)), dim3(256), 0, __VA_ARGS__);                        \
         break;                                                                                                         \
     }
 

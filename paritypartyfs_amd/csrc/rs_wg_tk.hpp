@@ -69,6 +69,20 @@ __device__ __forceinline__ void vm_wait_exact(uint32_t n)
     }
 }
 
+// PPFS_TK_LEAD2 tickets: the atomic is issued from inline asm (the compiler does not track it, so it
+// never inserts a wait of its own -- with the loop unrolled by two it fell back to vmcnt(0), which
+// also waited for the wave's fresh stores and atomic); the caller waits with a counted vmcnt and
+// then ties the register (tk_arrived) before reading it.
+__device__ __forceinline__ void tk_take_asm(uint32_t& tk, uint32_t* ctr)
+{
+    asm volatile("global_atomic_inc %0, %1, %2, off sc0" : "=v"(tk) : "v"(ctr), "v"(0xFFFFFFFFu) : "memory");
+}
+__device__ __forceinline__ uint32_t tk_arrived(uint32_t& tk)
+{
+    asm volatile("" : "+v"(tk));
+    return tk;
+}
+
 // Wave 0 (64 lanes) copies the first BYTES of the table blob into LDS at 0 by LDS-DMA: no register
 // round trip, and its loads never share a queue with the DMA waves' tiles.  Caller: vmcnt(0).
 template <int BYTES>
@@ -233,8 +247,12 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
             PPFS_TK_MARK(6);
         }
         const uint64_t ahead = __builtin_amdgcn_readfirstlane(s_tk[(iter + 2u) & 3u]);
-        if (tk_lane)
-            tk = atomicInc(my_ctr, 0xFFFFFFFFu); // the tile of iteration iter + 3 (PPFS_TK_LEAD2: + 4)
+        if (tk_lane) {
+            if constexpr (PPFS_TK_LEAD2)
+                tk_take_asm(tk, my_ctr); // the tile of iteration iter + 4
+            else
+                tk = atomicInc(my_ctr, 0xFFFFFFFFu); // the tile of iteration iter + 3
+        }
         const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + pc * 512u;
         const bool go = ahead < nfull;
         if (dmaw && go)
@@ -281,8 +299,13 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
             vm_wait_exact(st + kd * (hist & 1u));
         }
         if constexpr (PPFS_TK_LEAD2) {
-            if (tk_lane && iter >= 2u) // the ticket of (iteration iter - 2) + 4 (iteration 3's: the prologue)
-                s_tk[(iter + 2u) & 3u] = (uint32_t)tk_tile(tk_prev + 2u * g.gx, g, nfull);
+            // the ticket of (iteration iter - 2) + 4 (iteration 3's: the prologue).  Wave 0 issued after
+            // its atomic at least: 4 stores of that iteration, this iteration's atomic and 4 stores
+            if (wave == 0 && iter >= 2u) {
+                vm_wait_exact(9u);
+                if (lane == 0)
+                    s_tk[(iter + 2u) & 3u] = (uint32_t)tk_tile(tk_arrived(tk_prev) + 2u * g.gx, g, nfull);
+            }
         } else {
             (void)tk_prev;
             if (tk_lane)
@@ -301,6 +324,8 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
                 break;
             body(tkb, tka);
         }
+        if (wave == 0) // tickets still in flight land in tka / tkb: drain before those registers are reused
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(tka), "+v"(tkb)::"memory");
     } else {
         while (q0 < nfull)
             body(tka, tkb);
@@ -406,8 +431,12 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
             PPFS_TK_MARK(7);
         }
         const uint64_t q1 = __builtin_amdgcn_readfirstlane(s_tk[(iter + 1u) & 3u]);
-        if (tk_lane)
-            tk = atomicInc(my_ctr, 0xFFFFFFFFu); // the tile of iteration iter + 2 (PPFS_TK_LEAD2: + 3)
+        if (tk_lane) {
+            if constexpr (PPFS_TK_LEAD2)
+                tk_take_asm(tk, my_ctr); // the tile of iteration iter + 3
+            else
+                tk = atomicInc(my_ctr, 0xFFFFFFFFu); // the tile of iteration iter + 2
+        }
         const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + pc * 512u;
         if (dmaw && q1 < nfull)
             dma_tile192<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, raw + q1 * (TB * 255), tid, raw,
@@ -460,8 +489,13 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         if constexpr (PPFS_TK_LEAD2) {
-            if (tk_lane && iter >= 2u) // the ticket of (iteration iter - 2) + 3 (iteration 2's: the prologue)
-                s_tk[(iter + 1u) & 3u] = (uint32_t)tk_tile(tk_prev + g.gx, g, nfull);
+            // the ticket of (iteration iter - 2) + 3 (iteration 2's: the prologue).  Wave 0 issued after
+            // its atomic at least this iteration's atomic and, with payload output, 2 x 4 stores
+            if (wave == 0 && iter >= 2u) {
+                vm_wait_exact(want ? 9u : 1u);
+                if (lane == 0)
+                    s_tk[(iter + 1u) & 3u] = (uint32_t)tk_tile(tk_arrived(tk_prev) + g.gx, g, nfull);
+            }
         } else {
             (void)tk_prev;
             if (tk_lane)
@@ -479,6 +513,8 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
                 break;
             body(tkb, tka);
         }
+        if (wave == 0) // tickets still in flight land in tka / tkb: drain before those registers are reused
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(tka), "+v"(tkb)::"memory");
     } else {
         while (q0 < nfull)
             body(tka, tkb);

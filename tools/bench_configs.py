@@ -3,7 +3,7 @@
 
 BASELINE.json configs: cfg2/cfg3 RS(255,249) t=3 encode / 1-error decode, cfg4 Hamming and
 CRC 0x9960034c at block_size 4096, cfg5 RS(255,223) t=16 (per-GPU shard of 2^20 blocks), plus
-parity.  Each line: median kernel time over --reps launches (hipEvents on the launch stream),
+parity.  Each line: median kernel time over --reps launches (the kernels' dispatch-packet events),
 algorithmic bytes per launch, GB/s and fraction of the 8 TB/s HBM peak.  Launches are timed
 back to back (same kernel, same buffers) after a 0.3 s clock ramp, with fence-free HIP events.  A device-side round
 trip check (decode(encode(x)) == x, status as expected) guards every config; bit-exactness vs
@@ -37,8 +37,20 @@ def prewarm(fn, seconds):
         torch.cuda.synchronize()
 
 
+def timed_launch(he, i, fn):
+    """One engine call whose kernel records events 2 i, 2 i + 1 from its own dispatch packet
+    (ppfs_ecc_time_next_launch; bench.py's in-step timing): the kernel's duration, as rocprofv3
+    reports it, without the launch gap."""
+    from paritypartyfs_amd import _native
+
+    L = _native.lib()
+    L.ppfs_ecc_time_next_launch(he.ev[2 * i], he.ev[2 * i + 1])
+    fn()
+    L.ppfs_ecc_time_next_launch(None, None)
+
+
 def med_ms(fn, reps, stream, warm_s=0.3):
-    """Median launch time over `reps` back-to-back launches, fence-free HIP events (bench.py)."""
+    """Median kernel time over `reps` back-to-back launches (dispatch-packet events, timed_launch)."""
     import torch
 
     from bench import HipEvents
@@ -46,9 +58,7 @@ def med_ms(fn, reps, stream, warm_s=0.3):
     prewarm(fn, warm_s)
     he = HipEvents(2 * reps)
     for i in range(reps):
-        he.record(2 * i, stream)
-        fn()
-        he.record(2 * i + 1, stream)
+        timed_launch(he, i, fn)
     torch.cuda.synchronize()
     r = float(np.median([he.ms(2 * i, 2 * i + 1) for i in range(reps)]))
     he.close()
@@ -112,9 +122,7 @@ def run_config(name, typ, bs, t, poly_implicit, nb, reps, stream, dev, warm_s=0.
         he = HipEvents(2 * reps)
         for i in range(reps):
             raw.copy_(bad)
-            he.record(2 * i, stream)
-            eng.decode(raw, out, st, write_back=True, nblocks=nb)
-            he.record(2 * i + 1, stream)
+            timed_launch(he, i, lambda: eng.decode(raw, out, st, write_back=True, nblocks=nb))
         torch.cuda.synchronize()
         dec_ms = float(np.median([he.ms(2 * i, 2 * i + 1) for i in range(reps)]))
         he.close()
