@@ -441,11 +441,6 @@ std::vector<uint8_t> build_crc_fast_tables(uint64_t P, int n, uint32_t ds, uint3
     for (long m = 0; m < 16; ++m)
         ex.push_back(8L * ((long)ds + m - 1024L * (NP + 1)) + n - 1);
     ex.push_back(8L * ((long)ds - (long)bs) + n - 1);
-    // round 3 (PPFS_CRC_FOLD kernels): dword j of a piece d pieces before the last, straight to its
-    // place: x^(32 (3 - j) + 8192 d), d = 0..4 -- no Horner chain across a lane's pieces
-    for (long d = 0; d <= 4; ++d)
-        for (long j = 0; j < 4; ++j)
-            ex.push_back(32L * (3 - j) + 8192L * d);
 
     std::vector<uint8_t> out((size_t)ppfs_crc_fast_tables_bytes(), 0);
     uint32_t* t = (uint32_t*)out.data();

@@ -695,21 +695,8 @@ __global__ __launch_bounds__(256) void parity_fast_check_kernel(const uint8_t* _
 //   payload's real position (e < 0 uses x^-1: P(0) = 1).
 // ------------------------------------------------------------------------------------
 constexpr int CF_MAP = 512;                      // 8 nibbles x 16 entries x u32
-constexpr int CF_M0 = 0, CF_K = 4, CF_L = 5, CF_FENC = 11, CF_FCHK = 27, CF_W = 28, CF_NMAPS = 48;
-constexpr int CF_BYTES = CF_NMAPS * CF_MAP;     // 24 KiB
-// PPFS_CRC_FOLD (round 3): every dword of a lane's pieces goes through one map that also places it
-// (CF_W + 4 d + j = x^(32 (3 - j) + 8192 d)), so a lane's value is one level of independent maps
-// instead of a Horner chain across its pieces; and the first four levels of the lane tree move data
-// with DPP row shifts instead of ds_bpermute.  Same number of maps per block.
-#ifndef PPFS_CRC_FOLD
-#define PPFS_CRC_FOLD 0
-#endif
-constexpr bool CRC_FOLD = PPFS_CRC_FOLD;
-#ifndef PPFS_CRC_DPP
-#define PPFS_CRC_DPP PPFS_CRC_FOLD // the DPP lane-tree levels alone
-#endif
-constexpr bool CRC_DPP = PPFS_CRC_DPP;
-constexpr int CF_LDS = CRC_FOLD ? CF_BYTES : CF_W * CF_MAP; // the maps a kernel copies to LDS
+constexpr int CF_M0 = 0, CF_K = 4, CF_L = 5, CF_FENC = 11, CF_FCHK = 27, CF_NMAPS = 28;
+constexpr int CF_BYTES = CF_NMAPS * CF_MAP;     // 14 KiB
 // Blocks per wave of the CRC kernels: a workgroup stages the 14 KiB of maps once and then walks
 // CRC_BPW consecutive 4-block groups (one contiguous range, so the full grid keeps its address
 // order); with one group per workgroup the map staging read as much L2 as the blocks themselves.
@@ -717,11 +704,6 @@ constexpr int CF_LDS = CRC_FOLD ? CF_BYTES : CF_W * CF_MAP; // the maps a kernel
 #define PPFS_CRC_BPW 8
 #endif
 constexpr int CRC_BPW = PPFS_CRC_BPW;
-// resident workgroups per CU the CRC kernels are compiled for (launch bound): 4 keeps the register
-// prefetch of the next block within 128 VGPRs (4 waves per SIMD)
-#ifndef PPFS_CRC_MINWG
-#define PPFS_CRC_MINWG 1
-#endif
 
 // (x >> 8k) & 0x3C (a nibble * 4, the entry's byte offset): one v_and_b32_sdwa for k > 0
 __device__ __forceinline__ uint32_t sel3c(uint32_t x, int k)
@@ -784,55 +766,24 @@ __device__ __forceinline__ uint32_t crc_piece(const uint8_t* tbl, uint4 v, uint3
         ^ (n32 ? d3 : cmap(tbl + CF_M0 * CF_MAP, d3));
 }
 
-// value of lane l + 2^J of the same row of 16 (DPP row_shl), 0 past the row end
-template <int J> __device__ __forceinline__ uint32_t row_shl_pow2(uint32_t v)
-{
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 + (1 << J), 0xF, 0xF, false);
-}
-
 // Sum over the wave of value_l * x^(128 (63 - l)) -> wave-uniform
 __device__ __forceinline__ uint32_t crc_lane_tree(const uint8_t* tbl, uint32_t acc)
 {
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
-        uint32_t other;
-        if (CRC_DPP && j < 4) // lane l + 2^j of the same row of 16 (row_shl); the lanes whose partner
-            // lies past their row get 0 -- only the row leaders' sums are used by levels 4, 5
-            other = j == 0 ? row_shl_pow2<0>(acc) : j == 1 ? row_shl_pow2<1>(acc) : j == 2 ? row_shl_pow2<2>(acc) : row_shl_pow2<3>(acc);
-        else
-            other = __shfl_down(acc, 1 << j, 64);
+        const uint32_t other = __shfl_down(acc, 1 << j, 64);
         acc = cmap(tbl + (CF_L + j) * CF_MAP, acc) ^ other;
     }
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)acc);
 }
 
-// CRC_FOLD: 16 payload bytes d pieces before the lane's last -> their contribution, placed
-__device__ __forceinline__ uint32_t crc_piece_at(const uint8_t* tbl, uint4 v, uint32_t lo, uint32_t hi, bool n32, int d)
-{
-    uint32_t w[4] = { v.x, v.y, v.z, v.w };
-    if (lo > 0 || hi < 16) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            uint32_t keep = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                keep |= (4u * u + b >= lo && 4u * u + b < hi) ? (0xFFu << (8 * b)) : 0u;
-            w[u] &= keep;
-        }
-    }
-    const uint8_t* m = tbl + (CF_W + 4 * d) * CF_MAP;
-    const uint32_t d3 = bswap(w[3]);
-    return __builtin_amdgcn_bitop3_b32(cmap(m, bswap(w[0])), cmap(m + CF_MAP, bswap(w[1])), cmap(m + 2 * CF_MAP, bswap(w[2])), 0x96)
-        ^ ((n32 && d == 0) ? d3 : cmap(m + 3 * CF_MAP, d3));
-}
-
 template <int NP>
-__global__ __launch_bounds__(256, PPFS_CRC_MINWG) void crc_fast_encode_kernel(const uint8_t* __restrict__ data,
+__global__ __launch_bounds__(256) void crc_fast_encode_kernel(const uint8_t* __restrict__ data,
     uint8_t* __restrict__ raw, const uint8_t* __restrict__ skip, uint64_t nblocks_all, CrcFast a,
     const uint8_t* __restrict__ tables)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t tbl[CF_LDS];
-    for (uint32_t p = threadIdx.x; p < CF_LDS / 16; p += 256)
+    __shared__ __attribute__((aligned(16))) uint8_t tbl[CF_BYTES];
+    for (uint32_t p = threadIdx.x; p < CF_BYTES / 16; p += 256)
         *(uint4*)(tbl + 16 * p) = *(const uint4*)(tables + 16 * p);
     __syncthreads();
     const uint32_t lane = lane_id(), wave = wave_id();
@@ -859,14 +810,8 @@ __global__ __launch_bounds__(256, PPFS_CRC_MINWG) void crc_fast_encode_kernel(co
             const int32_t lo = (int32_t)m - q16, hi = (int32_t)(m + a.ds) - q16;
             const uint32_t lo_c = lo < 0 ? 0u : (lo > 16 ? 16u : (uint32_t)lo);
             const uint32_t hi_c = hi < 0 ? 0u : (hi > 16 ? 16u : (uint32_t)hi);
-            if constexpr (CRC_FOLD) {
-                const uint32_t pv = crc_piece_at(tbl, cur.v[k], lo_c, hi_c > lo_c ? hi_c : lo_c, n32, NP - k);
-                acc = k == 0 ? pv : acc ^ pv;
-                __builtin_amdgcn_sched_barrier(0); // one piece's lookups in flight at a time (registers)
-            } else {
-                const uint32_t pv = crc_piece(tbl, cur.v[k], lo_c, hi_c > lo_c ? hi_c : lo_c, n32);
-                acc = k == 0 ? pv : (cmap(tbl + CF_K * CF_MAP, acc) ^ pv);
-            }
+            const uint32_t pv = crc_piece(tbl, cur.v[k], lo_c, hi_c > lo_c ? hi_c : lo_c, n32);
+            acc = k == 0 ? pv : (cmap(tbl + CF_K * CF_MAP, acc) ^ pv);
         }
         const uint32_t Vs = crc_lane_tree(tbl, acc);
         const uint32_t V = cmap(tbl + (CF_FENC + m) * CF_MAP, Vs);
@@ -915,12 +860,12 @@ __global__ __launch_bounds__(256, PPFS_CRC_MINWG) void crc_fast_encode_kernel(co
 }
 
 template <int NP>
-__global__ __launch_bounds__(256, PPFS_CRC_MINWG) void crc_fast_check_kernel(const uint8_t* __restrict__ raw,
+__global__ __launch_bounds__(256) void crc_fast_check_kernel(const uint8_t* __restrict__ raw,
     uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks_all, CrcFast a,
     const uint8_t* __restrict__ tables)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t tbl[CF_LDS];
-    for (uint32_t p = threadIdx.x; p < CF_LDS / 16; p += 256)
+    __shared__ __attribute__((aligned(16))) uint8_t tbl[CF_BYTES];
+    for (uint32_t p = threadIdx.x; p < CF_BYTES / 16; p += 256)
         *(uint4*)(tbl + 16 * p) = *(const uint4*)(tables + 16 * p);
     __syncthreads();
     const uint32_t lane = lane_id(), wave = wave_id();
@@ -947,14 +892,8 @@ __global__ __launch_bounds__(256, PPFS_CRC_MINWG) void crc_fast_check_kernel(con
             const int32_t q16 = 16 * (64 * k + (int32_t)lane);
             const int32_t hi = (int32_t)ds - q16;
             const uint32_t hi_c = hi < 0 ? 0u : (hi > 16 ? 16u : (uint32_t)hi);
-            if constexpr (CRC_FOLD) {
-                const uint32_t pv = crc_piece_at(tbl, R[k], 0u, hi_c, n32, NP - 1 - k);
-                acc = k == 0 ? pv : acc ^ pv;
-                __builtin_amdgcn_sched_barrier(0);
-            } else {
-                const uint32_t pv = crc_piece(tbl, R[k], 0u, hi_c, n32);
-                acc = k == 0 ? pv : (cmap(tbl + CF_K * CF_MAP, acc) ^ pv);
-            }
+            const uint32_t pv = crc_piece(tbl, R[k], 0u, hi_c, n32);
+            acc = k == 0 ? pv : (cmap(tbl + CF_K * CF_MAP, acc) ^ pv);
         }
         const uint32_t Vs = crc_lane_tree(tbl, acc);
         const uint32_t V = cmap(tbl + CF_FCHK * CF_MAP, Vs);

@@ -443,36 +443,19 @@ template <int N> __device__ __forceinline__ void lds_window(uint32_t (&d)[N], co
 // Encode emission: 16 bytes of the codeword tile at piece p, from the LDS payload rows and the
 // combined parity slots.  Codeword byte j of block b = j / 255 (off = j % 255): parity byte off if
 // off < 2t, else payload byte K b + off - 2t.  A piece may run into block b+1 (off > 239).
-// The piece's LDS reads (payload window, parity slots of blocks b and b + 1) and, separately, its
-// assembly: the tile loops issue all their pieces' reads before the first assembly (round 3), so
-// the LDS latencies overlap instead of adding up piece after piece.
-struct EncWin {
-    uint32_t d[5];
-    uint64_t P0, P1;
-};
 template <int T2>
-__device__ __forceinline__ EncWin enc_piece_load(const uint8_t* lds, uint32_t buf, uint32_t par, uint32_t p)
+__device__ __forceinline__ uint4 enc_piece(const uint8_t* lds, uint32_t buf, uint32_t par, uint32_t p)
 {
     constexpr uint32_t K = 255 - T2;
     const uint32_t j0 = p * 16u, b = j0 / 255u, off = j0 - 255u * b;
     const uint32_t S = buf + PAD + K * b + off - T2; // LDS byte of output byte 0's payload source
-    EncWin w;
-    lds_window(w.d, lds, S);
-    w.P0 = *(const uint64_t*)(lds + par + 8u * b);
-    w.P1 = *(const uint64_t*)(lds + par + 8u * b + 8u);
-    return w;
-}
-template <int T2>
-__device__ __forceinline__ uint4 enc_piece_make(const EncWin& w, uint32_t buf, uint32_t p)
-{
-    constexpr uint32_t K = 255 - T2;
-    const uint32_t j0 = p * 16u, b = j0 / 255u, off = j0 - 255u * b;
-    const uint32_t S = buf + PAD + K * b + off - T2;
     const uint32_t sh = (S & 3u) * 8u;
+    uint32_t d[5];
+    lds_window(d, lds, S);
     uint32_t X[4], Y[4];
 #pragma unroll
     for (int m = 0; m < 4; ++m)
-        X[m] = __builtin_amdgcn_alignbit(w.d[m + 1], w.d[m], sh);
+        X[m] = __builtin_amdgcn_alignbit(d[m + 1], d[m], sh);
     // after the block boundary the source runs 2t bytes behind: Y byte k = X byte k - 2t
     constexpr int q2 = T2 / 4, r2 = T2 % 4;
 #pragma unroll
@@ -482,8 +465,8 @@ __device__ __forceinline__ uint4 enc_piece_make(const EncWin& w, uint32_t buf, u
         Y[m] = r2 ? __builtin_amdgcn_alignbit(hi, lo, 16) : hi;
     }
     // parity bytes of blocks b and b+1, byte q at byte q
-    const uint64_t P0 = w.P0 >> (8 * (8 - T2));
-    const uint64_t P1 = w.P1 >> (8 * (8 - T2));
+    const uint64_t P0 = *(const uint64_t*)(lds + par + 8u * b) >> (8 * (8 - T2));
+    const uint64_t P1 = *(const uint64_t*)(lds + par + 8u * b + 8u) >> (8 * (8 - T2));
     const uint32_t kb = off > 239u ? 255u - off : 16u;    // first byte of block b+1 in the piece
     const uint32_t c0 = off < (uint32_t)T2 ? T2 - off : 0u; // leading parity bytes of block b
     // parity of b: bytes [0, c0) = P0 bytes off.. ; parity of b+1: bytes [kb, kb+2t) = P1 << 8 kb
@@ -506,33 +489,21 @@ __device__ __forceinline__ uint4 enc_piece_make(const EncWin& w, uint32_t buf, u
     }
     return make_uint4(o[0], o[1], o[2], o[3]);
 }
-template <int T2>
-__device__ __forceinline__ uint4 enc_piece(const uint8_t* lds, uint32_t buf, uint32_t par, uint32_t p)
-{
-    return enc_piece_make<T2>(enc_piece_load<T2>(lds, buf, par, p), buf, p);
-}
 
-struct DecWin {
-    uint32_t d[7];
-};
-template <int T2> __device__ __forceinline__ DecWin dec_piece_load(const uint8_t* lds, uint32_t buf, uint32_t p)
-{
-    constexpr uint32_t K = 255 - T2;
-    const uint32_t j0 = p * 16u, b = j0 / K, off = j0 - K * b;
-    DecWin w;
-    lds_window(w.d, lds, buf + PAD + 255u * b + T2 + off);
-    return w;
-}
-template <int T2> __device__ __forceinline__ uint4 dec_piece_make(const DecWin& w, uint32_t buf, uint32_t p)
+// Decode emission: 16 bytes of the payload tile at piece p from the (corrected) LDS codeword rows:
+// payload byte j of block b = j / K (off = j % K) is codeword byte 255 b + 2t + off.
+template <int T2> __device__ __forceinline__ uint4 dec_piece(const uint8_t* lds, uint32_t buf, uint32_t p)
 {
     constexpr uint32_t K = 255 - T2;
     const uint32_t j0 = p * 16u, b = j0 / K, off = j0 - K * b;
     const uint32_t S = buf + PAD + 255u * b + T2 + off;
     const uint32_t sh = (S & 3u) * 8u;
+    uint32_t d[7];
+    lds_window(d, lds, S);
     uint32_t X[6];
 #pragma unroll
     for (int m = 0; m < 6; ++m)
-        X[m] = __builtin_amdgcn_alignbit(w.d[m + 1], w.d[m], sh);
+        X[m] = __builtin_amdgcn_alignbit(d[m + 1], d[m], sh);
     // past the block end the source skips block b+1's 2t parity bytes: Z byte k = X byte k + 2t
     constexpr int q2 = T2 / 4, r2 = T2 % 4;
     const uint32_t kb = off > K - 16u ? K - off : 16u;
@@ -549,12 +520,6 @@ template <int T2> __device__ __forceinline__ uint4 dec_piece_make(const DecWin& 
         o[m] = bfi((uint32_t)(mz >> ((m & 1) * 32)), Z, X[m]);
     }
     return make_uint4(o[0], o[1], o[2], o[3]);
-}
-// Decode emission: 16 bytes of the payload tile at piece p from the (corrected) LDS codeword rows:
-// payload byte j of block b = j / K (off = j % K) is codeword byte 255 b + 2t + off.
-template <int T2> __device__ __forceinline__ uint4 dec_piece(const uint8_t* lds, uint32_t buf, uint32_t p)
-{
-    return dec_piece_make<T2>(dec_piece_load<T2>(lds, buf, p), buf, p);
 }
 
 template <int NT = 1> __device__ __forceinline__ void st_nt(uint8_t* dst, uint4 v)

@@ -69,20 +69,6 @@ __device__ __forceinline__ void vm_wait_exact(uint32_t n)
     }
 }
 
-// PPFS_TK_LEAD2 tickets: the atomic is issued from inline asm (the compiler does not track it, so it
-// never inserts a wait of its own -- with the loop unrolled by two it fell back to vmcnt(0), which
-// also waited for the wave's fresh stores and atomic); the caller waits with a counted vmcnt and
-// then ties the register (tk_arrived) before reading it.
-__device__ __forceinline__ void tk_take_asm(uint32_t& tk, uint32_t* ctr)
-{
-    asm volatile("global_atomic_inc %0, %1, %2, off sc0" : "=v"(tk) : "v"(ctr), "v"(0xFFFFFFFFu) : "memory");
-}
-__device__ __forceinline__ uint32_t tk_arrived(uint32_t& tk)
-{
-    asm volatile("" : "+v"(tk));
-    return tk;
-}
-
 // Wave 0 (64 lanes) copies the first BYTES of the table blob into LDS at 0 by LDS-DMA: no register
 // round trip, and its loads never share a queue with the DMA waves' tiles.  Caller: vmcnt(0).
 template <int BYTES>
@@ -158,12 +144,6 @@ __device__ uint64_t g_tk_trace_dec[4096 * 2 * TK_TRACE_N];
 #ifndef PPFS_ENC_ILP2
 #define PPFS_ENC_ILP2 0 // 1: remainder as two 32-byte chains per lane (phase_remainder NMAP = 7)
 #endif
-#ifndef PPFS_TK_LEAD2
-#define PPFS_TK_LEAD2 0 // 1: tickets taken two iterations before they are published (not one)
-#endif
-#ifndef PPFS_WG_EMIT_BATCH
-#define PPFS_WG_EMIT_BATCH 0 // 1: a tile's four emission pieces read LDS together, then assemble + store
-#endif
 #ifndef PPFS_WG_SLX
 #define PPFS_WG_SLX 1 // SLX last-step tables instead of the x^(64 s) maps (rs_wg.hpp seg_remainder); 0 = maps
 #endif
@@ -223,8 +203,6 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
                 tk_clear(ctr_clear, g.nx);
             const uint32_t t2 = atomicInc(my_ctr, 0xFFFFFFFFu) + 2u * g.gx; // the tile of iteration 2
             s_tk[2] = (uint32_t)tk_tile(t2, g, nfull);
-            if constexpr (PPFS_TK_LEAD2)
-                s_tk[3] = (uint32_t)tk_tile(atomicInc(my_ctr, 0xFFFFFFFFu) + 2u * g.gx, g, nfull); // iteration 3
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // tables landed, ticket returned
     }
@@ -233,13 +211,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
     barrier_lds();
     PPFS_TK_MARK(0);
     uint32_t cur = 0, pc = 0, iter = 0;
-    // tk: the ticket this iteration takes; tk_prev: the one the previous iteration took (PPFS_TK_LEAD2:
-    // published at the end of this iteration, two iterations after its atomic went out; the loop then
-    // runs two iterations per trip so that the two registers keep fixed roles -- a register copy
-    // would make the compiler wait for the atomic one iteration early)
-    uint32_t tka, tkb; // no initial value: writing them outside wave 0's branch would make every wave
-                       // wait for the pending tickets (the compiler tracks pending writes per register)
-    auto body = [&](uint32_t& tk, uint32_t& tk_prev) {
+    while (q0 < nfull) {
         // A: tile q0 in LDS, the last emission reads done, the next ticket published (the first
         // pass: tables, parity slots and the iteration-2 ticket in place)
         if (iter) {
@@ -247,12 +219,11 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
             PPFS_TK_MARK(6);
         }
         const uint64_t ahead = __builtin_amdgcn_readfirstlane(s_tk[(iter + 2u) & 3u]);
-        if (tk_lane) {
-            if constexpr (PPFS_TK_LEAD2)
-                tk_take_asm(tk, my_ctr); // the tile of iteration iter + 4
-            else
-                tk = atomicInc(my_ctr, 0xFFFFFFFFu); // the tile of iteration iter + 3
-        }
+        // no initial value: writing the register outside wave 0's branch would make every wave wait
+        // for the previous ticket (the compiler tracks its pending write per register)
+        uint32_t tk;
+        if (tk_lane)
+            tk = atomicInc(my_ctr, 0xFFFFFFFFu); // the tile of iteration iter + 3
         const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + pc * 512u;
         const bool go = ahead < nfull;
         if (dmaw && go)
@@ -267,28 +238,12 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
         barrier_lds(); // B: parity slots complete
         PPFS_TK_MARK(3);
         uint8_t* dst = raw + q0 * (TB * 255);
-        if constexpr (PPFS_WG_EMIT_BATCH) {
-            // every piece's LDS reads first, then the assemblies and stores (latencies overlap)
-            EncWin w[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
-                w[k] = enc_piece_load<T2>(lds, buf, par, tid + 256u * k);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t p = tid + 256u * k;
-                const uint4 o = enc_piece_make<T2>(w[k], buf, p);
-                if ((k < 3 || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, raw, nblocks * 255u))
-                    st_nt<NTST>(dst + 16u * p, o);
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t p = tid + 256u * k;
-                const uint4 o = enc_piece<T2>(lds, buf, par, p);
-                if ((k < 3 || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, raw, nblocks * 255u))
-                    st_nt<NTST>(dst + 16u * p, o);
-            }
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t p = tid + 256u * k;
+            const uint4 o = enc_piece<T2>(lds, buf, par, p);
+            if ((k < 3 || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, raw, nblocks * 255u))
+                st_nt<NTST>(dst + 16u * p, o);
         }
         ++iter;
         PPFS_TK_MARK(4);
@@ -298,37 +253,13 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
             const uint32_t st = 4u * (iter < 2u ? iter : 2u);
             vm_wait_exact(st + kd * (hist & 1u));
         }
-        if constexpr (PPFS_TK_LEAD2) {
-            // the ticket of (iteration iter - 2) + 4 (iteration 3's: the prologue).  Wave 0 issued after
-            // its atomic at least: 4 stores of that iteration, this iteration's atomic and 4 stores
-            if (wave == 0 && iter >= 2u) {
-                vm_wait_exact(9u);
-                if (lane == 0)
-                    s_tk[(iter + 2u) & 3u] = (uint32_t)tk_tile(tk_arrived(tk_prev) + 2u * g.gx, g, nfull);
-            }
-        } else {
-            (void)tk_prev;
-            if (tk_lane)
-                s_tk[(iter + 2u) & 3u] = (uint32_t)tk_tile(tk + 2u * g.gx, g, nfull); // the tile of (iteration iter - 1) + 3
-        }
+        if (tk_lane)
+            s_tk[(iter + 2u) & 3u] = (uint32_t)tk_tile(tk + 2u * g.gx, g, nfull); // the tile of (iteration iter - 1) + 3
         PPFS_TK_MARK(5);
         cur = ring_add(cur, 1, NBUF);
         pc ^= 1u;
         q0 = q1;
         q1 = ahead;
-    };
-    if constexpr (PPFS_TK_LEAD2) {
-        while (q0 < nfull) {
-            body(tka, tkb);
-            if (q0 >= nfull)
-                break;
-            body(tkb, tka);
-        }
-        if (wave == 0) // tickets still in flight land in tka / tkb: drain before those registers are reused
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(tka), "+v"(tkb)::"memory");
-    } else {
-        while (q0 < nfull)
-            body(tka, tkb);
     }
     if (q0 == nfull && nfull < ntiles) { // the partial tile
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -416,27 +347,21 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
             if (blockIdx.x == 0)
                 tk_clear(ctr_clear, g.nx);
             s_tk[1] = (uint32_t)tk_tile(atomicInc(my_ctr, 0xFFFFFFFFu) + g.gx, g, nfull); // the tile of iteration 1
-            if constexpr (PPFS_TK_LEAD2)
-                s_tk[2] = (uint32_t)tk_tile(atomicInc(my_ctr, 0xFFFFFFFFu) + g.gx, g, nfull); // iteration 2
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // tile q0 / tables and the ticket landed
     barrier_lds();
     PPFS_TK_MARK(0);
     uint32_t cur = 0, pc = 0, iter = 0;
-    uint32_t tka, tkb; // (see the encode)
-    auto body = [&](uint32_t& tk, uint32_t& tk_prev) {
+    while (q0 < nfull) {
         if (iter) {
             barrier_lds(); // A: tile q0 in LDS, the last emission reads done, the next ticket published
             PPFS_TK_MARK(7);
         }
         const uint64_t q1 = __builtin_amdgcn_readfirstlane(s_tk[(iter + 1u) & 3u]);
-        if (tk_lane) {
-            if constexpr (PPFS_TK_LEAD2)
-                tk_take_asm(tk, my_ctr); // the tile of iteration iter + 3
-            else
-                tk = atomicInc(my_ctr, 0xFFFFFFFFu); // the tile of iteration iter + 2
-        }
+        uint32_t tk; // no initial value (see the encode)
+        if (tk_lane)
+            tk = atomicInc(my_ctr, 0xFFFFFFFFu); // the tile of iteration iter + 2
         const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + pc * 512u;
         if (dmaw && q1 < nfull)
             dma_tile192<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, raw + q1 * (TB * 255), tid, raw,
@@ -457,27 +382,12 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         PPFS_TK_MARK(4);
         if (want) {
             uint8_t* dst = data + q0 * (TB * K);
-            if constexpr (PPFS_WG_EMIT_BATCH) {
-                DecWin w[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    w[k] = dec_piece_load<T2>(lds, buf, tid + 256u * k);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t p = tid + 256u * k;
-                    const uint4 o = dec_piece_make<T2>(w[k], buf, p);
-                    if ((k < 3 || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, data, nblocks * K))
-                        st_nt<NTST>(dst + 16u * p, o);
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t p = tid + 256u * k;
-                    const uint4 o = dec_piece<T2>(lds, buf, p);
-                    if ((k < 3 || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, data, nblocks * K))
-                        st_nt<NTST>(dst + 16u * p, o);
-                }
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t p = tid + 256u * k;
+                const uint4 o = dec_piece<T2>(lds, buf, p);
+                if ((k < 3 || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, data, nblocks * K))
+                    st_nt<NTST>(dst + 16u * p, o);
             }
         }
         ++iter;
@@ -488,36 +398,12 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
             else
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        if constexpr (PPFS_TK_LEAD2) {
-            // the ticket of (iteration iter - 2) + 3 (iteration 2's: the prologue).  Wave 0 issued after
-            // its atomic at least this iteration's atomic and, with payload output, 2 x 4 stores
-            if (wave == 0 && iter >= 2u) {
-                vm_wait_exact(want ? 9u : 1u);
-                if (lane == 0)
-                    s_tk[(iter + 1u) & 3u] = (uint32_t)tk_tile(tk_arrived(tk_prev) + g.gx, g, nfull);
-            }
-        } else {
-            (void)tk_prev;
-            if (tk_lane)
-                s_tk[(iter + 1u) & 3u] = (uint32_t)tk_tile(tk + g.gx, g, nfull); // the tile of (iteration iter - 1) + 2
-        }
+        if (tk_lane)
+            s_tk[(iter + 1u) & 3u] = (uint32_t)tk_tile(tk + g.gx, g, nfull); // the tile of (iteration iter - 1) + 2
         PPFS_TK_MARK(6);
         cur ^= 1u;
         pc ^= 1u;
         q0 = q1;
-    };
-    if constexpr (PPFS_TK_LEAD2) {
-        while (q0 < nfull) {
-            body(tka, tkb);
-            if (q0 >= nfull)
-                break;
-            body(tkb, tka);
-        }
-        if (wave == 0) // tickets still in flight land in tka / tkb: drain before those registers are reused
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(tka), "+v"(tkb)::"memory");
-    } else {
-        while (q0 < nfull)
-            body(tka, tkb);
     }
     if (q0 == nfull && nfull < ntiles) { // the partial tile
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
