@@ -212,3 +212,38 @@ def test_debug_copy_checks_positive_control():
         assert v == -1 and _native.debug_dma_rejects() is None
     else:
         assert v == 1, v
+
+
+@pytest.mark.parametrize("bs,t", [(512, 3), (4096, 16), (4096, 0)], ids=["rs_t3", "rs_t16", "hamming4096"])
+def test_time_next_launch_records_the_kernel(bs, t):
+    """ppfs_ecc_time_next_launch: the next engine kernel records both events from its dispatch
+    packet (a positive duration no longer than the stream-event bracket around the call), the hook
+    disarms after one launch, and the launch it timed computes the same codewords as an untimed one."""
+    from bench import HipEvents
+    from paritypartyfs_amd import ECC_HAMMING
+
+    typ = ECC_REED_SOLOMON if t else ECC_HAMMING
+    eng = EccEngine(typ, bs, t)
+    n, k, nb = eng.raw_block_size, eng.data_size, 1 << 15
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream()
+    data = torch.randint(0, 256, (nb * k,), dtype=torch.uint8, device=dev)
+    ref = torch.zeros(nb * n, dtype=torch.uint8, device=dev)
+    cw = torch.zeros_like(ref)
+    eng.encode(data, ref, nblocks=nb)
+    L = _native.lib()
+    ev = HipEvents(4)
+    ev.record(0, stream)
+    assert L.ppfs_ecc_time_next_launch(ev.ev[2], ev.ev[3]) == 0
+    eng.encode(data, cw, nblocks=nb)
+    ev.record(1, stream)
+    torch.cuda.synchronize()
+    kernel_ms, bracket_ms = ev.ms(2, 3), ev.ms(0, 1)
+    assert 0.0 < kernel_ms <= bracket_ms + 1e-3
+    assert torch.equal(cw, ref)
+    # disarmed: a second launch records nothing new (the stop event keeps its timestamp)
+    eng.encode(data, cw, nblocks=nb)
+    torch.cuda.synchronize()
+    assert ev.ms(2, 3) == kernel_ms
+    ev.close()
+    eng.close()

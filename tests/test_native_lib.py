@@ -98,3 +98,10 @@ def test_inject_rejects_bad_buffers_without_gpu(lib):
     assert lib.ppfs_inject_device(buf, 0, 4, buf, buf, 0, None) < 0  # zero stride
     assert lib.ppfs_inject_device(buf, 16, 4, buf, buf, 2, None) < 0  # unknown mode
     assert lib.ppfs_inject_device(None, 255, 0, None, None, 0, None) == 0  # nothing to do
+
+
+def test_time_next_launch_arguments_without_gpu(lib):
+    """The timing hook (bench.py's dispatch-packet kernel times) needs both events or neither."""
+    assert lib.ppfs_ecc_time_next_launch(ctypes.c_void_p(1), None) == -22  # -EINVAL
+    assert lib.ppfs_ecc_time_next_launch(None, ctypes.c_void_p(1)) == -22
+    assert lib.ppfs_ecc_time_next_launch(None, None) == 0
