@@ -51,6 +51,8 @@ hipError_t ppfs_rs_generic_decode(uint8_t* r, uint8_t* d, uint8_t* st, uint8_t* 
     int wb, const uint8_t* tab, hipStream_t s);
 int ppfs_crc_tables_bytes(void);
 int ppfs_crc_fast_tables_bytes(void);
+int ppfs_crc_fast_lane_maps(void);
+int ppfs_crc_fast_six_maps(void);
 int ppfs_crc_fast_supported(uint32_t bs, uint32_t n);
 int ppfs_bitfast_supported(uint32_t bs);
 hipError_t ppfs_crc_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs, uint32_t ds,
@@ -428,7 +430,8 @@ std::vector<uint8_t> build_crc_tables(uint64_t P, int n, uint32_t ds)
 
 // Maps of the CRC fast path (bit_fast.hip, n <= 32): 8 nibble tables x 16 u32 entries each,
 // T[i][v] = (v << 4i) * C mod P for a constant C = x^e mod P.  Maps: x^0, x^32, x^64, x^96 (piece
-// dwords), x^8192 (one lane's pieces, 1 KiB apart), x^(128 2^j) j < 6 (lane tree), then the final
+// dwords), x^8192 (one lane's pieces, 1 KiB apart), x^(128 2^j) j < 6 (lane tree; the kernels use
+// j = 4, 5 after the lane maps below), then the final
 // factor placing the zero-padded 16-byte grid: encode x^(8 (ds + m - 1024 (NP + 1)) + n - 1) for
 // each payload misalignment m < 16, check x^(8 (ds - bs) + n - 1).
 std::vector<uint8_t> build_crc_fast_tables(uint64_t P, int n, uint32_t ds, uint32_t bs)
@@ -449,6 +452,30 @@ std::vector<uint8_t> build_crc_fast_tables(uint64_t P, int n, uint32_t ds, uint3
         for (int i = 0; i < 8; ++i)
             for (int v = 0; v < 16; ++v)
                 t[(mi * 8 + i) * 16 + v] = (uint32_t)c.mul(c.mod((uint64_t)v << (4 * i)), C);
+    }
+    // lane maps: lane b of NL = 16 multiplies by x^(128 (NL - 1 - b)), transposed: dword (16 i + v) NL + b
+    const int NL = ppfs_crc_fast_lane_maps();
+    uint32_t* lt = t + ex.size() * 8 * 16;
+    for (int b = 0; b < NL; ++b) {
+        const uint64_t C = c.xpow(128L * (NL - 1 - b));
+        for (int i = 0; i < 8; ++i)
+            for (int v = 0; v < 16; ++v)
+                lt[(16 * i + v) * NL + b] = (uint32_t)c.mul(c.mod((uint64_t)v << (4 * i)), C);
+    }
+    // 6-bit tables of the hot maps (bit_fast.hip PPFS_CRC_SIX): x^0, x^32, x^64, x^96, x^8192,
+    // x^2048, x^4096; sub-table j < 5 = 64 entries (v << 6j) C, then 4 entries (v << 30) C
+    if (ppfs_crc_fast_six_maps() > 0) {
+        uint8_t* st = (uint8_t*)(lt + 8 * 16 * NL);
+        const long sx[7] = { ex[0], ex[1], ex[2], ex[3], ex[4], ex[9], ex[10] };
+        for (int q = 0; q < 7; ++q, st += 5 * 256 + 16) {
+            const uint64_t C = c.xpow(sx[q]);
+            uint32_t* e = (uint32_t*)st;
+            for (int j = 0; j < 5; ++j)
+                for (int v = 0; v < 64; ++v)
+                    e[64 * j + v] = (uint32_t)c.mul(c.mod((uint64_t)v << (6 * j)), C);
+            for (int v = 0; v < 4; ++v)
+                e[320 + v] = (uint32_t)c.mul(c.mod((uint64_t)v << 30), C);
+        }
     }
     return out;
 }

@@ -690,13 +690,29 @@ __global__ __launch_bounds__(256) void parity_fast_check_kernel(const uint8_t* _
 // closed form in DESIGN.md / SURVEY.md §0.4).  Everything is a linear map of 32-bit values mod P,
 // done with nibble tables ("cmap": 8 LDS lookups of u32, every lane reading the same table):
 //   piece (16 B = dwords D0..D3, big-endian) -> D0 x^96 + D1 x^64 + D2 x^32 + D3 mod P;
-//   a lane's pieces (1 KiB apart) by Horner with x^8192; the 64 lanes by a 6-level tree with
-//   x^(128 2^j); then one block-uniform factor x^e that places the zero-padded 16-byte grid at the
-//   payload's real position (e < 0 uses x^-1: P(0) = 1).
+//   a lane's pieces (1 KiB apart) by Horner with x^8192; the 64 lanes: lane l by its own map
+//   x^(128 (15 - l % 16)), an XOR over each row of 16 lanes (DPP), then two tree levels x^2048,
+//   x^4096 over the 4 rows; then one block-uniform factor x^e that places the zero-padded 16-byte
+//   grid at the payload's real position (e < 0 uses x^-1: P(0) = 1).
 // ------------------------------------------------------------------------------------
 constexpr int CF_MAP = 512;                      // 8 nibbles x 16 entries x u32
 constexpr int CF_M0 = 0, CF_K = 4, CF_L = 5, CF_FENC = 11, CF_FCHK = 27, CF_NMAPS = 28;
-constexpr int CF_BYTES = CF_NMAPS * CF_MAP;     // 14 KiB
+// The 16 lane maps sit transposed after the CF_NMAPS maps: dword (16 i + v) x 16 + (lane % 16) =
+// entry v of nibble table i, so the lanes of a row read 16 different banks.  (Round 3, r3z: the lane
+// tree's 6 dependent maps become 1 + 2; 64 per-lane maps, 32 KiB, cost a workgroup per CU.)
+constexpr int CF_LANES = 16;
+constexpr int CF_LANE_OFF = CF_NMAPS * CF_MAP;
+// PPFS_CRC_SIX: the hot maps (piece dwords, Horner, the two tree levels) as 6-bit tables (5 x 64
+// entries + 4; a 64-entry u32 table fills each bank once, so any indices are conflict-free): 6 LDS
+// lookups per map instead of 8.  Stored after the lane maps, CF_MAP6 bytes each, in the order
+// M0..M3, K, L+4, L+5.
+#ifndef PPFS_CRC_SIX
+#define PPFS_CRC_SIX 0
+#endif
+constexpr int CF_MAP6 = 5 * 256 + 16;
+constexpr int CF_NSIX = PPFS_CRC_SIX ? 7 : 0;
+constexpr int CF_SIX_OFF = CF_NMAPS * CF_MAP + CF_LANES * CF_MAP;
+constexpr int CF_BYTES = CF_SIX_OFF + CF_NSIX * CF_MAP6; // 22 KiB (+ 8.9 KiB)
 // Blocks per wave of the CRC kernels: a workgroup stages the 14 KiB of maps once and then walks
 // CRC_BPW consecutive 4-block groups (one contiguous range, so the full grid keeps its address
 // order); with one group per workgroup the map staging read as much L2 as the blocks themselves.
@@ -741,6 +757,32 @@ __device__ __forceinline__ uint32_t cmap(const uint8_t* tb, uint32_t v)
         __builtin_amdgcn_bitop3_b32(e[3], e[4], e[5], 0x96), e[6] ^ e[7], 0x96);
 }
 
+#ifndef PPFS_CRC_RMASK
+#define PPFS_CRC_RMASK 0 // 1: crc_piece's byte mask from 64-bit shifts
+#endif
+
+// v(x) * C mod P from C's 6-bit tables (PPFS_CRC_SIX)
+__device__ __forceinline__ uint32_t cmap6(const uint8_t* tb, uint32_t v)
+{
+    uint32_t e[6];
+#pragma unroll
+    for (int j = 0; j < 5; ++j)
+        e[j] = *(const uint32_t*)(tb + j * 256 + (__builtin_amdgcn_ubfe(v, 6 * j, 6) << 2));
+    e[5] = *(const uint32_t*)(tb + 1280 + ((v >> 30) << 2));
+    return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(e[0], e[1], e[2], 0x96), e[3], e[4] ^ e[5], 0x96);
+}
+// a hot map: mi = CF_M0 .. CF_M0 + 3, CF_K, CF_L + 4, CF_L + 5
+template <int MI> __device__ __forceinline__ uint32_t hmap(const uint8_t* tbl, uint32_t v)
+{
+    if constexpr (CF_NSIX > 0) {
+        constexpr int SI = MI <= CF_K ? MI : MI - CF_L + 1; // 0..4, then 5, 6
+        static_assert(SI >= 0 && SI < 7, "hot maps only");
+        return cmap6(tbl + CF_SIX_OFF + SI * CF_MAP6, v);
+    } else {
+        return cmap(tbl + MI * CF_MAP, v);
+    }
+}
+
 struct CrcFast {
     uint32_t bs, ds, n, nbc, mask;
     uint64_t data_bytes;
@@ -751,6 +793,16 @@ __device__ __forceinline__ uint32_t crc_piece(const uint8_t* tbl, uint4 v, uint3
 {
     uint32_t w[4] = { v.x, v.y, v.z, v.w };
     if (lo > 0 || hi < 16) {
+#if PPFS_CRC_RMASK
+        // bytes [lo, hi) as two 64-bit masks (a handful of shifts instead of 16 byte compares)
+        auto ge = [](uint32_t b) { return b >= 8u ? 0ull : (~0ull << (8u * b)); }; // bytes >= b of 8
+        const uint64_t m0 = ge(lo) & ~ge(hi);
+        const uint64_t m1 = ge(lo > 8u ? lo - 8u : 0u) & ~ge(hi > 8u ? hi - 8u : 0u);
+        w[0] &= (uint32_t)m0;
+        w[1] &= (uint32_t)(m0 >> 32);
+        w[2] &= (uint32_t)m1;
+        w[3] &= (uint32_t)(m1 >> 32);
+#else
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             uint32_t keep = 0;
@@ -759,26 +811,50 @@ __device__ __forceinline__ uint32_t crc_piece(const uint8_t* tbl, uint4 v, uint3
                 keep |= (4u * u + b >= lo && 4u * u + b < hi) ? (0xFFu << (8 * b)) : 0u;
             w[u] &= keep;
         }
+#endif
     }
     const uint32_t d3 = bswap(w[3]);
-    return __builtin_amdgcn_bitop3_b32(cmap(tbl + 3 * CF_MAP, bswap(w[0])), cmap(tbl + 2 * CF_MAP, bswap(w[1])),
-               cmap(tbl + 1 * CF_MAP, bswap(w[2])), 0x96)
-        ^ (n32 ? d3 : cmap(tbl + CF_M0 * CF_MAP, d3));
+    return __builtin_amdgcn_bitop3_b32(hmap<CF_M0 + 3>(tbl, bswap(w[0])), hmap<CF_M0 + 2>(tbl, bswap(w[1])),
+               hmap<CF_M0 + 1>(tbl, bswap(w[2])), 0x96)
+        ^ (n32 ? d3 : hmap<CF_M0>(tbl, d3));
 }
 
-// Sum over the wave of value_l * x^(128 (63 - l)) -> wave-uniform
-__device__ __forceinline__ uint32_t crc_lane_tree(const uint8_t* tbl, uint32_t acc)
+// value * x^(128 (15 - lane % 16)) mod P from the transposed lane maps
+__device__ __forceinline__ uint32_t lane_cmap(const uint8_t* tbl, uint32_t v, uint32_t lane)
 {
+    const uint8_t* tb = tbl + CF_LANE_OFF + 4u * (lane & (CF_LANES - 1));
+    uint32_t e[8];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-        const uint32_t other = __shfl_down(acc, 1 << j, 64);
-        acc = cmap(tbl + (CF_L + j) * CF_MAP, acc) ^ other;
-    }
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)acc);
+    for (int i = 0; i < 8; ++i)
+        e[i] = *(const uint32_t*)(tb + i * 64 * CF_LANES + (__builtin_amdgcn_ubfe(v, 4 * i, 4) << 6));
+    return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(e[0], e[1], e[2], 0x96),
+        __builtin_amdgcn_bitop3_b32(e[3], e[4], e[5], 0x96), e[6] ^ e[7], 0x96);
 }
+
+// Sum over the wave of value_l * x^(128 (63 - l)) -> wave-uniform: each lane's row factor, the row
+// XOR (DPP butterfly: every lane of row r ends with R_r), then R_0 x^6144 + R_1 x^4096 + R_2 x^2048 + R_3
+// by two tree levels (the maps x^(128 2^j), j = 4, 5)
+__device__ __forceinline__ uint32_t crc_lane_sum(const uint8_t* tbl, uint32_t acc, uint32_t lane)
+{
+    uint32_t v = lane_cmap(tbl, acc, lane);
+    v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false); // row_half_mirror
+    v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false); // row_mirror
+#pragma unroll
+    for (int j = 4; j < 6; ++j) {
+        const uint32_t other = __shfl_down(v, 1 << j, 64);
+        v = (j == 4 ? hmap<CF_L + 4>(tbl, v) : hmap<CF_L + 5>(tbl, v)) ^ other;
+    }
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+// The lane maps put the encode kernel at 131 VGPRs: the floor keeps 4 waves per SIMD (128, no
+// spills; r3z A/B 1.64 vs 1.68 ms encode, 1.660 vs 1.668 check)
+#define PPFS_CRC_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 
 template <int NP>
-__global__ __launch_bounds__(256) void crc_fast_encode_kernel(const uint8_t* __restrict__ data,
+__global__ __launch_bounds__(256) PPFS_CRC_ATTR void crc_fast_encode_kernel(const uint8_t* __restrict__ data,
     uint8_t* __restrict__ raw, const uint8_t* __restrict__ skip, uint64_t nblocks_all, CrcFast a,
     const uint8_t* __restrict__ tables)
 {
@@ -811,9 +887,9 @@ __global__ __launch_bounds__(256) void crc_fast_encode_kernel(const uint8_t* __r
             const uint32_t lo_c = lo < 0 ? 0u : (lo > 16 ? 16u : (uint32_t)lo);
             const uint32_t hi_c = hi < 0 ? 0u : (hi > 16 ? 16u : (uint32_t)hi);
             const uint32_t pv = crc_piece(tbl, cur.v[k], lo_c, hi_c > lo_c ? hi_c : lo_c, n32);
-            acc = k == 0 ? pv : (cmap(tbl + CF_K * CF_MAP, acc) ^ pv);
+            acc = k == 0 ? pv : (hmap<CF_K>(tbl, acc) ^ pv);
         }
-        const uint32_t Vs = crc_lane_tree(tbl, acc);
+        const uint32_t Vs = crc_lane_sum(tbl, acc, lane);
         const uint32_t V = cmap(tbl + (CF_FENC + m) * CF_MAP, Vs);
         const uint32_t st = (V << 1) & a.mask;
         if (!(skip && PPFS_DBG_OK(skip + blk, 1, skip, nblocks_all) && skip[blk] == 5)) {
@@ -860,7 +936,7 @@ __global__ __launch_bounds__(256) void crc_fast_encode_kernel(const uint8_t* __r
 }
 
 template <int NP>
-__global__ __launch_bounds__(256) void crc_fast_check_kernel(const uint8_t* __restrict__ raw,
+__global__ __launch_bounds__(256) PPFS_CRC_ATTR void crc_fast_check_kernel(const uint8_t* __restrict__ raw,
     uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks_all, CrcFast a,
     const uint8_t* __restrict__ tables)
 {
@@ -893,9 +969,9 @@ __global__ __launch_bounds__(256) void crc_fast_check_kernel(const uint8_t* __re
             const int32_t hi = (int32_t)ds - q16;
             const uint32_t hi_c = hi < 0 ? 0u : (hi > 16 ? 16u : (uint32_t)hi);
             const uint32_t pv = crc_piece(tbl, R[k], 0u, hi_c, n32);
-            acc = k == 0 ? pv : (cmap(tbl + CF_K * CF_MAP, acc) ^ pv);
+            acc = k == 0 ? pv : (hmap<CF_K>(tbl, acc) ^ pv);
         }
-        const uint32_t Vs = crc_lane_tree(tbl, acc);
+        const uint32_t Vs = crc_lane_sum(tbl, acc, lane);
         const uint32_t V = cmap(tbl + CF_FCHK * CF_MAP, Vs);
         const uint32_t st = (V << 1) & a.mask;
         // stored field: n bits MSB first from byte ds (in the last raw piece, lane 63)
@@ -1003,6 +1079,8 @@ extern "C" hipError_t ppfs_ham_fast_decode(uint8_t* r, uint8_t* d, uint8_t* st, 
 }
 
 extern "C" int ppfs_crc_fast_tables_bytes(void) { return bf::CF_BYTES; }
+extern "C" int ppfs_crc_fast_lane_maps(void) { return bf::CF_LANES; }
+extern "C" int ppfs_crc_fast_six_maps(void) { return bf::CF_NSIX; }
 
 extern "C" hipError_t ppfs_crc_fast_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs,
     uint32_t ds, uint32_t n, uint64_t mask, const uint8_t* tab, hipStream_t s)
