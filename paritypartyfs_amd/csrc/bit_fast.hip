@@ -702,12 +702,13 @@ constexpr int CF_M0 = 0, CF_K = 4, CF_L = 5, CF_FENC = 11, CF_FCHK = 27, CF_NMAP
 // tree's 6 dependent maps become 1 + 2; 64 per-lane maps, 32 KiB, cost a workgroup per CU.)
 constexpr int CF_LANES = 16;
 constexpr int CF_LANE_OFF = CF_NMAPS * CF_MAP;
-// PPFS_CRC_SIX: the hot maps (piece dwords, Horner, the two tree levels) as 6-bit tables (5 x 64
+// The encode's hot maps (piece dwords, Horner, the two tree levels) also as 6-bit tables (5 x 64
 // entries + 4; a 64-entry u32 table fills each bank once, so any indices are conflict-free): 6 LDS
 // lookups per map instead of 8.  Stored after the lane maps, CF_MAP6 bytes each, in the order
-// M0..M3, K, L+4, L+5.
+// M0..M3, K, L+4, L+5.  (r3zc A/B: encode -1 %; the check kernel, 5 waves per SIMD with them, ran
+// 0.8 % slower, so it keeps the nibble maps and stages only the first CF_SIX_OFF bytes.)
 #ifndef PPFS_CRC_SIX
-#define PPFS_CRC_SIX 0
+#define PPFS_CRC_SIX 1
 #endif
 constexpr int CF_MAP6 = 5 * 256 + 16;
 constexpr int CF_NSIX = PPFS_CRC_SIX ? 7 : 0;
@@ -757,10 +758,6 @@ __device__ __forceinline__ uint32_t cmap(const uint8_t* tb, uint32_t v)
         __builtin_amdgcn_bitop3_b32(e[3], e[4], e[5], 0x96), e[6] ^ e[7], 0x96);
 }
 
-#ifndef PPFS_CRC_RMASK
-#define PPFS_CRC_RMASK 0 // 1: crc_piece's byte mask from 64-bit shifts
-#endif
-
 // v(x) * C mod P from C's 6-bit tables (PPFS_CRC_SIX)
 __device__ __forceinline__ uint32_t cmap6(const uint8_t* tb, uint32_t v)
 {
@@ -772,9 +769,9 @@ __device__ __forceinline__ uint32_t cmap6(const uint8_t* tb, uint32_t v)
     return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(e[0], e[1], e[2], 0x96), e[3], e[4] ^ e[5], 0x96);
 }
 // a hot map: mi = CF_M0 .. CF_M0 + 3, CF_K, CF_L + 4, CF_L + 5
-template <int MI> __device__ __forceinline__ uint32_t hmap(const uint8_t* tbl, uint32_t v)
+template <int MI, bool SIX> __device__ __forceinline__ uint32_t hmap(const uint8_t* tbl, uint32_t v)
 {
-    if constexpr (CF_NSIX > 0) {
+    if constexpr (SIX && CF_NSIX > 0) {
         constexpr int SI = MI <= CF_K ? MI : MI - CF_L + 1; // 0..4, then 5, 6
         static_assert(SI >= 0 && SI < 7, "hot maps only");
         return cmap6(tbl + CF_SIX_OFF + SI * CF_MAP6, v);
@@ -789,11 +786,11 @@ struct CrcFast {
 };
 
 // 16 payload bytes (memory order) -> piece value mod P; bytes outside [lo, hi) count as zero
+template <bool SIX>
 __device__ __forceinline__ uint32_t crc_piece(const uint8_t* tbl, uint4 v, uint32_t lo, uint32_t hi, bool n32)
 {
     uint32_t w[4] = { v.x, v.y, v.z, v.w };
     if (lo > 0 || hi < 16) {
-#if PPFS_CRC_RMASK
         // bytes [lo, hi) as two 64-bit masks (a handful of shifts instead of 16 byte compares)
         auto ge = [](uint32_t b) { return b >= 8u ? 0ull : (~0ull << (8u * b)); }; // bytes >= b of 8
         const uint64_t m0 = ge(lo) & ~ge(hi);
@@ -802,21 +799,11 @@ __device__ __forceinline__ uint32_t crc_piece(const uint8_t* tbl, uint4 v, uint3
         w[1] &= (uint32_t)(m0 >> 32);
         w[2] &= (uint32_t)m1;
         w[3] &= (uint32_t)(m1 >> 32);
-#else
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            uint32_t keep = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                keep |= (4u * u + b >= lo && 4u * u + b < hi) ? (0xFFu << (8 * b)) : 0u;
-            w[u] &= keep;
-        }
-#endif
     }
     const uint32_t d3 = bswap(w[3]);
-    return __builtin_amdgcn_bitop3_b32(hmap<CF_M0 + 3>(tbl, bswap(w[0])), hmap<CF_M0 + 2>(tbl, bswap(w[1])),
-               hmap<CF_M0 + 1>(tbl, bswap(w[2])), 0x96)
-        ^ (n32 ? d3 : hmap<CF_M0>(tbl, d3));
+    return __builtin_amdgcn_bitop3_b32(hmap<CF_M0 + 3, SIX>(tbl, bswap(w[0])), hmap<CF_M0 + 2, SIX>(tbl, bswap(w[1])),
+               hmap<CF_M0 + 1, SIX>(tbl, bswap(w[2])), 0x96)
+        ^ (n32 ? d3 : hmap<CF_M0, SIX>(tbl, d3));
 }
 
 // value * x^(128 (15 - lane % 16)) mod P from the transposed lane maps
@@ -834,6 +821,7 @@ __device__ __forceinline__ uint32_t lane_cmap(const uint8_t* tbl, uint32_t v, ui
 // Sum over the wave of value_l * x^(128 (63 - l)) -> wave-uniform: each lane's row factor, the row
 // XOR (DPP butterfly: every lane of row r ends with R_r), then R_0 x^6144 + R_1 x^4096 + R_2 x^2048 + R_3
 // by two tree levels (the maps x^(128 2^j), j = 4, 5)
+template <bool SIX>
 __device__ __forceinline__ uint32_t crc_lane_sum(const uint8_t* tbl, uint32_t acc, uint32_t lane)
 {
     uint32_t v = lane_cmap(tbl, acc, lane);
@@ -844,7 +832,7 @@ __device__ __forceinline__ uint32_t crc_lane_sum(const uint8_t* tbl, uint32_t ac
 #pragma unroll
     for (int j = 4; j < 6; ++j) {
         const uint32_t other = __shfl_down(v, 1 << j, 64);
-        v = (j == 4 ? hmap<CF_L + 4>(tbl, v) : hmap<CF_L + 5>(tbl, v)) ^ other;
+        v = (j == 4 ? hmap<CF_L + 4, SIX>(tbl, v) : hmap<CF_L + 5, SIX>(tbl, v)) ^ other;
     }
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
@@ -852,9 +840,13 @@ __device__ __forceinline__ uint32_t crc_lane_sum(const uint8_t* tbl, uint32_t ac
 // The lane maps put the encode kernel at 131 VGPRs: the floor keeps 4 waves per SIMD (128, no
 // spills; r3z A/B 1.64 vs 1.68 ms encode, 1.660 vs 1.668 check)
 #define PPFS_CRC_ATTR __attribute__((amdgpu_waves_per_eu(4)))
+#ifndef PPFS_CRC_ENC_WPE
+#define PPFS_CRC_ENC_WPE 4
+#endif
+#define PPFS_CRC_ENC_ATTR __attribute__((amdgpu_waves_per_eu(PPFS_CRC_ENC_WPE)))
 
 template <int NP>
-__global__ __launch_bounds__(256) PPFS_CRC_ATTR void crc_fast_encode_kernel(const uint8_t* __restrict__ data,
+__global__ __launch_bounds__(256) PPFS_CRC_ENC_ATTR void crc_fast_encode_kernel(const uint8_t* __restrict__ data,
     uint8_t* __restrict__ raw, const uint8_t* __restrict__ skip, uint64_t nblocks_all, CrcFast a,
     const uint8_t* __restrict__ tables)
 {
@@ -886,10 +878,10 @@ __global__ __launch_bounds__(256) PPFS_CRC_ATTR void crc_fast_encode_kernel(cons
             const int32_t lo = (int32_t)m - q16, hi = (int32_t)(m + a.ds) - q16;
             const uint32_t lo_c = lo < 0 ? 0u : (lo > 16 ? 16u : (uint32_t)lo);
             const uint32_t hi_c = hi < 0 ? 0u : (hi > 16 ? 16u : (uint32_t)hi);
-            const uint32_t pv = crc_piece(tbl, cur.v[k], lo_c, hi_c > lo_c ? hi_c : lo_c, n32);
-            acc = k == 0 ? pv : (hmap<CF_K>(tbl, acc) ^ pv);
+            const uint32_t pv = crc_piece<true>(tbl, cur.v[k], lo_c, hi_c > lo_c ? hi_c : lo_c, n32);
+            acc = k == 0 ? pv : (hmap<CF_K, true>(tbl, acc) ^ pv);
         }
-        const uint32_t Vs = crc_lane_sum(tbl, acc, lane);
+        const uint32_t Vs = crc_lane_sum<true>(tbl, acc, lane);
         const uint32_t V = cmap(tbl + (CF_FENC + m) * CF_MAP, Vs);
         const uint32_t st = (V << 1) & a.mask;
         if (!(skip && PPFS_DBG_OK(skip + blk, 1, skip, nblocks_all) && skip[blk] == 5)) {
@@ -940,8 +932,8 @@ __global__ __launch_bounds__(256) PPFS_CRC_ATTR void crc_fast_check_kernel(const
     uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks_all, CrcFast a,
     const uint8_t* __restrict__ tables)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t tbl[CF_BYTES];
-    for (uint32_t p = threadIdx.x; p < CF_BYTES / 16; p += 256)
+    __shared__ __attribute__((aligned(16))) uint8_t tbl[CF_SIX_OFF];
+    for (uint32_t p = threadIdx.x; p < CF_SIX_OFF / 16; p += 256)
         *(uint4*)(tbl + 16 * p) = *(const uint4*)(tables + 16 * p);
     __syncthreads();
     const uint32_t lane = lane_id(), wave = wave_id();
@@ -968,10 +960,10 @@ __global__ __launch_bounds__(256) PPFS_CRC_ATTR void crc_fast_check_kernel(const
             const int32_t q16 = 16 * (64 * k + (int32_t)lane);
             const int32_t hi = (int32_t)ds - q16;
             const uint32_t hi_c = hi < 0 ? 0u : (hi > 16 ? 16u : (uint32_t)hi);
-            const uint32_t pv = crc_piece(tbl, R[k], 0u, hi_c, n32);
-            acc = k == 0 ? pv : (hmap<CF_K>(tbl, acc) ^ pv);
+            const uint32_t pv = crc_piece<false>(tbl, R[k], 0u, hi_c, n32);
+            acc = k == 0 ? pv : (hmap<CF_K, false>(tbl, acc) ^ pv);
         }
-        const uint32_t Vs = crc_lane_sum(tbl, acc, lane);
+        const uint32_t Vs = crc_lane_sum<false>(tbl, acc, lane);
         const uint32_t V = cmap(tbl + CF_FCHK * CF_MAP, Vs);
         const uint32_t st = (V << 1) & a.mask;
         // stored field: n bits MSB first from byte ds (in the last raw piece, lane 63)
