@@ -703,8 +703,8 @@ constexpr int CF_M0 = 0, CF_K = 4, CF_L = 5, CF_FENC = 11, CF_FCHK = 27, CF_NMAP
 constexpr int CF_LANES = 16;
 constexpr int CF_LANE_OFF = CF_NMAPS * CF_MAP;
 // The encode's hot maps (piece dwords, Horner, the two tree levels) also as 6-bit tables (5 x 64
-// entries + 4; a 64-entry u32 table fills each bank once, so any indices are conflict-free): 6 LDS
-// lookups per map instead of 8.  Stored after the lane maps, CF_MAP6 bytes each, in the order
+// entries + 4): 6 LDS lookups per map instead of 8.  (ds_read_b32 conflicts between dwords 32
+// apart, so a 64-entry table is 2-way conflicted -- PMC, DESIGN 4.0 -- and still wins.)  Stored after the lane maps, CF_MAP6 bytes each, in the order
 // M0..M3, K, L+4, L+5.  (r3zc A/B: encode -1 %; the check kernel, 5 waves per SIMD with them, ran
 // 0.8 % slower, so it keeps the nibble maps and stages only the first CF_SIX_OFF bytes.)
 #ifndef PPFS_CRC_SIX
