@@ -26,6 +26,7 @@
 
 #include "../../include/ppfs_ecc.h"
 #include "rs_layout.hpp"
+#include "rs_sched.hpp"
 #include "launch.hpp"
 #include "server_box.hpp"
 
@@ -275,6 +276,9 @@ template <int T2> std::vector<uint8_t> build_rs_wg_tables_t()
                         G.mul((uint8_t)(v << (4 * h)), G.exp[e]);
                 }
     build_gf_block(out.data() + L::OFF_GF);
+    const std::vector<uint16_t> es = ppfs::sched::build_encode(T2), ds = ppfs::sched::build_decode(T2);
+    std::memcpy(out.data() + L::OFF_ESCHED, es.data(), es.size() * sizeof(uint16_t));
+    std::memcpy(out.data() + L::OFF_DSCHED, ds.data(), ds.size() * sizeof(uint16_t));
     return out;
 }
 
@@ -514,10 +518,16 @@ struct ppfs_ecc_ctx {
     // launch of the same kind on the stream used (launches on one stream are ordered; no two streams
     // share a slot); tk_par = the set the next launch of each kind uses.  Further streams use the
     // static walk.
+    // Ordering (round 4): a slot remembers the caller-stream event slot (ev[] below) of the stream
+    // that last launched on it; a slot passes to another stream only once that event has completed,
+    // and every device call first waits for the previous call's event on its stream handle, so a
+    // stream created at a destroyed stream's address never runs beside a kernel still counting on
+    // the old stream's set.
     static constexpr int kTkSlots = 16, kTkSetWords = 1024; // encode 512 words (rs_wq: 32 counters 64 B apart), decode 512
     uint32_t* d_ctr = nullptr;
     hipStream_t tk_stream[kTkSlots] = {};
     uint8_t tk_par[kTkSlots][2] = {};
+    int tk_ev[kTkSlots] = {}; // ev[] slot of the slot's last user
     int tk_n = 0;
     // scratch for write_device status when the caller passes none
     uint8_t* d_scratch = nullptr;
@@ -551,6 +561,7 @@ struct ppfs_ecc_ctx {
     static constexpr int kEvSlots = 32;
     hipStream_t ev_stream[kEvSlots] = {};
     hipEvent_t ev[kEvSlots] = {};
+    bool ev_rec[kEvSlots] = {}; // recorded at least once
     int ev_n = 0;
     bool ev_overflow = false;
     // the context's own stream for its stream-ordered device allocations (mem_alloc / mem_free)
@@ -683,30 +694,98 @@ bool capturing(hipStream_t s)
     return st != hipStreamCaptureStatusNone;
 }
 
+// The caller-stream event slot of handle s (-1: none, and with `create` none could be made).
+int ev_slot(ppfs_ecc_ctx* c, hipStream_t s, bool create)
+{
+    int i = 0;
+    while (i < c->ev_n && c->ev_stream[i] != s)
+        ++i;
+    if (i < c->ev_n)
+        return i;
+    if (!create)
+        return -1;
+    if (c->ev_n == ppfs_ecc_ctx::kEvSlots
+        || hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
+        (void)hipGetLastError();
+        c->ev_overflow = true;
+        return -1;
+    }
+    c->ev_stream[i] = s;
+    c->ev_rec[i] = false;
+    c->ev_n++;
+    return i;
+}
+
+// Before a device entry point queues work on caller stream s: order it after the last call queued
+// on the same handle.  For the same stream the runtime returns at once (an event recorded on the
+// waiting stream itself); it matters when s is a new stream created at the address of a destroyed
+// one whose work may still run: the new stream's kernels then never share that work's ticket set
+// (ctr_for) or outlive-check (destroy waits on the event re-recorded after this call).
+void order_caller_stream(ppfs_ecc_ctx* c, hipStream_t s)
+{
+    if ((c->hs[0] && s == c->hs[0]) || (c->hs[1] && s == c->hs[1]) || capturing(s))
+        return;
+    const int i = ev_slot(c, s, false);
+    if (i >= 0 && c->ev_rec[i] && hipStreamWaitEvent(s, c->ev[i], 0) != hipSuccess)
+        (void)hipGetLastError();
+}
+
 // The ticket-counter set of stream s (nullptr: the static-walk kernel runs).  A set is shared by
 // every launch on its stream, which is safe only because launches on one stream are ordered.  A
 // launch captured into a graph gets no set: its replays may run on other streams or overlap each
-// other (two kernels on one set would skip or repeat tiles).  The 17th distinct stream of a
-// context also falls back (slots are not recycled: a slot's stream may still be running a kernel
-// on it); ppfs_ecc_stream_kernel_name reports which path a stream gets.
+// other (two kernels on one set would skip or repeat tiles).  A stream without a slot takes a free
+// one, or one whose last user's work has completed (its event); with none, or without a caller
+// event slot to order it by, it falls back to the static walk.  ppfs_ecc_stream_kernel_name reports
+// which path a stream gets.
 struct TkSets {
     uint32_t* mine = nullptr;  // the set this launch counts on
     uint32_t* clear = nullptr; // the set it zeroes (the previous launch's)
     int slot = -1, op = 0;
 };
-TkSets ctr_for(ppfs_ecc_ctx* c, hipStream_t s, int op /* 0 encode, 1 decode */)
+// the slot stream s would use (-1: none); with `take`, assign it
+int tk_slot(ppfs_ecc_ctx* c, hipStream_t s, bool take)
 {
-    TkSets t;
     if (!c->d_ctr || capturing(s))
-        return t;
+        return -1;
+    const int e = ev_slot(c, s, take);
+    if (take && e < 0)
+        return -1;
     int i = 0;
     while (i < c->tk_n && c->tk_stream[i] != s)
         ++i;
     if (i == c->tk_n) {
-        if (c->tk_n == ppfs_ecc_ctx::kTkSlots)
-            return t;
-        c->tk_stream[c->tk_n++] = s;
+        if (c->tk_n < ppfs_ecc_ctx::kTkSlots) {
+            if (take)
+                c->tk_n++;
+        } else {
+            // recycle a slot whose last user's work is complete (the event query is not a wait);
+            // the set its next launch counts on was zeroed by that completed work
+            i = -1;
+            for (int j = 0; j < c->tk_n && i < 0; ++j) {
+                if (!c->ev_rec[c->tk_ev[j]]) // its last record failed: nothing tells when it is done
+                    continue;
+                const hipError_t q = hipEventQuery(c->ev[c->tk_ev[j]]);
+                if (q == hipSuccess)
+                    i = j;
+                else if (q != hipErrorNotReady)
+                    (void)hipGetLastError();
+            }
+            if (i < 0)
+                return -1;
+        }
+        if (take)
+            c->tk_stream[i] = s;
     }
+    if (take)
+        c->tk_ev[i] = e;
+    return i;
+}
+TkSets ctr_for(ppfs_ecc_ctx* c, hipStream_t s, int op /* 0 encode, 1 decode */)
+{
+    TkSets t;
+    const int i = tk_slot(c, s, true);
+    if (i < 0)
+        return t;
     const int par = c->tk_par[i][op];
     uint32_t* base = c->d_ctr + (size_t)i * 2 * ppfs_ecc_ctx::kTkSetWords + (size_t)op * (ppfs_ecc_ctx::kTkSetWords / 2);
     t.mine = base + (size_t)par * ppfs_ecc_ctx::kTkSetWords;
@@ -728,25 +807,21 @@ hipError_t tk_commit(ppfs_ecc_ctx* c, const TkSets& t, hipError_t e)
 // Captured work is the graph's: the caller keeps the context alive while graphs that use it exist.
 void note_caller_stream(ppfs_ecc_ctx* c, hipStream_t s)
 {
-    if (s == c->hs[0] || s == c->hs[1] || capturing(s)) // the context's own streams: destroy drains them
+    // the context's own streams (destroy drains them) -- compared only once they exist: before the
+    // host path first runs they are null, which is also the default stream's handle, and work on
+    // the default stream must be tracked like any other caller stream's
+    if ((c->hs[0] && s == c->hs[0]) || (c->hs[1] && s == c->hs[1]) || capturing(s))
         return;
-    int i = 0;
-    while (i < c->ev_n && c->ev_stream[i] != s)
-        ++i;
-    if (i == c->ev_n) {
-        if (c->ev_n == ppfs_ecc_ctx::kEvSlots
-            || hipEventCreateWithFlags(&c->ev[i], hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
-            (void)hipGetLastError();
-            c->ev_overflow = true;
-            return;
-        }
-        c->ev_stream[i] = s;
-        c->ev_n++;
-    }
+    const int i = ev_slot(c, s, true);
+    if (i < 0)
+        return; // ev_overflow: destroy synchronizes the device
     if (hipEventRecord(c->ev[i], s) != hipSuccess) {
         (void)hipGetLastError();
         c->ev_overflow = true;
+        c->ev_rec[i] = false;
+        return;
     }
+    c->ev_rec[i] = true;
 }
 } // namespace
 
@@ -882,8 +957,12 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
             if (e == hipSuccess)
                 e = hipStreamSynchronize(c->ms);
         }
-        if (bounce && e == hipSuccess)
+        if (bounce) {
+            // whatever e is: no copy from the bounce may still be queued when it returns to the cache
+            if (e != hipSuccess)
+                (void)hipStreamSynchronize(c->ms);
             pin_free(bounce, tables.size(), kPinStage);
+        }
         if (e != hipSuccess) {
             ppfs_ecc_destroy(c);
             return fail(PPFS_ECC_EHIP, "table upload", e);
@@ -1194,25 +1273,34 @@ static int queued(ppfs_ecc_ctx* c, int r, size_t nblocks, void* stream, const ch
         note_caller_stream(c, (hipStream_t)stream);
     return sync_check(r, stream, what);
 }
+// ... and before it queues anything: after the last call on the same stream handle
+static void* ordered(ppfs_ecc_ctx* c, size_t nblocks, void* stream)
+{
+    if (c && nblocks)
+        order_caller_stream(c, (hipStream_t)stream);
+    return stream;
+}
 
 extern "C" int ppfs_ecc_encode_device(ppfs_ecc_ctx* c, const uint8_t* d_data, uint8_t* d_raw, size_t nblocks,
     void* stream)
 {
-    return queued(c, ppfs_ecc_encode_device_impl(c, d_data, d_raw, nblocks, stream), nblocks, stream, "encode (async)");
+    return queued(c, ppfs_ecc_encode_device_impl(c, d_data, d_raw, nblocks, ordered(c, nblocks, stream)), nblocks,
+        stream, "encode (async)");
 }
 
 extern "C" int ppfs_ecc_decode_device(ppfs_ecc_ctx* c, uint8_t* d_raw, uint8_t* d_data, uint8_t* d_status,
     size_t nblocks, int write_back, uint8_t* d_spill, void* stream)
 {
-    return queued(c, ppfs_ecc_decode_device_impl(c, d_raw, d_data, d_status, nblocks, write_back, d_spill, stream),
+    return queued(c,
+        ppfs_ecc_decode_device_impl(c, d_raw, d_data, d_status, nblocks, write_back, d_spill, ordered(c, nblocks, stream)),
         nblocks, stream, "decode (async)");
 }
 
 extern "C" int ppfs_ecc_write_device(ppfs_ecc_ctx* c, const uint8_t* d_data, uint8_t* d_raw, uint8_t* d_status,
     size_t nblocks, void* stream)
 {
-    return queued(c, ppfs_ecc_write_device_impl(c, d_data, d_raw, d_status, nblocks, stream), nblocks, stream,
-        "write (async)");
+    return queued(c, ppfs_ecc_write_device_impl(c, d_data, d_raw, d_status, nblocks, ordered(c, nblocks, stream)),
+        nblocks, stream, "write (async)");
 }
 
 namespace ppfs {
@@ -1233,10 +1321,8 @@ extern "C" const char* ppfs_ecc_stream_kernel_name(ppfs_ecc_ctx* c, void* stream
         return "";
     if (c->d_ctr) { // 2t <= 8: ticket kernels while the stream has (or can get) a counter set
         const hipStream_t s = (hipStream_t)stream;
-        bool has = false;
-        for (int i = 0; i < c->tk_n; ++i)
-            has = has || c->tk_stream[i] == s;
-        if (capturing(s) || (!has && c->tk_n == ppfs_ecc_ctx::kTkSlots))
+        const bool evok = ev_slot(c, s, false) >= 0 || c->ev_n < ppfs_ecc_ctx::kEvSlots;
+        if (!evok || tk_slot(c, s, false) < 0)
             return "rs255-wg-seg4-lds"; // rs_wg.hpp static walk
     }
     return c->kname;

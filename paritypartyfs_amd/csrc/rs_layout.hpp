@@ -31,17 +31,17 @@ template <int T2> struct RsWgLayout {
     // MAP32 (after the decode layout, read by the 8-wave encode only): m = 0..6, the x^(q + 32(m+1))
     // maps of 32-byte segments
     static constexpr int OFF_MAP32 = TABLE_BYTES;
-    // CTR: zeroed tile-ticket counters of the dynamic-tile kernels (rs_wg.hpp): encode at +0,
-    // decode at +2048; in each, 8 counters (one per XCD) and the workgroups-done count, one
-    // 128-byte line each.  Each launch leaves them at zero.
     // SLX (round 3): the slicing tables of segment m = 1..3 with x^(64 m) folded in, 16 nibble
     // tables each: table 2i+h, value v -> (v << 4h) * x^(2t+i+64m) mod g, read by the LAST slicing
     // step of segment m, which then needs no x^(64 m) map (rs_wg.hpp seg_remainder)
     static constexpr int OFF_SLX = OFF_MAP32 + 7 * MAP_STRIDE;
     static constexpr int SLX_BYTES = 3 * 16 * TBL;
-    static constexpr int OFF_CTR = OFF_SLX + SLX_BYTES;
-    static constexpr int CTR_BYTES = 4096;
-    static constexpr int BLOB_BYTES = OFF_CTR + CTR_BYTES;
+    // ESCHED / DSCHED (round 4): the encode / decode emission schedules (rs_sched.hpp), 256 threads
+    // x 4 rounds of u16, read from global memory once per workgroup (not copied to LDS)
+    static constexpr int OFF_ESCHED = OFF_SLX + SLX_BYTES;
+    static constexpr int SCHED_BYTES = 2048;
+    static constexpr int OFF_DSCHED = OFF_ESCHED + SCHED_BYTES;
+    static constexpr int BLOB_BYTES = OFF_DSCHED + SCHED_BYTES;
     static_assert(TABLE_BYTES % 16 == 0 && BLOB_BYTES % 16 == 0, "tables are copied in 16-byte pieces");
 };
 

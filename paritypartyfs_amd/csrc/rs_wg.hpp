@@ -230,131 +230,11 @@ __device__ __forceinline__ void phase_remainder(uint8_t* lds, uint32_t buf, uint
     phase_remainder_row<T2, LEN, NMAP, XOFF>(lds, buf + PAD + (uint32_t)LEN * blk, par, wave, blk);
 }
 
-// Lock-step pieces of step8 / seg_map for two independent chains: the lookups of both chains are
-// issued before either chain's XOR tree, so their LDS latencies overlap.
-template <bool FIRST, int NB>
-__device__ __forceinline__ void step8_issue(uint2 (&e)[16], const uint32_t (&s)[2], uint32_t lo, uint32_t hi, const uint8_t* sl)
-{
-    if constexpr (!FIRST) {
-        lo ^= s[0];
-        hi ^= s[1];
-    }
-    constexpr int NL = FIRST ? NB : 8;
-    const uint32_t ll = lo << 3, lh = lo >> 1, hl = hi << 3, hh = hi >> 1;
-#pragma unroll
-    for (int i = 0; i < NL; ++i) {
-        const uint32_t xl = i < 4 ? ll : hl, xh = i < 4 ? lh : hh;
-        e[2 * i] = ld8(sl + (2 * i) * 128 + sel78(xl, i));
-        e[2 * i + 1] = ld8(sl + (2 * i + 1) * 128 + sel78(xh, i));
-    }
-}
-template <int N> __device__ __forceinline__ void xor_first(uint32_t (&s)[2], const uint2 (&e)[16])
-{
-    uint2 f[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-        f[i] = e[i];
-    s[0] = 0;
-    s[1] = 0;
-    xor_entries<N>(s, f);
-}
-template <int T2, int S> __device__ __forceinline__ void map_issue(uint2 (&e)[16], const uint32_t (&s)[2], const uint8_t* lds)
-{
-    using L = RsWgLayout<T2>;
-    const uint8_t* mp = lds + L::OFF_MAP + (S - 1) * L::MAP_STRIDE;
-#pragma unroll
-    for (int q = 0; q < T2; ++q) {
-        const int P = 8 - T2 + q;
-        const uint32_t x = s[P >> 2];
-        e[2 * q] = ld8(mp + (2 * q) * 128 + sel78(x << 3, P & 3));
-        e[2 * q + 1] = ld8(mp + (2 * q + 1) * 128 + sel78(x >> 1, P & 3));
-    }
-}
-
-// the chunk (lo, hi) of a segment at step c, its top chunk masked to TOPN bytes
-template <int NC, int TOPN>
-__device__ __forceinline__ void seg_chunk(uint32_t& lo, uint32_t& hi, const uint32_t* R, int c, uint32_t sh)
-{
-    lo = __builtin_amdgcn_alignbit(R[2 * c + 1], R[2 * c], sh);
-    hi = __builtin_amdgcn_alignbit(R[2 * c + 2], R[2 * c + 1], sh);
-    if (c == NC - 1) {
-        if constexpr (TOPN < 4) {
-            lo &= (1u << (8 * TOPN)) - 1u;
-            hi = 0;
-        } else if constexpr (TOPN == 4) {
-            hi = 0;
-        } else if constexpr (TOPN < 8) {
-            hi &= (1u << (8 * (TOPN - 4))) - 1u;
-        }
-    }
-}
-
-// NMAP = 7 (the ticket encode, round 3): the x^(32 m) maps (MAP32 copied to OFF_MAP), and each lane
-// runs its 64-byte segment as two independent 32-byte chains, sub-segments 2W and 2W + 1, in lock
-// step (4 slicing steps each, then both maps): 5 dependent table rounds instead of 9, for 12 more
-// lookups
-template <int T2, int LEN, int W>
-__device__ __forceinline__ void seg_remainder_ilp2(uint32_t (&s)[2], const uint8_t* lds, uint32_t row)
-{
-    constexpr int SA = 2 * W, SB = 2 * W + 1, LOA = 32 * SA, LOB = 32 * SB;
-    constexpr int LSA = (LEN - LOA) < 32 ? (LEN - LOA) : 32, LSB = (LEN - LOB) < 32 ? (LEN - LOB) : 32;
-    constexpr int NCA = (LSA + 7) / 8, NCB = (LSB + 7) / 8;
-    constexpr int TOPA = LSA - 8 * (NCA - 1), TOPB = LSB - 8 * (NCB - 1);
-    static_assert(NCA == 4 && NCB >= 1 && NCB <= 4, "32-byte sub-segments");
-    const uint32_t a0 = row + LOA, sh = (a0 & 3u) * 8u; // LOB = LOA + 32: the same shift
-    const uint32_t* w = (const uint32_t*)(lds + (a0 & ~3u));
-    uint32_t RA[2 * NCA + 1], RB[2 * NCB + 1];
-#pragma unroll
-    for (int q = 0; q < 2 * NCA + 1; ++q)
-        RA[q] = w[q];
-#pragma unroll
-    for (int q = 0; q < 2 * NCB + 1; ++q)
-        RB[q] = w[8 + q];
-    const uint8_t* sl = lds + RsWgLayout<T2>::OFF_SL;
-    uint32_t sa[2] = { 0u, 0u }, sb[2] = { 0u, 0u };
-#pragma unroll
-    for (int c = NCA - 1; c >= 0; --c) {
-        uint2 ea[16], eb[16];
-        uint32_t lo, hi;
-        seg_chunk<NCA, TOPA>(lo, hi, RA, c, sh);
-        if (c == NCA - 1)
-            step8_issue<true, TOPA>(ea, sa, lo, hi, sl);
-        else
-            step8_issue<false, 8>(ea, sa, lo, hi, sl);
-        if (c < NCB) {
-            seg_chunk<NCB, TOPB>(lo, hi, RB, c, sh);
-            if (c == NCB - 1)
-                step8_issue<true, TOPB>(eb, sb, lo, hi, sl);
-            else
-                step8_issue<false, 8>(eb, sb, lo, hi, sl);
-        }
-        if (c == NCA - 1)
-            xor_first<2 * TOPA>(sa, ea);
-        else
-            xor_first<16>(sa, ea);
-        if (c < NCB) {
-            if (c == NCB - 1)
-                xor_first<2 * TOPB>(sb, eb);
-            else
-                xor_first<16>(sb, eb);
-        }
-    }
-    uint2 ea[16], eb[16];
-    if constexpr (W > 0)
-        map_issue<T2, SA>(ea, sa, lds);
-    map_issue<T2, SB>(eb, sb, lds);
-    if constexpr (W > 0)
-        xor_first<2 * T2>(sa, ea);
-    xor_first<2 * T2>(sb, eb);
-    s[0] = sa[0] ^ sb[0];
-    s[1] = sa[1] ^ sb[1];
-}
-
 // the same for a LEN-byte row at LDS byte `row` (any row layout)
 template <int T2, int LEN, int NMAP, int XOFF>
 __device__ __forceinline__ void phase_remainder_row(uint8_t* lds, uint32_t row, uint32_t par, uint32_t wave, uint32_t blk)
 {
-    static_assert(NMAP == 1 || NMAP == 2 || NMAP == 3 || NMAP == 7, "x^(64 s) or x^(32 s) maps, or SLX tables");
+    static_assert(NMAP == 1 || NMAP == 2 || NMAP == 3, "x^(64 s) maps, or SLX tables");
     static_assert(NMAP != 1 || XOFF > 0, "SLX tables need their LDS offset");
     uint32_t s[2];
     if constexpr (NMAP == 1) {
@@ -370,21 +250,6 @@ __device__ __forceinline__ void phase_remainder_row(uint8_t* lds, uint32_t row, 
             break;
         default:
             seg_remainder<T2, LEN, 3, 64, XOFF>(s, lds, row);
-            break;
-        }
-    } else if constexpr (NMAP == 7) {
-        switch (wave) {
-        case 0:
-            seg_remainder_ilp2<T2, LEN, 0>(s, lds, row);
-            break;
-        case 1:
-            seg_remainder_ilp2<T2, LEN, 1>(s, lds, row);
-            break;
-        case 2:
-            seg_remainder_ilp2<T2, LEN, 2>(s, lds, row);
-            break;
-        default:
-            seg_remainder_ilp2<T2, LEN, 3>(s, lds, row);
             break;
         }
     } else switch (wave) {
@@ -640,13 +505,12 @@ __device__ __forceinline__ void vm_wait_newer(uint32_t n)
 
 // COMPACT (encode only): 2 maps (phase_remainder NMAP = 2) and tile buffers sized for the 64
 // payload rows (PAD + 64 K + 32) instead of 64 codewords, so 3 ring buffers fit 3 workgroups / CU
-// MAPS (encode only): 7 = the x^(32 m) maps at OFF_MAP (phase_remainder NMAP = 7)
 // MAPS = 1: the SLX last-step tables (3 x 2 KiB, seg_remainder) instead of the maps: the encode holds
 // SL + SLX (OFF_SLX = L::OFF_MAP), the decode the whole decode table prefix + SLX after it
 template <int T2, bool DEC, int NBUF, bool COMPACT = false, int MAPS = 0> struct Lds {
     using L = RsWgLayout<T2>;
     static_assert(!(DEC && COMPACT), "compact layout: encode only");
-    static_assert(MAPS == 0 || MAPS == 1 || (MAPS == 7 && !DEC && !COMPACT), "32-byte maps: encode only");
+    static_assert(MAPS == 0 || MAPS == 1, "x^(64 s) maps or SLX tables");
     static constexpr int NMAP = MAPS ? MAPS : COMPACT ? 2 : 3;
     static constexpr int OFF_SLX = MAPS == 1 ? (DEC ? L::TABLE_BYTES : L::OFF_MAP) : 0;
     static constexpr int TBL = MAPS == 1 ? OFF_SLX + L::SLX_BYTES

@@ -53,6 +53,13 @@ __device__ __forceinline__ void dma_tile192(uint8_t* dst, const uint8_t* __restr
 // s_waitcnt vmcnt(n) for a wave-uniform n in [0, 31] (exact: the counts below are known per wave)
 __device__ __forceinline__ void vm_wait_exact(uint32_t n)
 {
+#ifdef PPFS_ECC_DEBUG
+    // the checked build may skip a DMA (PPFS_DBG_OK), so fewer loads are in flight than counted and
+    // an exact count would let an older tile's loads still fly: wait for everything
+    (void)n;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+#endif
     switch (__builtin_amdgcn_readfirstlane(n)) {
 #define PPFS_VMW(N)                                                                                                    \
     case N:                                                                                                            \
@@ -100,25 +107,18 @@ __device__ __forceinline__ TkGeom tk_geom()
     return g;
 }
 
-#ifndef PPFS_TK_MAPC
-#define PPFS_TK_MAPC 0 // ablation: 1 = each XCD's counter walks a contiguous range of tiles
-#endif
-// the tile of local ticket j on this XCD: interleaved (j nx + xc) or, with PPFS_TK_MAPC, the XCD's
-// contiguous range of per = nfull / nx + 1 tiles (tiles past nfull -> nfull + 1: none)
-__device__ __forceinline__ uint64_t tk_tile(uint64_t j, const TkGeom& g, uint64_t nfull)
-{
-    if constexpr (PPFS_TK_MAPC) {
-        const uint64_t per = nfull / g.nx + 1u, t = (uint64_t)g.xc * per + j;
-        return (j < per && t <= nfull) ? t : nfull + 1u;
-    } else {
-        return j * g.nx + g.xc;
-    }
-}
+// the tile of local ticket j on this XCD: interleaved, j nx + xc (round 3 measured each XCD walking
+// a contiguous range instead: no gain)
+__device__ __forceinline__ uint64_t tk_tile(uint64_t j, const TkGeom& g, uint64_t /*nfull*/) { return j * g.nx + g.xc; }
 
-// block 0, one lane: zero the counter set the previous launch on this stream used
-__device__ __forceinline__ void tk_clear(uint32_t* __restrict__ ctr_clear, uint32_t nx)
+// block 0, one lane: zero the counter set the previous launch on this stream used -- all 8 counter
+// lines, whatever this launch's nx: the previous launch may have counted on more XCD counters than
+// this (small) one does, and a counter left dirty would start a later large launch's tickets past
+// tiles nobody then encodes
+__device__ __forceinline__ void tk_clear(uint32_t* __restrict__ ctr_clear)
 {
-    for (uint32_t x = 0; x < nx; ++x)
+#pragma unroll
+    for (uint32_t x = 0; x < 8u; ++x)
         __hip_atomic_store(ctr_clear + 32u * x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -141,12 +141,53 @@ __device__ uint64_t g_tk_trace_dec[4096 * 2 * TK_TRACE_N];
 #define PPFS_TK_MARK(i) ((void)0)
 #endif
 
-#ifndef PPFS_ENC_ILP2
-#define PPFS_ENC_ILP2 0 // 1: remainder as two 32-byte chains per lane (phase_remainder NMAP = 7)
-#endif
-#ifndef PPFS_WG_SLX
-#define PPFS_WG_SLX 1 // SLX last-step tables instead of the x^(64 s) maps (rs_wg.hpp seg_remainder); 0 = maps
-#endif
+// Interior emission pieces: the 16 bytes at LDS byte a + sh / 8 (a dword aligned, sh = 0, 8, 16, 24).
+// A window of 5 dwords is read by exactly ds_read2_b32 (0, 1), ds_read2_b32 (2, 3), ds_read_b32 (4)
+// (left to itself the compiler reads dwords (0, 1), (1, 2), (3, 4): 6 dword reads), N windows in
+// flight at once before one wait; asm reads are not tracked by the compiler, so the wait is explicit
+// and names the results.
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+struct Win5 {
+    u32x2v d01, d23;
+    uint32_t d4;
+};
+__device__ __forceinline__ uint4 win_piece(const Win5& w, uint32_t sh)
+{
+    return make_uint4(__builtin_amdgcn_alignbit(w.d01.y, w.d01.x, sh), __builtin_amdgcn_alignbit(w.d23.x, w.d01.y, sh),
+        __builtin_amdgcn_alignbit(w.d23.y, w.d23.x, sh), __builtin_amdgcn_alignbit(w.d4, w.d23.y, sh));
+}
+__device__ __forceinline__ void win5x1(Win5& w0, uint32_t a0)
+{
+    asm volatile("ds_read2_b32 %0, %3 offset1:1\n\tds_read2_b32 %1, %3 offset0:2 offset1:3\n\tds_read_b32 %2, %3 offset:16\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=v"(w0.d01), "=v"(w0.d23), "=v"(w0.d4)
+                 : "v"(a0)
+                 : "memory");
+}
+__device__ __forceinline__ void win5x3(Win5& w0, Win5& w1, Win5& w2, uint32_t a0, uint32_t a1, uint32_t a2)
+{
+    asm volatile("ds_read2_b32 %0, %9 offset1:1\n\tds_read2_b32 %1, %9 offset0:2 offset1:3\n\tds_read_b32 %2, %9 offset:16\n\t"
+                 "ds_read2_b32 %3, %10 offset1:1\n\tds_read2_b32 %4, %10 offset0:2 offset1:3\n\tds_read_b32 %5, %10 offset:16\n\t"
+                 "ds_read2_b32 %6, %11 offset1:1\n\tds_read2_b32 %7, %11 offset0:2 offset1:3\n\tds_read_b32 %8, %11 offset:16\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(w0.d01), "=&v"(w0.d23), "=&v"(w0.d4), "=&v"(w1.d01), "=&v"(w1.d23), "=&v"(w1.d4), "=&v"(w2.d01),
+                 "=&v"(w2.d23), "=&v"(w2.d4)
+                 : "v"(a0), "v"(a1), "v"(a2)
+                 : "memory");
+}
+// rs_sched.hpp enc_src / dec_src on the device: LDS byte of an interior piece's first source byte
+template <int T2> __device__ __forceinline__ uint32_t sched_enc_src(uint32_t p)
+{
+    const uint32_t j0 = 16u * p, b = j0 / 255u, off = j0 - 255u * b;
+    return (uint32_t)PAD + (255u - T2) * b + off - (uint32_t)T2;
+}
+template <int T2> __device__ __forceinline__ uint32_t sched_dec_src(uint32_t p)
+{
+    constexpr uint32_t K = 255u - T2;
+    const uint32_t j0 = 16u * p, b = j0 / K, off = j0 - K * b;
+    return (uint32_t)PAD + 255u * b + (uint32_t)T2 + off;
+}
+
 template <int T2, int WPC = 2, int NTST = 1>
 __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t* __restrict__ data,
     uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables, uint32_t* __restrict__ ctr,
@@ -154,14 +195,14 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
 {
     constexpr int NBUF = 3;
     using L = RsWgLayout<T2>;
-    using D = Lds<T2, false, NBUF, false, PPFS_ENC_ILP2 ? 7 : PPFS_WG_SLX ? 1 : 0>;
+    using D = Lds<T2, false, NBUF, false, 1>; // SL + SLX tables
     constexpr int BUF = D::BUFB;
-    constexpr int LDS_ALLOC = lds_alloc<D::BYTES + 64, WPC>();
+    constexpr uint32_t OFF_TK = D::BYTES; // 4 ticket slots: slot i & 3 = tile of iteration i
+    constexpr uint32_t OFF_SCHED = D::BYTES + 64; // the emission schedule (rs_sched.hpp), read once
+    constexpr int LDS_ALLOC = lds_alloc<D::BYTES + 64 + L::SCHED_BYTES, WPC>();
     static_assert(WPC * LDS_ALLOC <= 163840, "LDS for WPC workgroups per CU");
     constexpr int K = L::K;
     constexpr int IN_PIECES = TB * K / 16;
-    constexpr int OUT_PIECES = TB * 255 / 16;
-    constexpr uint32_t OFF_TK = D::BYTES; // 4 ticket slots: slot i & 3 = tile of iteration i
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_ALLOC];
     uint32_t* const s_tk = (uint32_t*)(lds + OFF_TK);
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
@@ -187,20 +228,14 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
             dma_tile192<IN_PIECES>(lds + D::OFF_BUF + BUF + PAD, data + q1 * (TB * K), tid, data, nblocks * K);
         hist = go ? 1u : 0u;
     } else {
-        if constexpr (D::NMAP == 7) { // SL, then MAP32 in the place of MAP
-            dma_tables_w0<L::OFF_MAP>(lds, tables, lane);
-            dma_tables_w0<7 * L::MAP_STRIDE>(lds + L::OFF_MAP, tables + L::OFF_MAP32, lane);
-        } else if constexpr (D::NMAP == 1) { // SL, then SLX in the place of MAP
-            dma_tables_w0<L::OFF_MAP>(lds, tables, lane);
-            dma_tables_w0<L::SLX_BYTES>(lds + D::OFF_SLX, tables + L::OFF_SLX, lane);
-        } else {
-            dma_tables_w0<D::TBL>(lds, tables, lane);
-        }
+        dma_tables_w0<L::OFF_MAP>(lds, tables, lane); // SL, then SLX in the place of MAP
+        dma_tables_w0<L::SLX_BYTES>(lds + D::OFF_SLX, tables + L::OFF_SLX, lane);
+        dma_tables_w0<L::SCHED_BYTES>(lds + OFF_SCHED, tables + L::OFF_ESCHED, lane);
         *(uint64_t*)(lds + D::OFF_PAR + 8u * lane) = 0; // both parity slot sets (2 x 64 x 8 B)
         *(uint64_t*)(lds + D::OFF_PAR + 512u + 8u * lane) = 0;
         if (tk_lane) {
             if (blockIdx.x == 0)
-                tk_clear(ctr_clear, g.nx);
+                tk_clear(ctr_clear);
             const uint32_t t2 = atomicInc(my_ctr, 0xFFFFFFFFu) + 2u * g.gx; // the tile of iteration 2
             s_tk[2] = (uint32_t)tk_tile(t2, g, nfull);
         }
@@ -209,6 +244,21 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
     if (dmaw)
         vm_wait_exact(kd * hist); // tile q0 landed, q1 may fly
     barrier_lds();
+    // this thread's emission pieces, one per round (rs_sched.hpp): rounds 0-2 are interior pieces
+    // (LDS window at a[k], funnel shift sh[k], output byte o[k]); round 3 interior, boundary or none
+    uint32_t ea[4], esh[4], eo[4], kind3;
+    {
+        const uint2 sc = *(const uint2*)(lds + OFF_SCHED + 8u * tid);
+        const uint32_t e[4] = { sc.x & 0xFFFFu, sc.x >> 16, sc.y & 0xFFFFu, sc.y >> 16 };
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t pk = e[k] & 0x3FFu, S = sched_enc_src<T2>(pk);
+            ea[k] = S & ~3u;
+            esh[k] = (S & 3u) * 8u;
+            eo[k] = 16u * pk;
+        }
+        kind3 = e[3] == 0xFFFFu ? 2u : (e[3] >> 15);
+    }
     PPFS_TK_MARK(0);
     uint32_t cur = 0, pc = 0, iter = 0;
     while (q0 < nfull) {
@@ -238,12 +288,25 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
         barrier_lds(); // B: parity slots complete
         PPFS_TK_MARK(3);
         uint8_t* dst = raw + q0 * (TB * 255);
+        { // rounds 0-2, interior pieces: 4 funnel shifts each, the 3 windows read together
+            const uint32_t lb = lds_addr(lds) + buf;
+            Win5 w[3];
+            win5x3(w[0], w[1], w[2], lb + ea[0], lb + ea[1], lb + ea[2]);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t p = tid + 256u * k;
-            const uint4 o = enc_piece<T2>(lds, buf, par, p);
-            if ((k < 3 || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, raw, nblocks * 255u))
-                st_nt<NTST>(dst + 16u * p, o);
+            for (int k = 0; k < 3; ++k)
+                if (PPFS_DBG_OK(dst + eo[k], 16, raw, nblocks * 255u))
+                    st_nt<NTST>(dst + eo[k], win_piece(w[k], esh[k]));
+        }
+        { // round 3: the last interior pieces, then the boundary pieces (general merge), one store
+            uint4 o;
+            if (kind3 == 0u) {
+                Win5 w;
+                win5x1(w, lds_addr(lds) + buf + ea[3]);
+                o = win_piece(w, esh[3]);
+            } else
+                o = enc_piece<T2>(lds, buf, par, eo[3] >> 4);
+            if (kind3 != 2u && PPFS_DBG_OK(dst + eo[3], 16, raw, nblocks * 255u))
+                st_nt<NTST>(dst + eo[3], o);
         }
         ++iter;
         PPFS_TK_MARK(4);
@@ -309,13 +372,13 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
 {
     constexpr int NBUF = 2;
     using L = RsWgLayout<T2>;
-    using D = Lds<T2, true, NBUF, false, PPFS_WG_SLX ? 1 : 0>;
-    constexpr int LDS_ALLOC = lds_alloc<D::BYTES + 64, WPC>();
+    using D = Lds<T2, true, NBUF, false, 1>; // decode tables + SLX
+    constexpr uint32_t OFF_TK = D::BYTES; // 4 ticket slots: slot i & 3 = tile of iteration i
+    constexpr uint32_t OFF_SCHED = D::BYTES + 64; // the emission schedule (rs_sched.hpp), read once
+    constexpr int LDS_ALLOC = lds_alloc<D::BYTES + 64 + L::SCHED_BYTES, WPC>();
     static_assert(WPC * LDS_ALLOC <= 163840, "LDS for WPC workgroups per CU");
     constexpr int K = L::K;
     constexpr int IN_PIECES = TB * 255 / 16;
-    constexpr int OUT_PIECES = TB * K / 16;
-    constexpr uint32_t OFF_TK = D::BYTES; // 4 ticket slots: slot i & 3 = tile of iteration i
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_ALLOC];
     uint32_t* const s_tk = (uint32_t*)(lds + OFF_TK);
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
@@ -335,22 +398,33 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         if (q0 < nfull)
             dma_tile192<IN_PIECES>(lds + D::OFF_BUF + PAD, raw + q0 * (TB * 255), tid, raw, nblocks * 255u);
     } else {
-        if constexpr (D::NMAP == 1) { // the decode tables, then SLX after them
-            dma_tables_w0<L::TABLE_BYTES>(lds, tables, lane);
-            dma_tables_w0<L::SLX_BYTES>(lds + D::OFF_SLX, tables + L::OFF_SLX, lane);
-        } else {
-            dma_tables_w0<D::TBL>(lds, tables, lane);
-        }
+        dma_tables_w0<L::TABLE_BYTES>(lds, tables, lane); // the decode tables, then SLX after them
+        dma_tables_w0<L::SLX_BYTES>(lds + D::OFF_SLX, tables + L::OFF_SLX, lane);
+        dma_tables_w0<L::SCHED_BYTES>(lds + OFF_SCHED, tables + L::OFF_DSCHED, lane);
         *(uint64_t*)(lds + D::OFF_PAR + 8u * lane) = 0;
         *(uint64_t*)(lds + D::OFF_PAR + 512u + 8u * lane) = 0;
         if (tk_lane) {
             if (blockIdx.x == 0)
-                tk_clear(ctr_clear, g.nx);
+                tk_clear(ctr_clear);
             s_tk[1] = (uint32_t)tk_tile(atomicInc(my_ctr, 0xFFFFFFFFu) + g.gx, g, nfull); // the tile of iteration 1
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // tile q0 / tables and the ticket landed
     barrier_lds();
+    // this thread's emission pieces (rs_sched.hpp), as in the encode
+    uint32_t ea[4], esh[4], eo[4], kind3;
+    {
+        const uint2 sc = *(const uint2*)(lds + OFF_SCHED + 8u * tid);
+        const uint32_t e[4] = { sc.x & 0xFFFFu, sc.x >> 16, sc.y & 0xFFFFu, sc.y >> 16 };
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t pk = e[k] & 0x3FFu, S = sched_dec_src<T2>(pk);
+            ea[k] = S & ~3u;
+            esh[k] = (S & 3u) * 8u;
+            eo[k] = 16u * pk;
+        }
+        kind3 = e[3] == 0xFFFFu ? 2u : (e[3] >> 15);
+    }
     PPFS_TK_MARK(0);
     uint32_t cur = 0, pc = 0, iter = 0;
     while (q0 < nfull) {
@@ -382,13 +456,23 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         PPFS_TK_MARK(4);
         if (want) {
             uint8_t* dst = data + q0 * (TB * K);
+            const uint32_t lb = lds_addr(lds) + buf;
+            Win5 w[3];
+            win5x3(w[0], w[1], w[2], lb + ea[0], lb + ea[1], lb + ea[2]);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t p = tid + 256u * k;
-                const uint4 o = dec_piece<T2>(lds, buf, p);
-                if ((k < 3 || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, data, nblocks * K))
-                    st_nt<NTST>(dst + 16u * p, o);
+            for (int k = 0; k < 3; ++k)
+                if (PPFS_DBG_OK(dst + eo[k], 16, data, nblocks * K))
+                    st_nt<NTST>(dst + eo[k], win_piece(w[k], esh[k]));
+            uint4 o; // round 3: interior or a piece across a block end (general merge); one store
+            if (kind3 == 0u) {
+                Win5 w3;
+                win5x1(w3, lb + ea[3]);
+                o = win_piece(w3, esh[3]);
+            } else {
+                o = dec_piece<T2>(lds, buf, eo[3] >> 4);
             }
+            if (kind3 != 2u && PPFS_DBG_OK(dst + eo[3], 16, data, nblocks * K))
+                st_nt<NTST>(dst + eo[3], o);
         }
         ++iter;
         PPFS_TK_MARK(5);

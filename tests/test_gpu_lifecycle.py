@@ -6,7 +6,9 @@
 - a hipGraph captured from encode + decode uses the static-walk kernels, never a stream's
   ticket-counter set, so replays of two such graphs on two streams at once, and a replay beside
   eager work on the capture's stream, stay bit-exact (api.cpp ctr_for, ADVICE r2);
-- ppfs_ecc_stream_kernel_name reports the static walk for a 17th stream and during capture;
+- ticket-counter slots pass to a 17th stream once an earlier slot's work is complete, and a stream
+  created at a destroyed stream's address is ordered after its work (round 4);
+- work on the default stream is waited for by destroy (ADVICE r3);
 - every range registered through ppfs_ecc_host_register is released by `pinned` (the registry the
   conftest guard checks after every GPU test);
 - the PPFS_ECC_DEBUG build's copy checks refuse a pageable source (positive control).
@@ -173,23 +175,109 @@ def test_graph_replays_on_two_streams_at_once(oracle):
     eng.close()
 
 
-def test_stream_kernel_name_reports_the_static_walk_past_16_streams():
+def test_stream_slots_are_recycled_past_16_streams(oracle):
+    """16 ticket-counter slots: a 17th..20th stream takes a slot whose last user's work has completed
+    (round 4; it used to fall back to the static walk for good), and every stream's codewords stay
+    bit-exact; during capture the static walk runs."""
+    nb = 3 * 64 * 7 + 13
+    n, k, data, cw = _rs_batch(oracle, nb, 35)
     eng = EccEngine(ECC_REED_SOLOMON, 512, 3)
-    d = torch.zeros(64 * 249, dtype=torch.uint8, device="cuda")
-    r = torch.zeros(64 * 255, dtype=torch.uint8, device="cuda")
-    streams = [torch.cuda.Stream() for _ in range(17)]
-    names = []
-    for s in streams:
-        names.append(eng.stream_kernel_name(s))
-        eng.encode(d, r, stream=s)
+    d = torch.from_numpy(data).cuda()
+    streams = [torch.cuda.Stream() for _ in range(20)]
+    outs = [torch.zeros(nb * n, dtype=torch.uint8, device="cuda") for _ in streams]
+    for s, o in zip(streams[:16], outs[:16]):
+        assert eng.stream_kernel_name(s) == "rs255-wg-tk-lds"
+        eng.encode(d, o, stream=s)
     torch.cuda.synchronize()
-    assert names[:16] == ["rs255-wg-tk-lds"] * 16
-    assert eng.stream_kernel_name(streams[16]) == STATIC
-    assert eng.stream_kernel_name(streams[3]) == "rs255-wg-tk-lds"
+    for s, o in zip(streams[16:], outs[16:]):  # every earlier slot's work is complete: recycled
+        assert eng.stream_kernel_name(s) == "rs255-wg-tk-lds"
+        eng.encode(d, o, stream=s)
+        eng.decode(o, None, None, write_back=False, stream=s)
+    torch.cuda.synchronize()
+    for o in outs:
+        assert np.array_equal(o.cpu().numpy(), cw)
+    for s, o in zip(streams[:4], outs[:4]):  # back on the first streams, after their slots moved on
+        o.zero_()
+        eng.encode(d, o, stream=s)
+    torch.cuda.synchronize()
+    for o in outs[:4]:
+        assert np.array_equal(o.cpu().numpy(), cw)
     eng.close()
     hm = EccEngine(ECC_REED_SOLOMON, 4096, 16)  # no ticket kernels: always its own path
     assert hm.stream_kernel_name(streams[16]) == hm.kernel_name == "rs255-bs-byte-lds"
     hm.close()
+
+
+def _hip():
+    import ctypes
+    L = ctypes.CDLL("libamdhip64.so")  # the runtime torch loaded (the engine's too)
+    return ctypes, L
+
+
+def test_recycled_stream_handle_never_shares_a_live_ticket_set(oracle):
+    """A stream destroyed with a large encode still in flight, then streams created until one comes
+    back at the destroyed stream's address (the runtime reuses the object's memory): the launch on
+    the new stream is ordered after the old stream's work (api.cpp order_caller_stream) instead of
+    counting on the same ticket set beside it.  Both outputs are bit-exact."""
+    ct, L = _hip()
+    big = 1 << 20
+    n, k, data, cw = _rs_batch(oracle, big, 36)
+    d = torch.from_numpy(data).cuda()
+    eng = EccEngine(ECC_REED_SOLOMON, 512, 3)
+    small_nb = 64 * 40 + 7
+    torch.cuda.synchronize()
+    hit = 0
+    for trial in range(4):
+        out_a = torch.zeros(big * n, dtype=torch.uint8, device="cuda")
+        out_b = torch.zeros(small_nb * n, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        sa = ct.c_void_p()
+        assert L.hipStreamCreateWithFlags(ct.byref(sa), ct.c_uint(1)) == 0  # non-blocking
+        for _ in range(3):
+            eng.encode(d, out_a, nblocks=big, stream=sa.value)
+        assert L.hipStreamDestroy(sa) == 0  # returns with the encodes in flight
+        made, sb = [], None
+        for _ in range(64):
+            s = ct.c_void_p()
+            assert L.hipStreamCreateWithFlags(ct.byref(s), ct.c_uint(1)) == 0
+            if s.value == sa.value:
+                sb = s
+                break
+            made.append(s)
+        if sb is not None:
+            hit += 1
+            eng.encode(d, out_b, nblocks=small_nb, stream=sb.value)
+            assert L.hipStreamSynchronize(sb) == 0
+            assert L.hipStreamDestroy(sb) == 0
+        for s in made:
+            assert L.hipStreamDestroy(s) == 0
+        torch.cuda.synchronize()
+        assert np.array_equal(out_a.cpu().numpy(), cw)
+        if sb is not None:
+            assert np.array_equal(out_b.cpu().numpy(), cw[: small_nb * n])
+    eng.close()
+    if not hit:
+        pytest.skip("the runtime never reused a destroyed stream's handle")
+
+
+def test_default_stream_work_outlives_nothing_at_close(oracle):
+    """Encode and decode queued on the default (null) stream, then close at once: destroy waits for
+    that work (its completion event is recorded although the context's own host streams do not exist
+    yet), so the outputs are complete and the freed tables were not read afterwards."""
+    nb = (1 << 19) + 3
+    n, k, data, cw = _rs_batch(oracle, nb, 37)
+    d = torch.from_numpy(data).cuda()
+    for _ in range(3):
+        eng = EccEngine(ECC_REED_SOLOMON, 512, 3)
+        r = torch.zeros(nb * n, dtype=torch.uint8, device="cuda")
+        o = torch.zeros(nb * k, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        eng.encode(d, r, nblocks=nb, stream=0)
+        eng.decode(r, o, None, write_back=False, nblocks=nb, stream=0)
+        eng.close()
+        torch.cuda.synchronize()
+        assert np.array_equal(r.cpu().numpy(), cw)
+        assert torch.equal(o, d)
 
 
 def test_pinned_releases_every_registered_range():

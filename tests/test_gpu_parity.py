@@ -177,6 +177,33 @@ def test_rs_ragged_tiles(oracle, bs, t):
         assert np.array_equal(host(raw_d), o_fixed), nb
 
 
+def test_rs_ticket_sets_after_a_small_launch(oracle):
+    """One engine, one stream: a large batch (8 XCD ticket counters), then batches of fewer than 8
+    tiles (a grid of < 8 workgroups counts on fewer counters and used to zero only those of the
+    set the large launch left dirty), then large again -- encode and decode, each vs the oracle.  A
+    stale counter would start the second large launch's tickets past tiles nobody then encodes
+    (rs_wg_tk.hpp tk_clear)."""
+    bs, t = 512, 3
+    n, k, _ = oracle.rs_sizes(bs, t)
+    eng = EccEngine(ECC_REED_SOLOMON, bs, t)
+    for step, nb in enumerate([3 * 768 * 64 + 11, 448, 100, 7, 3 * 768 * 64 + 11, 1 << 16, 130, 1 << 16]):
+        rng = rng_for("tkclear", step, nb)
+        data = rng.integers(0, 256, nb * k, dtype=np.uint8)
+        raw_d = torch.zeros(nb * n, dtype=torch.uint8, device="cuda")
+        eng.encode(dev(data), raw_d, nblocks=nb)
+        cw = oracle.rs_encode(bs, t, data)
+        assert np.array_equal(host(raw_d), cw), (step, nb)
+        bad = inject_rs_fast(rng, cw, n, t, nb)
+        o_data, o_st, o_fixed, _, _ = oracle.rs_decode(bs, t, bad)
+        raw_d = dev(bad)
+        data_d = torch.zeros(nb * k, dtype=torch.uint8, device="cuda")
+        st_d = torch.full((nb,), 77, dtype=torch.uint8, device="cuda")
+        eng.decode(raw_d, data_d, st_d, write_back=True, nblocks=nb)
+        assert np.array_equal(host(st_d), o_st), (step, nb)
+        assert np.array_equal(host(data_d), o_data), (step, nb)
+        assert np.array_equal(host(raw_d), o_fixed), (step, nb)
+
+
 def test_rs_full_batch_roundtrip_properties():
     """BASELINE configs[1]/[2] at full size (2^20 RS(255,249) blocks): encode, one byte error per
     block, decode with write-back.  Size-independent properties: every payload restored, every
