@@ -185,6 +185,25 @@ __device__ __forceinline__ void ham_stage_write(uint8_t* buf, const HamEncStage<
         *(uint4*)(buf + 16u * (64u * k + lane)) = s.v[k];
 }
 
+// bytes [lo, hi) of a 16-byte piece (the partial first / last piece of an unaligned row: the
+// other bytes belong to the neighbouring rows, written by other waves): whole dwords where the
+// range covers them, single bytes at the two ends
+__device__ __forceinline__ void store_piece_part(uint8_t* dst, const uint32_t (&o)[4], uint32_t lo, uint32_t hi)
+{
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint32_t d0 = 4 * u;
+        if (lo <= d0 && d0 + 4 <= hi) {
+            *(uint32_t*)(dst + d0) = o[u];
+        } else {
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if (d0 + b >= lo && d0 + b < hi)
+                    dst[d0 + b] = (uint8_t)(o[u] >> (8 * b));
+        }
+    }
+}
+
 template <int NP>
 __global__ __launch_bounds__(256) void ham_fast_encode_kernel(const uint8_t* __restrict__ data, uint8_t* __restrict__ raw,
     const uint8_t* __restrict__ skip, uint64_t nblocks_all, HamFast a)
@@ -211,9 +230,13 @@ __global__ __launch_bounds__(256) void ham_fast_encode_kernel(const uint8_t* __r
         const uint32_t m = (uint32_t)((blk * a.ds) & 15u); // payload byte 0 sits at LDS byte m
         uint8_t* rb = raw + blk * a.bs;
         const bool skipped = skip && PPFS_DBG_OK(skip + blk, 1, skip, nblocks_all) && skip[blk] == 5;
-        // old raw tail word (bits past L keep their contents): the last word of the block
+        // old raw tail word (bits past L keep their contents): the last word of the block.  When the
+        // unused tail is whole bytes (block_size 4096: bytes 4093..4095) it is not read at all: the
+        // last piece's store leaves those bytes alone instead (round 4: the 4-byte read fetched a
+        // whole line per block, 1.039x the algorithmic read bytes)
+        const bool tail_bytes = ((a.L + 1u) & 7u) == 0u;
         uint32_t old_tail = 0;
-        if (lane == 63 && PPFS_DBG_OK(rb + 4 * lastw, 4, raw, nblocks_all * a.bs))
+        if (!tail_bytes && lane == 63 && PPFS_DBG_OK(rb + 4 * lastw, 4, raw, nblocks_all * a.bs))
             old_tail = bswap(*(const uint32_t*)(rb + 4 * lastw));
         uint32_t X[NP][4];
         uint32_t ax = 0, aw = 0;
@@ -270,6 +293,13 @@ __global__ __launch_bounds__(256) void ham_fast_encode_kernel(const uint8_t* __r
                     X[k][0] |= ((S >> j) & 1u) << 31;
                 }
                 if (k == NP - 1 && lane == 63) {
+                    if (tail_bytes) { // bytes [0, (L + 1) / 8 - (bs - 16)) of the last piece only
+                        const uint32_t o[4] = { bswap(X[k][0]), bswap(X[k][1]), bswap(X[k][2]), bswap(X[k][3]) };
+                        const uint32_t nb = (a.L + 1u) / 8u - (a.bs - 16u);
+                        if (PPFS_DBG_OK(rb + a.bs - 16u, nb, raw, nblocks_all * a.bs))
+                            store_piece_part(rb + a.bs - 16u, o, 0u, nb);
+                        continue;
+                    }
                     const uint32_t keep = ~top_bits(a.L - 32 * lastw + 1);
                     X[k][3] = (X[k][3] & ~keep) | (old_tail & keep);
                 }
@@ -282,25 +312,6 @@ __global__ __launch_bounds__(256) void ham_fast_encode_kernel(const uint8_t* __r
         __builtin_amdgcn_wave_barrier();
         if (!BF_PREFETCH && nx < nblocks)
             ham_stage_load<NP>(st, data, nx, a, lane);
-    }
-}
-
-// bytes [lo, hi) of a 16-byte piece (the partial first / last piece of an unaligned row: the
-// other bytes belong to the neighbouring rows, written by other waves): whole dwords where the
-// range covers them, single bytes at the two ends
-__device__ __forceinline__ void store_piece_part(uint8_t* dst, const uint32_t (&o)[4], uint32_t lo, uint32_t hi)
-{
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const uint32_t d0 = 4 * u;
-        if (lo <= d0 && d0 + 4 <= hi) {
-            *(uint32_t*)(dst + d0) = o[u];
-        } else {
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                if (d0 + b >= lo && d0 + b < hi)
-                    dst[d0 + b] = (uint8_t)(o[u] >> (8 * b));
-        }
     }
 }
 
@@ -407,38 +418,45 @@ __global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restric
             for (int k = 0; k < NP; ++k)
                 R[k] = gld16c(raw + nx * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
         }
-        uint32_t ax = 0, aw = 0;
+        // Syndrome (round 4: fewer VALU).  S = XOR of the positions of the set bits = (XOR over odd-
+        // parity words w of w) << 5 | qbits(XOR of all words).  Parity is byte-order free, so the
+        // words stay in memory order and only the XOR of all words is byte-swapped.  The odd-parity
+        // word XOR is built from the parities of word groups (parity(a) ^ parity(b) = parity(a ^ b)):
+        // the lane's word w = 256 k + 4 lane + u contributes 4 lane if odd, plus 256 k + u, whose bits
+        // are the parities of the words with that bit of k or u set.  Only the block's last word (lane
+        // 63, piece NP - 1, u = 3) holds bits past L, which are not part of the code.
+        uint32_t xk[NP][4];
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                xk[k][u] = X[k][u];
+        if (lane == 63)
+            xk[NP - 1][3] &= bswap(top_bits(a.L - 32u * lastw + 1u));
+        uint32_t ax = 0, xu0 = 0, xu1 = 0, xk0 = 0, xk1 = 0;
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t w = 256u * k + 4u * lane + u;
-                uint32_t x = bswap(X[k][u]);
-                if (32 * w + 31 > a.L)
-                    x &= top_bits(a.L >= 32 * w ? a.L - 32 * w + 1 : 0); // used bits only
-                ax ^= x;
-                aw ^= (__builtin_popcount(x) & 1u) ? w : 0u;
-            }
+            const uint32_t g = xk[k][0] ^ xk[k][1] ^ xk[k][2] ^ xk[k][3];
+            ax ^= g;
+            xu0 ^= xk[k][1] ^ xk[k][3];
+            xu1 ^= xk[k][2] ^ xk[k][3];
+            if (k & 1)
+                xk0 ^= g;
+            if (k & 2)
+                xk1 ^= g;
         }
-        const uint32_t red = wave_xor(((aw << 5 | qbits(ax)) << 1) | (__builtin_popcount(ax) & 1u));
+        const uint32_t pall = __builtin_popcount(ax) & 1u;
+        const uint32_t aw = (pall ? 4u * lane : 0u) | (__builtin_popcount(xu0) & 1u) | ((__builtin_popcount(xu1) & 1u) << 1)
+            | ((__builtin_popcount(xk0) & 1u) << 8) | ((__builtin_popcount(xk1) & 1u) << 9);
+        const uint32_t red = wave_xor(((aw << 5 | qbits(bswap(ax))) << 1) | pall);
         const uint32_t S = red >> 1, par = red & 1u;
         const uint32_t st = par ? 1u : (S ? 5u : 0u);
         uint8_t* rb = raw + blk * a.bs;
-        if (par) {
-            // flip bit S in the owner lane's register copy; write back that byte
-            const uint32_t ws = S >> 5;
-            if (((ws >> 2) & 63u) == lane) {
-                const uint32_t flip = 0x80u << (8 * ((S >> 3) & 3u)) >> (S & 7u);
-#pragma unroll
-                for (int k = 0; k < NP; ++k)
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-                        if (256u * k + 4u * lane + u == ws)
-                            X[k][u] ^= flip;
-                if (write_back && PPFS_DBG_OK(rb + (S >> 3), 1, raw, nblocks_all * a.bs))
-                    rb[S >> 3] = (uint8_t)(rb[S >> 3] ^ (0x80u >> (S & 7u)));
-            }
-        }
+        // the owner lane of bit S (raw word S >> 5 = 256 k + 4 lane + u) flips it in the LDS image
+        // below and writes the byte back
+        const bool owner = par && ((S >> 7) & 63u) == lane;
+        if (owner && write_back && PPFS_DBG_OK(rb + (S >> 3), 1, raw, nblocks_all * a.bs))
+            rb[S >> 3] = (uint8_t)(rb[S >> 3] ^ (0x80u >> (S & 7u)));
         if (status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
             status[blk] = (uint8_t)st;
         if (data && st != 5) {
@@ -447,6 +465,10 @@ __global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restric
                 *(uint4*)(img + 16u * (64u * k + lane)) = make_uint4(X[k][0], X[k][1], X[k][2], X[k][3]);
             if (lane < 4)
                 *(uint32_t*)(img + NP * 1024 + 4 * lane) = 0;
+            // the correction, after the image stores of the same wave (LDS ops of a wave run in order)
+            if (owner)
+                __hip_atomic_fetch_xor((uint32_t*)(img + ((S >> 5) << 2)), 0x80u << (8 * ((S >> 3) & 3u)) >> (S & 7u),
+                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             // payload row [blk ds, +ds) as 16-byte pieces of the global 16-byte grid
@@ -1065,6 +1087,8 @@ extern "C" hipError_t ppfs_ham_fast_decode(uint8_t* r, uint8_t* d, uint8_t* st, 
 {
     const bf::HamFast a { bs, ds, L, nb * (uint64_t)ds };
     if ((nb + 4ull * bf::BF_BPW - 1) / (4ull * bf::BF_BPW) > (1ull << 30))
+        return hipErrorInvalidValue;
+    if (L < 32u * (bs / 4u - 1u) || L >= 8u * bs) // the kernel masks the last word only (true for 1-4 KiB)
         return hipErrorInvalidValue;
     PPFS_NP_DISPATCH(bs, bf::ham_fast_decode_kernel, (nb + bf::BF_BPW - 1) / bf::BF_BPW, s, r, d, st, nb, wb, a)
     return hipGetLastError();

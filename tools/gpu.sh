@@ -6,6 +6,7 @@
 #   tests[=K]    pytest -m gpu over tests/ (K: a -k expression; '+' stands for a space)
 #   lifecycle    pytest -m gpu over tests/test_gpu_lifecycle.py
 #   rs           the RS parity tests (tests/test_gpu_parity.py -k rs)
+#   parity       every test of tests/test_gpu_parity.py (RS, CRC, Hamming, parity vs the oracle)
 #   smoke        __graft_entry__.smoke()
 #   bench        the default bench line (no CPU column, no host-inclusive leg)
 #   benchfull    the default bench line with every leg (what the driver runs)
@@ -33,6 +34,9 @@ for step in "$@"; do
     rs)
         timeout -k 10 600 $PYT tests/test_gpu_parity.py -k rs > ${O}_rs.log 2>&1
         rc=$?; tail -3 ${O}_rs.log; [ $rc -eq 0 ] || exit $rc ;;
+    parity)
+        timeout -k 10 900 $PYT tests/test_gpu_parity.py > ${O}_parity.log 2>&1
+        rc=$?; tail -3 ${O}_parity.log; [ $rc -eq 0 ] || exit $rc ;;
     smoke)
         timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > ${O}_smoke.log 2>&1
         rc=$?; tail -2 ${O}_smoke.log; [ $rc -eq 0 ] || exit $rc ;;
