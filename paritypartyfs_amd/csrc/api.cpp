@@ -569,6 +569,19 @@ struct ppfs_ecc_ctx {
     size_t pin_bytes = 0; // bytes of each h_pin[] buffer (pin cache key)
 };
 
+// PPFS_ECC_TRACE=1 (diagnostics): timestamped steps of context creation on stderr
+static void trace_step(const char* what)
+{
+    static const bool on = [] {
+        const char* v = std::getenv("PPFS_ECC_TRACE");
+        return v && *v && *v != '0';
+    }();
+    if (!on)
+        return;
+    const double t = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    std::fprintf(stderr, "[ppfs_ecc %.6f] %s\n", t, what);
+}
+
 namespace {
 // ---------------------------------------------------------------------------------------
 // Memory that never synchronizes the device when it is freed.  hipFree and hipHostFree wait for
@@ -624,12 +637,15 @@ hipError_t mem_alloc(ppfs_ecc_ctx* c, void** p, size_t n)
     *p = nullptr;
     if (!c->ms) {
         const hipError_t e = hipStreamCreateWithFlags(&c->ms, hipStreamNonBlocking);
+        trace_step("mem_alloc: stream created");
         if (e != hipSuccess)
             return e;
     }
     hipError_t e = pool_alloc(p, n, c->ms);
+    trace_step("mem_alloc: pool allocation queued");
     if (e == hipSuccess)
         e = hipStreamSynchronize(c->ms); // usable from any stream from here on
+    trace_step("mem_alloc: stream synchronized");
     return e;
 }
 // caller: nothing still queued reads p
@@ -723,7 +739,11 @@ int ev_slot(ppfs_ecc_ctx* c, hipStream_t s, bool create)
 // (ctr_for) or outlive-check (destroy waits on the event re-recorded after this call).
 void order_caller_stream(ppfs_ecc_ctx* c, hipStream_t s)
 {
-    if ((c->hs[0] && s == c->hs[0]) || (c->hs[1] && s == c->hs[1]) || capturing(s))
+    static const bool off = [] { // diagnostics: PPFS_ECC_NO_ORDER=1 skips the wait
+        const char* v = std::getenv("PPFS_ECC_NO_ORDER");
+        return v && *v && *v != '0';
+    }();
+    if (off || (c->hs[0] && s == c->hs[0]) || (c->hs[1] && s == c->hs[1]) || capturing(s))
         return;
     const int i = ev_slot(c, s, false);
     if (i >= 0 && c->ev_rec[i] && hipStreamWaitEvent(s, c->ev[i], 0) != hipSuccess)
@@ -933,13 +953,16 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
         delete c;
         return fail(PPFS_ECC_EHIP, "hipSetDevice", e);
     }
+    trace_step("create: device set");
     if (c->rs_fast && c->rs_t2 <= 8) {
         const size_t cb = sizeof(uint32_t) * ppfs_ecc_ctx::kTkSlots * 2 * ppfs_ecc_ctx::kTkSetWords;
         e = mem_alloc(c, (void**)&c->d_ctr, cb);
+        trace_step("create: counters allocated");
         if (e == hipSuccess)
             e = hipMemsetAsync(c->d_ctr, 0, cb, c->ms);
         if (e == hipSuccess)
             e = hipStreamSynchronize(c->ms);
+        trace_step("create: counters zeroed");
         if (e != hipSuccess) {
             ppfs_ecc_destroy(c);
             return fail(PPFS_ECC_EHIP, "ticket counters", e);
@@ -949,14 +972,17 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
         // through a page-locked bounce buffer: the engine never hands pageable memory to a copy
         uint8_t* bounce = nullptr;
         e = mem_alloc(c, (void**)&c->d_tables, tables.size());
+        trace_step("create: tables allocated");
         if (e == hipSuccess)
             e = pin_alloc((void**)&bounce, tables.size(), kPinStage);
+        trace_step("create: bounce buffer");
         if (e == hipSuccess) {
             std::memcpy(bounce, tables.data(), tables.size());
             e = dma_async(c->d_tables, bounce, tables.size(), hipMemcpyHostToDevice, c->ms);
             if (e == hipSuccess)
                 e = hipStreamSynchronize(c->ms);
         }
+        trace_step("create: tables uploaded");
         if (bounce) {
             // whatever e is: no copy from the bounce may still be queued when it returns to the cache
             if (e != hipSuccess)
@@ -1609,6 +1635,7 @@ static int server_launch(ppfs_ecc_ctx* c)
 {
     const uint32_t gen = (++c->srv_gen) & ~ppfs::SRV_EXITED;
     c->srv_gen = gen;
+    trace_step("server: launch");
     __atomic_store_n(&c->h_box->stop, 0u, __ATOMIC_RELEASE);
     if (c->p.ecc_type == PPFS_ECC_REED_SOLOMON && c->rs_fast)
         HIP_TRY(ppfs_rs_server_launch(c->rs_t2, c->d_box, c->d_zc, c->zc_bytes, c->d_tables, gen, kSrvIdleUs, c->srv_stream),
@@ -1667,7 +1694,14 @@ static int server_call(ppfs_ecc_ctx* c, HostOp op, const Layout& L, size_t nb, i
         const int r = ensure_box(c);
         if (r)
             return r;
-        HIP_TRY(hipStreamCreateWithFlags(&c->srv_stream, hipStreamNonBlocking), "server stream");
+        const char* pe = std::getenv("PPFS_ECC_SRV_PRIO"); // diagnostics: the server on a high-priority stream
+        if (pe && *pe && *pe != '0') {
+            int least = 0, greatest = 0;
+            HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest), "stream priorities");
+            HIP_TRY(hipStreamCreateWithPriority(&c->srv_stream, hipStreamNonBlocking, greatest), "server stream");
+        } else {
+            HIP_TRY(hipStreamCreateWithFlags(&c->srv_stream, hipStreamNonBlocking), "server stream");
+        }
     }
     SrvBox* b = c->h_box;
     const SrvLayout sl = srv_layout((uint32_t)nb, c->data, c->raw);

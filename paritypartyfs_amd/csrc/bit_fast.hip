@@ -166,10 +166,14 @@ __device__ __forceinline__ void ham_stage_load(HamEncStage<NP>& s, const uint8_t
         if (p < npc) {
             if (g + 16 <= a.data_bytes) {
                 v = gld16c(data + g, data, a.data_bytes);
-            } else {
+            } else { // the batch's last bytes: one flat predicated load per byte (no nested
+                     // divergence, which spilled the exec masks of 16 levels into SGPRs)
+                const uint32_t nb = g < a.data_bytes ? (uint32_t)(a.data_bytes - g) : 0u;
                 uint32_t w[4] = { 0, 0, 0, 0 };
-                for (uint32_t b = 0; b < 16 && g + b < a.data_bytes; ++b)
-                    w[b >> 2] |= (uint32_t)data[g + b] << (8 * (b & 3));
+#pragma unroll
+                for (uint32_t b = 0; b < 16; ++b)
+                    if (b < nb)
+                        w[b >> 2] |= (uint32_t)data[g + b] << (8 * (b & 3));
                 v = make_uint4(w[0], w[1], w[2], w[3]);
             }
         }

@@ -160,8 +160,8 @@ __device__ __forceinline__ void win5x1(Win5& w0, uint32_t a0)
 {
     asm volatile("ds_read2_b32 %0, %3 offset1:1\n\tds_read2_b32 %1, %3 offset0:2 offset1:3\n\tds_read_b32 %2, %3 offset:16\n\t"
                  "s_waitcnt lgkmcnt(0)"
-                 : "=v"(w0.d01), "=v"(w0.d23), "=v"(w0.d4)
-                 : "v"(a0)
+                 : "=&v"(w0.d01), "=&v"(w0.d23), "=&v"(w0.d4) // early clobber: no result may overwrite
+                 : "v"(a0)                                        // the address before the last read issues
                  : "memory");
 }
 __device__ __forceinline__ void win5x3(Win5& w0, Win5& w1, Win5& w2, uint32_t a0, uint32_t a1, uint32_t a2)
@@ -198,8 +198,13 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
     using D = Lds<T2, false, NBUF, false, 1>; // SL + SLX tables
     constexpr int BUF = D::BUFB;
     constexpr uint32_t OFF_TK = D::BYTES; // 4 ticket slots: slot i & 3 = tile of iteration i
-    constexpr uint32_t OFF_SCHED = D::BYTES + 64; // the emission schedule (rs_sched.hpp), read once
-    constexpr int LDS_ALLOC = lds_alloc<D::BYTES + 64 + L::SCHED_BYTES, WPC>();
+    // the output tile staged in LDS (natural piece order for the stores); the emission schedule
+    // (rs_sched.hpp) is read from the same bytes once, before the first tile
+    constexpr uint32_t OFF_STG = D::BYTES + 64, OFF_SCHED = OFF_STG;
+    constexpr int OUT_PIECES = TB * 255 / 16;
+    constexpr int STG_BYTES = OUT_PIECES * 16;
+    static_assert(STG_BYTES >= L::SCHED_BYTES, "the schedule fits the staging buffer");
+    constexpr int LDS_ALLOC = lds_alloc<D::BYTES + 64 + STG_BYTES, WPC>();
     static_assert(WPC * LDS_ALLOC <= 163840, "LDS for WPC workgroups per CU");
     constexpr int K = L::K;
     constexpr int IN_PIECES = TB * K / 16;
@@ -294,19 +299,29 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
             win5x3(w[0], w[1], w[2], lb + ea[0], lb + ea[1], lb + ea[2]);
 #pragma unroll
             for (int k = 0; k < 3; ++k)
-                if (PPFS_DBG_OK(dst + eo[k], 16, raw, nblocks * 255u))
-                    st_nt<NTST>(dst + eo[k], win_piece(w[k], esh[k]));
+                *(uint4*)(lds + OFF_STG + eo[k]) = win_piece(w[k], esh[k]);
         }
-        { // round 3: the last interior pieces, then the boundary pieces (general merge), one store
+        { // round 3: the last interior pieces, then the boundary pieces (general merge)
             uint4 o;
             if (kind3 == 0u) {
                 Win5 w;
                 win5x1(w, lds_addr(lds) + buf + ea[3]);
                 o = win_piece(w, esh[3]);
-            } else
+            } else {
                 o = enc_piece<T2>(lds, buf, par, eo[3] >> 4);
-            if (kind3 != 2u && PPFS_DBG_OK(dst + eo[3], 16, raw, nblocks * 255u))
-                st_nt<NTST>(dst + eo[3], o);
+            }
+            if (kind3 != 2u)
+                *(uint4*)(lds + OFF_STG + eo[3]) = o;
+        }
+        barrier_lds(); // S: the whole output tile staged
+        // stores in the natural order: a wave writes 1 KiB of consecutive output per instruction
+        // (round 4: stored straight from the schedule's lanes, 128-byte runs from four blocks, the
+        // t = 3 encode ran at half speed -- partial lines everywhere)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t p = tid + 256u * k;
+            if ((k < 3 || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, raw, nblocks * 255u))
+                st_nt<NTST>(dst + 16u * p, *(const uint4*)(lds + OFF_STG + 16u * p));
         }
         ++iter;
         PPFS_TK_MARK(4);
@@ -374,11 +389,11 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
     using L = RsWgLayout<T2>;
     using D = Lds<T2, true, NBUF, false, 1>; // decode tables + SLX
     constexpr uint32_t OFF_TK = D::BYTES; // 4 ticket slots: slot i & 3 = tile of iteration i
-    constexpr uint32_t OFF_SCHED = D::BYTES + 64; // the emission schedule (rs_sched.hpp), read once
-    constexpr int LDS_ALLOC = lds_alloc<D::BYTES + 64 + L::SCHED_BYTES, WPC>();
+    constexpr int LDS_ALLOC = lds_alloc<D::BYTES + 64, WPC>();
     static_assert(WPC * LDS_ALLOC <= 163840, "LDS for WPC workgroups per CU");
     constexpr int K = L::K;
     constexpr int IN_PIECES = TB * 255 / 16;
+    constexpr int OUT_PIECES = TB * K / 16;
     __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_ALLOC];
     uint32_t* const s_tk = (uint32_t*)(lds + OFF_TK);
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
@@ -400,7 +415,6 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
     } else {
         dma_tables_w0<L::TABLE_BYTES>(lds, tables, lane); // the decode tables, then SLX after them
         dma_tables_w0<L::SLX_BYTES>(lds + D::OFF_SLX, tables + L::OFF_SLX, lane);
-        dma_tables_w0<L::SCHED_BYTES>(lds + OFF_SCHED, tables + L::OFF_DSCHED, lane);
         *(uint64_t*)(lds + D::OFF_PAR + 8u * lane) = 0;
         *(uint64_t*)(lds + D::OFF_PAR + 512u + 8u * lane) = 0;
         if (tk_lane) {
@@ -411,20 +425,6 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // tile q0 / tables and the ticket landed
     barrier_lds();
-    // this thread's emission pieces (rs_sched.hpp), as in the encode
-    uint32_t ea[4], esh[4], eo[4], kind3;
-    {
-        const uint2 sc = *(const uint2*)(lds + OFF_SCHED + 8u * tid);
-        const uint32_t e[4] = { sc.x & 0xFFFFu, sc.x >> 16, sc.y & 0xFFFFu, sc.y >> 16 };
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t pk = e[k] & 0x3FFu, S = sched_dec_src<T2>(pk);
-            ea[k] = S & ~3u;
-            esh[k] = (S & 3u) * 8u;
-            eo[k] = 16u * pk;
-        }
-        kind3 = e[3] == 0xFFFFu ? 2u : (e[3] >> 15);
-    }
     PPFS_TK_MARK(0);
     uint32_t cur = 0, pc = 0, iter = 0;
     while (q0 < nfull) {
@@ -456,23 +456,13 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         PPFS_TK_MARK(4);
         if (want) {
             uint8_t* dst = data + q0 * (TB * K);
-            const uint32_t lb = lds_addr(lds) + buf;
-            Win5 w[3];
-            win5x3(w[0], w[1], w[2], lb + ea[0], lb + ea[1], lb + ea[2]);
 #pragma unroll
-            for (int k = 0; k < 3; ++k)
-                if (PPFS_DBG_OK(dst + eo[k], 16, data, nblocks * K))
-                    st_nt<NTST>(dst + eo[k], win_piece(w[k], esh[k]));
-            uint4 o; // round 3: interior or a piece across a block end (general merge); one store
-            if (kind3 == 0u) {
-                Win5 w3;
-                win5x1(w3, lb + ea[3]);
-                o = win_piece(w3, esh[3]);
-            } else {
-                o = dec_piece<T2>(lds, buf, eo[3] >> 4);
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t p = tid + 256u * k;
+                const uint4 o = dec_piece<T2>(lds, buf, p);
+                if ((k < 3 || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, data, nblocks * K))
+                    st_nt<NTST>(dst + 16u * p, o);
             }
-            if (kind3 != 2u && PPFS_DBG_OK(dst + eo[3], 16, data, nblocks * K))
-                st_nt<NTST>(dst + eo[3], o);
         }
         ++iter;
         PPFS_TK_MARK(5);
