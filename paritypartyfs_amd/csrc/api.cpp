@@ -1694,12 +1694,14 @@ static int server_call(ppfs_ecc_ctx* c, HostOp op, const Layout& L, size_t nb, i
         const int r = ensure_box(c);
         if (r)
             return r;
-        const char* pe = std::getenv("PPFS_ECC_SRV_PRIO"); // diagnostics: the server on a high-priority stream
-        if (pe && *pe && *pe != '0') {
-            int least = 0, greatest = 0;
-            HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest), "stream priorities");
-            HIP_TRY(hipStreamCreateWithPriority(&c->srv_stream, hipStreamNonBlocking, greatest), "server stream");
-        } else {
+        // The resident launch gets a stream of its own priority level: HIP maps streams of one
+        // priority onto GPU_MAX_HW_QUEUES hardware queues, and a stream sharing the server's queue
+        // waits behind the resident launch (round 4: another context's creation in a fresh process
+        // waited for good; with more hardware queues, or the server at high priority, it did not)
+        int least = 0, greatest = 0;
+        if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess || least == greatest
+            || hipStreamCreateWithPriority(&c->srv_stream, hipStreamNonBlocking, greatest) != hipSuccess) {
+            (void)hipGetLastError();
             HIP_TRY(hipStreamCreateWithFlags(&c->srv_stream, hipStreamNonBlocking), "server stream");
         }
     }

@@ -49,7 +49,12 @@ __device__ __forceinline__ uint32_t next_request(const SrvBox* box, uint32_t see
             if (take)
                 last = now;
             s_cmd[0] = take ? (uint32_t)w : seen;
-            s_cmd[1] = stop || (!take && (now - last > 100ull * idle_us || now - t0 > 100ull * SRV_LIFETIME_US));
+            // the lifetime holds under a continuous stream of requests too (round 4: a client that
+            // posts its next request within the 512-poll window kept one launch resident for good, and
+            // a stream sharing its hardware queue -- another context's creation -- waited forever).
+            // Leaving with a request pending is safe: the host sees EXITED and relaunches, and the
+            // new launch serves every cmd != done.
+            s_cmd[1] = stop || now - t0 > 100ull * SRV_LIFETIME_US || (!take && now - last > 100ull * idle_us);
         }
         __syncthreads();
         const uint32_t r = s_cmd[0], leave = s_cmd[1];
