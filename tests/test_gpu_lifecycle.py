@@ -196,8 +196,10 @@ def test_stream_slots_are_recycled_past_16_streams(oracle):
     torch.cuda.synchronize()
     for o in outs:
         assert np.array_equal(o.cpu().numpy(), cw)
-    for s, o in zip(streams[:4], outs[:4]):  # back on the first streams, after their slots moved on
+    for o in outs[:4]:
         o.zero_()
+    torch.cuda.synchronize()  # the zeroing (current stream) before the encodes on the other streams
+    for s, o in zip(streams[:4], outs[:4]):  # back on the first streams, after their slots moved on
         eng.encode(d, o, stream=s)
     torch.cuda.synchronize()
     for o in outs[:4]:
