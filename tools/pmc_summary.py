@@ -81,6 +81,22 @@ def main():
                         "avg_launch_ns": float(r["AverageNs"]),
                         "hbm_read_bytes_per_launch": fetch, "hbm_write_bytes_per_launch": write,
                         "hbm_bytes_per_launch": fetch + write, "counters": c}
+    # the traced run's own bench line (tools/profile_box.sh bench_line.json): its in-step kernel
+    # times (dispatch packets) against the rocprofv3 averages of the same invocation
+    bl = os.path.join(d, "bench_line.json")
+    if os.path.exists(bl) and os.path.getsize(bl) > 0:
+        line = json.loads(open(bl).read().strip().splitlines()[-1])
+        km = line.get("kernels_ms", {})
+        lines += ["", f"Bench line of the traced run: value {line.get('value')} GiB/s, in-step frac "
+                  f"{line.get('in_step_frac')}, roofline.frac {line.get('roofline', {}).get('frac')}"]
+        alg = line.get("roofline", {}).get("algorithmic_bytes_per_launch")
+        for kind, pref in (("encode", ("rs_wg_encode_tk", "rs_bs_encode")), ("decode", ("rs_wg_decode_tk", "rs_bs_decode"))):
+            for k, v in latest.items():
+                if k.startswith(pref) and km.get(kind) and alg:
+                    ra = v["avg_launch_ns"] / 1e6
+                    lines.append(f"- {kind}: in-step {km[kind] * 1e3:.2f} us (frac {alg / (km[kind] * 1e-3) / 8e12:.4f}) vs "
+                                 f"rocprofv3 avg {ra * 1e3:.2f} us over all launches (frac {alg / (ra * 1e-3) / 8e12:.4f}); "
+                                 f"ratio {km[kind] / ra:.4f}")
     lines += ["", "Counters (median per dispatch):", ""]
     for k, v in latest.items():
         lines.append(f"- `{v['kernel_full']}`: " + ", ".join(f"{a}={b:.4g}" for a, b in sorted(v["counters"].items())))
