@@ -279,6 +279,8 @@ template <int T2> std::vector<uint8_t> build_rs_wg_tables_t()
     const std::vector<uint16_t> es = ppfs::sched::build_encode(T2), ds = ppfs::sched::build_decode(T2);
     std::memcpy(out.data() + L::OFF_ESCHED, es.data(), es.size() * sizeof(uint16_t));
     std::memcpy(out.data() + L::OFF_DSCHED, ds.data(), ds.size() * sizeof(uint16_t));
+    const std::vector<uint8_t> rm = ppfs::sched::row_map(L::K);
+    std::memcpy(out.data() + L::OFF_ROWMAP, rm.data(), rm.size());
     return out;
 }
 
@@ -341,7 +343,7 @@ std::vector<uint8_t> build_rs_pair_tables(int t2)
     return out;
 }
 
-std::vector<uint8_t> build_rs_fast_tables(int t2)
+std::vector<uint8_t> build_rs_fast_tables_uncached(int t2)
 {
     if (t2 > 16)
         return build_rs_pair_tables(t2);
@@ -361,6 +363,19 @@ std::vector<uint8_t> build_rs_fast_tables(int t2)
         return s;
     }
     }
+}
+
+// the blob depends on 2t only; built once per process (the emission schedule search of the t <= 4
+// layouts takes tens of ms)
+std::vector<uint8_t> build_rs_fast_tables(int t2)
+{
+    static std::mutex mu;
+    static std::map<int, std::vector<uint8_t>> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(t2);
+    if (it == cache.end())
+        it = cache.emplace(t2, build_rs_fast_tables_uncached(t2)).first;
+    return it->second;
 }
 
 // ---------------------------------------------------------------------------------------

@@ -365,12 +365,19 @@ __device__ __forceinline__ void ham_mid_piece(const uint8_t* img, uint32_t b0, u
         j++;
     const uint32_t r0 = i0 + j + 2;
     const uint32_t n = (2u << j) - r0; // payload bits before the parity position
-    const uint32_t* src = (const uint32_t*)(img + ((r0 >> 5) << 2));
-    const uint32_t sft = r0 & 31u;
-    uint32_t E[5];
+    // the 5 dwords from raw word r0 / 32: two 16-byte-aligned reads and a dword select (round 4:
+    // 5 dword reads of windows 16 B apart put 32 lanes on 8 banks, 4-way conflicts; a ds_read_b128
+    // lane group reading consecutive 16-byte pieces is conflict-free)
+    const uint32_t q = (r0 >> 7) << 4, d = (r0 >> 5) & 3u, sft = r0 & 31u;
+    const uint4 wa = *(const uint4*)(img + q), wb = *(const uint4*)(img + q + 16u);
+    const uint32_t W[8] = { wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w };
+    uint32_t F[7], E[5];
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+        F[i] = (d & 1u) ? W[i + 1] : W[i];
 #pragma unroll
     for (int i = 0; i < 5; ++i)
-        E[i] = bswap(src[i]);
+        E[i] = bswap((d & 2u) ? F[i + 2] : F[i]);
     if (n >= 128) {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -457,9 +464,11 @@ __global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restric
         const uint32_t st = par ? 1u : (S ? 5u : 0u);
         uint8_t* rb = raw + blk * a.bs;
         // the owner lane of bit S (raw word S >> 5 = 256 k + 4 lane + u) flips it in the LDS image
-        // below and writes the byte back
+        // below and writes the corrected byte back from there (round 4: it read the byte back from
+        // global memory, a dependent load in every corrected block); without a payload output there
+        // is no image, and the byte is patched in place
         const bool owner = par && ((S >> 7) & 63u) == lane;
-        if (owner && write_back && PPFS_DBG_OK(rb + (S >> 3), 1, raw, nblocks_all * a.bs))
+        if (!data && owner && write_back && PPFS_DBG_OK(rb + (S >> 3), 1, raw, nblocks_all * a.bs))
             rb[S >> 3] = (uint8_t)(rb[S >> 3] ^ (0x80u >> (S & 7u)));
         if (status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
             status[blk] = (uint8_t)st;
@@ -470,9 +479,12 @@ __global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restric
             if (lane < 4)
                 *(uint32_t*)(img + NP * 1024 + 4 * lane) = 0;
             // the correction, after the image stores of the same wave (LDS ops of a wave run in order)
-            if (owner)
+            if (owner) {
                 __hip_atomic_fetch_xor((uint32_t*)(img + ((S >> 5) << 2)), 0x80u << (8 * ((S >> 3) & 3u)) >> (S & 7u),
                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (write_back && PPFS_DBG_OK(rb + (S >> 3), 1, raw, nblocks_all * a.bs))
+                    rb[S >> 3] = img[S >> 3]; // the corrected byte (same lane: after its flip)
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             // payload row [blk ds, +ds) as 16-byte pieces of the global 16-byte grid
@@ -924,23 +936,14 @@ __global__ __launch_bounds__(256) PPFS_CRC_ENC_ATTR void crc_fast_encode_kernel(
                     nb = first_next;
                 uint4 o = shift_pieces(cur.v[k], nb, m);
                 if (k == NP - 1 && lane == 63) {
-                    uint32_t w[4] = { o.x, o.y, o.z, o.w };
-                    const uint32_t base = a.ds - 16u * (64u * (NP - 1) + 63u); // field byte 0 in the piece
-#pragma unroll
-                    for (int b = 0; b < 16; ++b) {
-                        const int32_t u = b - (int32_t)base;
-                        if (u >= 0 && u < (int32_t)a.nbc) {
-                            uint32_t byte;
-                            if (8u * (uint32_t)(u + 1) <= a.n) {
-                                byte = (st >> (a.n - 8u * (uint32_t)(u + 1))) & 0xFFu;
-                            } else {
-                                const uint32_t rbits = a.n & 7u;
-                                byte = ((st & ((1u << rbits) - 1u)) << (8 - rbits)) | (old_last & ((1u << (8 - rbits)) - 1u));
-                            }
-                            w[b >> 2] = (w[b >> 2] & ~(0xFFu << (8 * (b & 3)))) | (byte << (8 * (b & 3)));
-                        }
-                    }
-                    o = make_uint4(w[0], w[1], w[2], w[3]);
+                    // the field is the block's last nbc (<= 4) bytes (bs = ds + nbc), i.e. the top nbc
+                    // bytes of the last dword: the n CRC bits left-aligned, MSB first, a partial last
+                    // byte keeping its old low bits (round 4: byte by byte, ~100 VALU per block)
+                    const uint32_t sh = 8u * (4u - a.nbc), rbits = a.n & 7u;
+                    const uint32_t field = bswap(st << (32u - a.n)) << sh;
+                    const uint32_t fmask = 0xFFFFFFFFu << sh;
+                    const uint32_t keep = rbits ? ((1u << (8u - rbits)) - 1u) << 24 : 0u; // old low bits
+                    o.w = (o.w & ~fmask) | field | ((old_last << 24) & keep);
                 }
                 if (PPFS_DBG_OK(rb + 16u * (64u * k + lane), 16, raw, nblocks_all * a.bs))
                     gst16_raw(rb + 16u * (64u * k + lane), o);

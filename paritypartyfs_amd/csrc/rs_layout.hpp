@@ -37,11 +37,13 @@ template <int T2> struct RsWgLayout {
     static constexpr int OFF_SLX = OFF_MAP32 + 7 * MAP_STRIDE;
     static constexpr int SLX_BYTES = 3 * 16 * TBL;
     // ESCHED / DSCHED (round 4): the encode / decode emission schedules (rs_sched.hpp), 256 threads
-    // x 4 rounds of u16, read from global memory once per workgroup (not copied to LDS)
+    // x 4 rounds of u16; the encode DMAs its schedule into the staging buffer once per workgroup
     static constexpr int OFF_ESCHED = OFF_SLX + SLX_BYTES;
     static constexpr int SCHED_BYTES = 2048;
     static constexpr int OFF_DSCHED = OFF_ESCHED + SCHED_BYTES;
-    static constexpr int BLOB_BYTES = OFF_DSCHED + SCHED_BYTES;
+    // ROWMAP (round 4): the encode's lane -> payload row of phase 1 (rs_sched.hpp row_map), 64 bytes
+    static constexpr int OFF_ROWMAP = OFF_DSCHED + SCHED_BYTES;
+    static constexpr int BLOB_BYTES = OFF_ROWMAP + 64;
     static_assert(TABLE_BYTES % 16 == 0 && BLOB_BYTES % 16 == 0, "tables are copied in 16-byte pieces");
 };
 

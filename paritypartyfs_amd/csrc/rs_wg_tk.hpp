@@ -203,7 +203,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
     constexpr uint32_t OFF_STG = D::BYTES + 64, OFF_SCHED = OFF_STG;
     constexpr int OUT_PIECES = TB * 255 / 16;
     constexpr int STG_BYTES = OUT_PIECES * 16;
-    static_assert(STG_BYTES >= L::SCHED_BYTES, "the schedule fits the staging buffer");
+    static_assert(STG_BYTES >= L::SCHED_BYTES + 64, "the schedule and row map fit the staging buffer");
     constexpr int LDS_ALLOC = lds_alloc<D::BYTES + 64 + STG_BYTES, WPC>();
     static_assert(WPC * LDS_ALLOC <= 163840, "LDS for WPC workgroups per CU");
     constexpr int K = L::K;
@@ -213,7 +213,6 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
     const bool dmaw = wave != 0, tk_lane = wave == 0 && lane == 0;
     const uint32_t kd = dmaw ? dma_count<IN_PIECES>(wave) : 0u; // this wave's DMA instructions per tile
-    const uint32_t row = lane_row(lane);
     const uint64_t nfull = nblocks / TB, ntiles = (nblocks + TB - 1) / TB;
     const TkGeom g = tk_geom();
     uint32_t* const my_ctr = ctr + 32u * g.xc; // 128-byte lines
@@ -236,6 +235,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
         dma_tables_w0<L::OFF_MAP>(lds, tables, lane); // SL, then SLX in the place of MAP
         dma_tables_w0<L::SLX_BYTES>(lds + D::OFF_SLX, tables + L::OFF_SLX, lane);
         dma_tables_w0<L::SCHED_BYTES>(lds + OFF_SCHED, tables + L::OFF_ESCHED, lane);
+        dma_tables_w0<64>(lds + OFF_SCHED + L::SCHED_BYTES, tables + L::OFF_ROWMAP, lane);
         *(uint64_t*)(lds + D::OFF_PAR + 8u * lane) = 0; // both parity slot sets (2 x 64 x 8 B)
         *(uint64_t*)(lds + D::OFF_PAR + 512u + 8u * lane) = 0;
         if (tk_lane) {
@@ -252,6 +252,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
     // this thread's emission pieces, one per round (rs_sched.hpp): rounds 0-2 are interior pieces
     // (LDS window at a[k], funnel shift sh[k], output byte o[k]); round 3 interior, boundary or none
     uint32_t ea[4], esh[4], eo[4], kind3;
+    const uint32_t row = lds[OFF_SCHED + L::SCHED_BYTES + lane]; // phase 1's payload row (rs_sched.hpp row_map)
     {
         const uint2 sc = *(const uint2*)(lds + OFF_SCHED + 8u * tid);
         const uint32_t e[4] = { sc.x & 0xFFFFu, sc.x >> 16, sc.y & 0xFFFFu, sc.y >> 16 };

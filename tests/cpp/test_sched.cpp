@@ -8,8 +8,13 @@
 //     (src & ~3), 4 funnel shifts by (src & 3) * 8 -- equals the codeword / payload bytes of that
 //     piece, on random rows;
 //   - the window reads of a 32-lane half (ds_read_b32 lane group) conflict no more than the natural
-//     order p = tid + 256 k does (printed: LDS cycles of the window reads per tile).
+//     order p = tid + 256 k does (printed: LDS cycles of the window reads per tile);
+//   - the encode's staging stores (ds_write_b128, 8-lane groups, banks (a / 4) mod 32) of rounds
+//     0-2 are conflict-free for 2t = 4 and 6 (printed: LDS cycles per tile, all rounds);
+//   - row_map(K) is a permutation of the 64 rows whose lanes 0-31 read their row starts on distinct
+//     banks and lanes 32-63 at most 2 to a bank (phase 1's dword reads).
 // Prints "ALL PASSED".
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -80,7 +85,7 @@ static void check(int t2, bool dec)
         }
     }
     std::vector<int> seen(npieces, 0);
-    int interior = 0, boundary = 0, cyc_sched = 0, cyc_nat = 0;
+    int interior = 0, boundary = 0, cyc_sched = 0, cyc_nat = 0, cyc_stage = 0;
     for (uint32_t k = 0; k < 4; ++k) {
         for (uint32_t w = 0; w < 4; ++w) {
             std::vector<uint32_t> s_lane(64, ~0u), n_lane(64, ~0u);
@@ -123,13 +128,47 @@ static void check(int t2, bool dec)
             CHECK(k == 3 || have == 64, "t2 %d dec %d: wave %u round %u has %d pieces", t2, dec, w, k, have);
             cyc_sched += window_cycles(s_lane);
             cyc_nat += window_cycles(n_lane);
+            // staging stores: per 8-lane group, the most pieces on one bank quad (p mod 8)
+            for (uint32_t g = 0; g < 8; ++g) {
+                int quad[8] = {}, m = 0, n = 0;
+                for (uint32_t l = 8 * g; l < 8 * g + 8; ++l) {
+                    const uint16_t e = sc[4 * (64 * w + l) + k];
+                    if (e != kNone) {
+                        m = std::max(m, ++quad[e & 7u]);
+                        ++n;
+                    }
+                }
+                cyc_stage += m;
+                CHECK(dec || (t2 != 4 && t2 != 6) || k == 3 || m == 1, "t2 %d: round %u wave %u group %u stores %d-way", t2, k, w, g, m);
+            }
         }
     }
     for (uint32_t p = 0; p < npieces; ++p)
         CHECK(seen[p] == 1, "t2 %d dec %d: piece %u emitted %d times", t2, dec, p, seen[p]);
-    std::printf("2t=%d %s: %d interior + %d boundary pieces; window-read LDS cycles per tile %d (natural order %d)\n",
-        t2, dec ? "decode" : "encode", interior, boundary, cyc_sched, cyc_nat);
+    std::printf("2t=%d %s: %d interior + %d boundary pieces; window-read LDS cycles per tile %d (natural order %d); "
+                "staging-store group cycles %d (ideal 128)\n",
+        t2, dec ? "decode" : "encode", interior, boundary, cyc_sched, cyc_nat, cyc_stage);
     CHECK(cyc_sched <= cyc_nat, "t2 %d dec %d: schedule conflicts more than the natural order", t2, dec);
+}
+
+static void check_rows(uint32_t len)
+{
+    const std::vector<uint8_t> rm = row_map(len);
+    CHECK(rm.size() == 64, "row map size");
+    std::vector<int> seen(64, 0);
+    int worst[2] = { 0, 0 };
+    for (int h = 0; h < 2; ++h) {
+        int bank[32] = {};
+        for (int l = 32 * h; l < 32 * h + 32; ++l) {
+            CHECK(rm[l] < 64, "row %u", rm[l]);
+            seen[rm[l] & 63]++;
+            worst[h] = std::max(worst[h], ++bank[(len * rm[l] / 4u) & 31u]);
+        }
+    }
+    for (int r = 0; r < 64; ++r)
+        CHECK(seen[r] == 1, "len %u: row %d mapped %d times", len, r, seen[r]);
+    CHECK(worst[0] == 1 && worst[1] <= 2, "len %u: row reads %d-way / %d-way", len, worst[0], worst[1]);
+    std::printf("row_map(%u): lanes 0-31 %d-way, lanes 32-63 %d-way\n", len, worst[0], worst[1]);
 }
 
 int main()
@@ -137,6 +176,7 @@ int main()
     for (int t2 = 2; t2 <= 8; t2 += 2) {
         check(t2, false);
         check(t2, true);
+        check_rows(255u - (uint32_t)t2);
     }
     if (fails) {
         std::printf("%d FAILED\n", fails);

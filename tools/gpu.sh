@@ -15,6 +15,8 @@
 #   prof         tools/profile_box.sh TAG (rocprofv3 kernel trace + PMC passes)
 #   ab=A,B[,N]   interleaved bench A/B of two library builds (paths), N rounds (default 3)
 #   tktrace      phase traces of the t <= 4 kernels (the trace build, tools/build_alt.sh)
+#   lds[=ARGS]   one rocprofv3 PMC pass (SQ_LDS_IDX_ACTIVE, SQ_LDS_BANK_CONFLICT) over a short bench
+#                run (ARGS: extra bench flags, '+' for a space): conflict cycles / LDS cycles per kernel
 set -o pipefail
 TAG=${1:?tag}
 shift
@@ -71,6 +73,14 @@ for step in "$@"; do
         T=$PWD/paritypartyfs_amd/_lib/alt/libppfs_ecc_trace.so
         PPFS_ECC_LIB=$T timeout -k 10 120 python tools/tk_trace.py 2> /dev/null > ${O}_tktrace.jsonl || { tail ${O}_tktrace.jsonl; exit 1; }
         cat ${O}_tktrace.jsonl ;;
+    lds | lds=*)
+        A=${step#lds}; A=${A#=}; A=${A//+/ }
+        R=/tmp/lds_${TAG}_$$; mkdir -p $R/lds
+        ( cd /tmp && TMPDIR=/tmp timeout -s KILL 240 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT -d $R/lds -o lds \
+            --output-format csv -- python3 $OLDPWD/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-host-inclusive \
+            --no-configs $A ) > ${O}_lds.log 2>&1 || { tail -5 ${O}_lds.log; exit 1; }
+        python3 tools/pmc_reduce.py $R ${O}_lds.json && rm -rf $R
+        python3 -c "import json,sys; d=json.load(open(sys.argv[1])); [print(k, 'conflict/active %.4f' % (v['SQ_LDS_BANK_CONFLICT'] / max(v['SQ_LDS_IDX_ACTIVE'], 1)), v) for k, v in d.items() if v.get('SQ_LDS_IDX_ACTIVE')]" ${O}_lds.json ;;
     *)
         echo "unknown step $step"; exit 2 ;;
     esac

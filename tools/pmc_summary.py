@@ -81,6 +81,18 @@ def main():
                         "avg_launch_ns": float(r["AverageNs"]),
                         "hbm_read_bytes_per_launch": fetch, "hbm_write_bytes_per_launch": write,
                         "hbm_bytes_per_launch": fetch + write, "counters": c}
+    # per-dispatch durations (tools/trace_reduce.py): the in-step launches apart from the rest
+    durs = {}
+    tdp = os.path.join(d, "trace_durations.json")
+    if os.path.exists(tdp):
+        shutil.copy(tdp, os.path.join(prof, f"{tag}_trace_durations.json"))
+        for k, v in json.load(open(tdp)).items():
+            durs[short(k)] = v
+        for k, v in latest.items():
+            st = (durs.get(v["kernel_full"]) or {}).get("in_step")
+            if st:
+                v["avg_launch_ns_in_step"] = st["mean_us"] * 1e3
+                v["in_step_launches"] = st["n"]
     # the traced run's own bench line (tools/profile_box.sh bench_line.json): its in-step kernel
     # times (dispatch packets) against the rocprofv3 averages of the same invocation
     bl = os.path.join(d, "bench_line.json")
@@ -97,6 +109,10 @@ def main():
                     lines.append(f"- {kind}: in-step {km[kind] * 1e3:.2f} us (frac {alg / (km[kind] * 1e-3) / 8e12:.4f}) vs "
                                  f"rocprofv3 avg {ra * 1e3:.2f} us over all launches (frac {alg / (ra * 1e-3) / 8e12:.4f}); "
                                  f"ratio {km[kind] / ra:.4f}")
+                    if "avg_launch_ns_in_step" in v:
+                        ri = v["avg_launch_ns_in_step"] / 1e6
+                        lines.append(f"  - rocprofv3 avg over the {v['in_step_launches']} in-step launches (tools/trace_reduce.py): "
+                                     f"{ri * 1e3:.2f} us (frac {alg / (ri * 1e-3) / 8e12:.4f}); ratio {km[kind] / ri:.4f}")
     lines += ["", "Counters (median per dispatch):", ""]
     for k, v in latest.items():
         lines.append(f"- `{v['kernel_full']}`: " + ", ".join(f"{a}={b:.4g}" for a, b in sorted(v["counters"].items())))

@@ -14,6 +14,7 @@ cd /tmp && export TMPDIR=/tmp
 B="python3 $ROOTDIR/bench.py --steps 50 --warmup 5 --prewarm-s 0.3 --no-cpu-baseline --no-host-inclusive $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $RAW/trace -o trace --output-format csv -- $B > $OUT/trace.log 2>&1 || { echo "trace failed"; tail -20 $OUT/trace.log; exit 1; }
 cp $RAW/trace/trace_kernel_stats.csv $OUT/
+python3 $ROOTDIR/tools/trace_reduce.py $RAW/trace/trace_kernel_trace.csv $OUT/trace_durations.json || echo "trace_reduce failed"
 grep '^{"metric"' $OUT/trace.log | tail -1 > $OUT/bench_line.json || true # the traced run's own bench line
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $RAW/fetch -o fetch --output-format csv -- $B > $OUT/fetch.log 2>&1 || { echo "fetch failed"; tail -20 $OUT/fetch.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $RAW/write -o write --output-format csv -- $B > $OUT/write.log 2>&1 || { echo "write failed"; tail -20 $OUT/write.log; exit 1; }

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Run one codec's encode and decode on 2^20 blocks a few times (for rocprofv3 PMC passes).
-usage: python3 tools/run_one.py {hamming,crc,parity,rs3,rs16} [block_size] [reps]"""
+usage: python3 tools/run_one.py {hamming,crc,parity,rs3,rs16} [block_size] [reps] [err]
+err: flip one bit of raw byte 100 of every block before each decode (the 1-error decode)"""
 import os
 import sys
 
@@ -24,7 +25,11 @@ out = torch.empty_like(data)
 st = torch.empty(nb, dtype=torch.uint8, device="cuda")
 for _ in range(reps):
     eng.encode(data, raw, nblocks=nb)
+err = len(sys.argv) > 4 and sys.argv[4] == "err"
+col = raw.view(nb, n)[:, 100]
 for _ in range(reps):
+    if err:
+        raw.view(nb, n)[:, 100] = col ^ 1
     eng.decode(raw, out, st, write_back=True, nblocks=nb)
 torch.cuda.synchronize()
 assert torch.equal(out, data)
