@@ -96,6 +96,9 @@ constexpr int WAVES = 4;
 constexpr bool BF_PREFETCH = PPFS_BF_PREFETCH;
 // Blocks per wave of the Hamming / parity kernels: a workgroup walks BF_BPW consecutive 4-block
 // groups (one contiguous range, so the grid keeps its address order).
+#ifndef PPFS_HAM_WB64
+#define PPFS_HAM_WB64 0 // Hamming decode write-back: the corrected byte's 64-byte region (A/B)
+#endif
 #ifndef PPFS_BF_BPW
 #define PPFS_BF_BPW 1
 #endif
@@ -234,13 +237,12 @@ __global__ __launch_bounds__(256) void ham_fast_encode_kernel(const uint8_t* __r
         const uint32_t m = (uint32_t)((blk * a.ds) & 15u); // payload byte 0 sits at LDS byte m
         uint8_t* rb = raw + blk * a.bs;
         const bool skipped = skip && PPFS_DBG_OK(skip + blk, 1, skip, nblocks_all) && skip[blk] == 5;
-        // old raw tail word (bits past L keep their contents): the last word of the block.  When the
-        // unused tail is whole bytes (block_size 4096: bytes 4093..4095) it is not read at all: the
-        // last piece's store leaves those bytes alone instead (round 4: the 4-byte read fetched a
-        // whole line per block, 1.039x the algorithmic read bytes)
-        const bool tail_bytes = ((a.L + 1u) & 7u) == 0u;
+        // old raw tail word (bits past L keep their contents): the last word of the block.  (Round 4
+        // measured the alternative for whole-byte tails -- no read, the last piece stored without
+        // them: 2 % slower on cfg4, the partial-sector write costs more than the 4-byte read's line,
+        // which is the 1.039x of the read bytes.)
         uint32_t old_tail = 0;
-        if (!tail_bytes && lane == 63 && PPFS_DBG_OK(rb + 4 * lastw, 4, raw, nblocks_all * a.bs))
+        if (lane == 63 && PPFS_DBG_OK(rb + 4 * lastw, 4, raw, nblocks_all * a.bs))
             old_tail = bswap(*(const uint32_t*)(rb + 4 * lastw));
         uint32_t X[NP][4];
         uint32_t ax = 0, aw = 0;
@@ -258,12 +260,19 @@ __global__ __launch_bounds__(256) void ham_fast_encode_kernel(const uint8_t* __r
             } else {
                 const uint32_t j = 36u - (uint32_t)__builtin_clz(w0); // log2(32 w0)
                 const uint32_t o = 8 * m + 32 * w0 - j - 2;           // stream bit of word w0, position 0
-                const uint32_t* src = (const uint32_t*)(buf + ((o >> 5) << 2));
-                const uint32_t s = o & 31u;
-                uint32_t E[5];
+                // the 5 dwords from word o / 32: two 16-byte-aligned reads and a dword select, as in
+                // ham_mid_piece (5 dword reads of windows 16 B apart: 4-way bank conflicts)
+                const uint32_t q = (o >> 7) << 4, d = (o >> 5) & 3u, s = o & 31u;
+                const uint4 wa = *(const uint4*)(buf + q), wb = *(const uint4*)(buf + q + 16u);
+                const uint32_t W[8] = { wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w };
+                const uint32_t m1 = (d & 1u) ? ~0u : 0u, m2 = (d & 2u) ? ~0u : 0u;
+                uint32_t F[7], E[5];
+#pragma unroll
+                for (int i = 0; i < 7; ++i)
+                    F[i] = (m1 & W[i + 1]) | (~m1 & W[i]);
 #pragma unroll
                 for (int i = 0; i < 5; ++i)
-                    E[i] = bswap(src[i]);
+                    E[i] = bswap((m2 & F[i + 2]) | (~m2 & F[i]));
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
                     X[k][u] = (uint32_t)((((uint64_t)E[u] << 32) | E[u + 1]) >> (32 - s));
@@ -297,13 +306,6 @@ __global__ __launch_bounds__(256) void ham_fast_encode_kernel(const uint8_t* __r
                     X[k][0] |= ((S >> j) & 1u) << 31;
                 }
                 if (k == NP - 1 && lane == 63) {
-                    if (tail_bytes) { // bytes [0, (L + 1) / 8 - (bs - 16)) of the last piece only
-                        const uint32_t o[4] = { bswap(X[k][0]), bswap(X[k][1]), bswap(X[k][2]), bswap(X[k][3]) };
-                        const uint32_t nb = (a.L + 1u) / 8u - (a.bs - 16u);
-                        if (PPFS_DBG_OK(rb + a.bs - 16u, nb, raw, nblocks_all * a.bs))
-                            store_piece_part(rb + a.bs - 16u, o, 0u, nb);
-                        continue;
-                    }
                     const uint32_t keep = ~top_bits(a.L - 32 * lastw + 1);
                     X[k][3] = (X[k][3] & ~keep) | (old_tail & keep);
                 }
@@ -371,13 +373,15 @@ __device__ __forceinline__ void ham_mid_piece(const uint8_t* img, uint32_t b0, u
     const uint32_t q = (r0 >> 7) << 4, d = (r0 >> 5) & 3u, sft = r0 & 31u;
     const uint4 wa = *(const uint4*)(img + q), wb = *(const uint4*)(img + q + 16u);
     const uint32_t W[8] = { wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w };
+    // bitwise selects (v_bfi_b32): a ?: on the lane's d compiles to a dynamic index into scratch
+    const uint32_t m1 = (d & 1u) ? ~0u : 0u, m2 = (d & 2u) ? ~0u : 0u;
     uint32_t F[7], E[5];
 #pragma unroll
     for (int i = 0; i < 7; ++i)
-        F[i] = (d & 1u) ? W[i + 1] : W[i];
+        F[i] = (m1 & W[i + 1]) | (~m1 & W[i]);
 #pragma unroll
     for (int i = 0; i < 5; ++i)
-        E[i] = bswap((d & 2u) ? F[i + 2] : F[i]);
+        E[i] = bswap((m2 & F[i + 2]) | (~m2 & F[i]));
     if (n >= 128) {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -482,11 +486,18 @@ __global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restric
             if (owner) {
                 __hip_atomic_fetch_xor((uint32_t*)(img + ((S >> 5) << 2)), 0x80u << (8 * ((S >> 3) & 3u)) >> (S & 7u),
                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (write_back && PPFS_DBG_OK(rb + (S >> 3), 1, raw, nblocks_all * a.bs))
+                if (!PPFS_HAM_WB64 && write_back && PPFS_DBG_OK(rb + (S >> 3), 1, raw, nblocks_all * a.bs))
                     rb[S >> 3] = img[S >> 3]; // the corrected byte (same lane: after its flip)
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
+            if (PPFS_HAM_WB64 && par && write_back && lane < 4u) {
+                // the corrected byte's whole 64-byte aligned region, 16 B per lane from the corrected
+                // image: full sectors, where a lone byte store is a partial-sector write
+                const uint32_t q = (((S >> 3) & ~63u) >> 4) + lane;
+                if (PPFS_DBG_OK(rb + 16u * q, 16, raw, nblocks_all * a.bs))
+                    gst16(rb + 16u * q, *(const uint4*)(img + 16u * q));
+            }
             // payload row [blk ds, +ds) as 16-byte pieces of the global 16-byte grid
             const uint64_t start = blk * a.ds, a0 = start & ~15ull;
             const uint32_t m = (uint32_t)(start - a0);

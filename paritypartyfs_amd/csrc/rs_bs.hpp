@@ -57,9 +57,6 @@ __device__ uint64_t g_bs_trace[4096 * BS_TRACE_N];
 #define PPFS_BS_TR_ARGS
 #endif
 
-#ifndef PPFS_BS_ABL_HALF
-#define PPFS_BS_ABL_HALF 0 // timing ablation: half the chain steps, each with both columns' reads
-#endif
 #ifndef PPFS_BS_LOGCHK
 #define PPFS_BS_LOGCHK 0 // decode: single-error confirmation in the log domain
 #endif
@@ -133,23 +130,6 @@ __device__ __forceinline__ void bs_lookups(uint32_t (&acc)[4], const uint8_t* ld
         a = xor3(a, w(4), w(5));
         acc[q] = xor3(a, w(6), w(7));
     }
-#if PPFS_BS_ABL_HALF
-    // timing ablation only (wrong results): the other column's 8 reads too, as a lane holding the
-    // whole 32-byte state would issue
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint32_t ad = __builtin_amdgcn_perm(i < 4 ? L.off_a : L.off_b, i < 4 ? rl : rh, 0x0C0C0000u | ((uint32_t)(i & 3) << 8) | (4u + (uint32_t)(i & 3))) ^ 16u;
-        e[i] = pair::ld16(lds, OFF_TAB + ad);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        auto w = [&](int i) -> uint32_t { return q == 0 ? e[i].x : q == 1 ? e[i].y : q == 2 ? e[i].z : e[i].w; };
-        uint32_t a = xor3(acc[q], w(0), w(1));
-        a = xor3(a, w(2), w(3));
-        a = xor3(a, w(4), w(5));
-        acc[q] = xor3(a, w(6), w(7));
-    }
-#endif
 }
 
 // Remainder column c of a LEN-byte row at LDS byte `row` (rs_pair.hpp pair_remainder with the
@@ -165,7 +145,7 @@ __device__ __forceinline__ void bs_remainder(uint32_t (&s)[4], const uint8_t* ld
     asm("" : "+v"(cm)); // a mask, not a select: keeps (dpp & cm) one v_and_b32_dpp
     uint32_t up = w[2 * NC];
 #pragma unroll
-    for (int j = NC - 1; j >= (PPFS_BS_ABL_HALF ? NC / 2 : 0); --j) {
+    for (int j = NC - 1; j >= 0; --j) {
         const uint32_t d1 = w[2 * j + 1], d0 = w[2 * j];
         uint32_t hi = __builtin_amdgcn_alignbit(up, d1, sh); // payload bytes 8j+4 .. 8j+7
         uint32_t lo = __builtin_amdgcn_alignbit(d1, d0, sh); // payload bytes 8j .. 8j+3
@@ -278,7 +258,7 @@ __device__ __forceinline__ uint32_t bs_correct(uint8_t* lds, const uint8_t* gfp,
     bool wb, uint64_t raw_bytes PPFS_BS_TR_PARAMS)
 {
     const bool err = valid && pair::pair_or<1>(s[0] | s[1] | s[2] | s[3]) != 0u;
-    if (PPFS_BS_ABL_HALF || !__builtin_amdgcn_ballot_w64(err))
+    if (!__builtin_amdgcn_ballot_w64(err))
         return 0u;
     const Gf gf { gfp };
     const uint16_t* t = (const uint16_t*)(s12p + 8192u * c); // state byte u = 16c + k

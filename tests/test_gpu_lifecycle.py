@@ -331,9 +331,11 @@ def test_time_next_launch_records_the_kernel(bs, t):
     kernel_ms, bracket_ms = ev.ms(2, 3), ev.ms(0, 1)
     assert 0.0 < kernel_ms <= bracket_ms + 1e-3
     assert torch.equal(cw, ref)
-    # disarmed: a second launch records nothing new (the stop event keeps its timestamp)
+    # disarmed: a second launch records nothing new (the stop event keeps its timestamp; reading the
+    # same pair again may differ in the last nanosecond of the tick -> ms conversion, a new launch's
+    # duration by far more)
     eng.encode(data, cw, nblocks=nb)
     torch.cuda.synchronize()
-    assert ev.ms(2, 3) == kernel_ms
+    assert abs(ev.ms(2, 3) - kernel_ms) < 1e-5
     ev.close()
     eng.close()

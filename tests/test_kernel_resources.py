@@ -1,0 +1,66 @@
+"""Code-object checks of the shipped library (CPU only): the gfx950 kernels on the hot paths use no
+scratch memory and spill no VGPRs.
+
+A per-lane select written as `cond ? a[i + 1] : a[i]` over a register array can compile to a dynamic
+index into scratch (round 4: the Hamming decode emission took 64 B of scratch per lane and ran 3x
+slower); this catches that class of regression from the kernel descriptors alone, without a GPU.
+The metadata comes from the library's offload bundles (llvm-objdump --offloading, then
+llvm-readelf --notes on each gfx950 code object), extracted into a temporary directory."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "paritypartyfs_amd", "_lib",
+                   "libppfs_ecc.so")
+
+# hot-path kernels (name fragments of the mangled names): no scratch, no VGPR spills
+HOT = ("rs_wg_encode_tk_kernel", "rs_wg_decode_tk_kernel", "rs_bs_encode_kernel", "ham_fast_encode_kernel",
+       "ham_fast_decode_kernel", "crc_fast_encode_kernel", "crc_fast_check_kernel", "parity_fast")
+# the cfg5 decode calls the general (2+ error) correction out of line: that call's frame is its only
+# scratch (a fixed few dozen bytes, touched only by blocks with 2+ errors)
+CALL_FRAME = {"rs_bs_decode_kernel": 128}
+
+
+def kernel_descriptors(tmp_path):
+    if not (os.path.exists(os.path.join(LLVM, "llvm-objdump")) and os.path.exists(os.path.join(LLVM, "llvm-readelf"))):
+        pytest.skip("ROCm LLVM tools not found")
+    if not os.path.exists(LIB):
+        pytest.skip("library not built")
+    lib = tmp_path / "l.so"
+    shutil.copy(LIB, lib)
+    subprocess.run([os.path.join(LLVM, "llvm-objdump"), "--offloading", str(lib)], cwd=tmp_path, check=True,
+                   stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    objs = sorted(p for p in os.listdir(tmp_path) if p.endswith("gfx950"))
+    assert objs, "no gfx950 code object in the library"
+    out = {}
+    for o in objs:
+        notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", o], cwd=tmp_path, check=True,
+                               capture_output=True, text=True).stdout
+        name = None
+        for line in notes.splitlines():
+            m = re.match(r"\s+\.name:\s+(\S+)", line)
+            if m:
+                name = m.group(1)
+                out.setdefault(name, {})
+                continue
+            m = re.match(r"\s+\.(private_segment_fixed_size|vgpr_spill_count|sgpr_spill_count|vgpr_count):\s+(\d+)",
+                         line)
+            if m and name:
+                out[name][m.group(1)] = int(m.group(2))
+    return out
+
+
+def test_hot_kernels_use_no_scratch(tmp_path):
+    k = kernel_descriptors(tmp_path)
+    hot = {n: d for n, d in k.items() if any(h in n for h in HOT)}
+    assert len(hot) >= 10, sorted(k)
+    bad = {n: d for n, d in hot.items() if d.get("private_segment_fixed_size", 0) or d.get("vgpr_spill_count", 0)}
+    assert not bad, bad
+    for frag, limit in CALL_FRAME.items():
+        for n, d in k.items():
+            if frag in n:
+                assert d.get("private_segment_fixed_size", 0) <= limit and d.get("vgpr_spill_count", 0) == 0, (n, d)

@@ -93,6 +93,22 @@ def main():
             if st:
                 v["avg_launch_ns_in_step"] = st["mean_us"] * 1e3
                 v["in_step_launches"] = st["n"]
+    # the same command's untraced bench line (tools/profile_box.sh bench_line_untraced.json): the
+    # profile's in-step averages reproduce its roofline.frac
+    ul = os.path.join(d, "bench_line_untraced.json")
+    if os.path.exists(ul) and os.path.getsize(ul) > 0:
+        line = json.loads(open(ul).read().strip().splitlines()[-1])
+        shutil.copy(ul, os.path.join(prof, f"{tag}_bench_untraced.json"))
+        km, alg = line.get("kernels_ms", {}), line.get("roofline", {}).get("algorithmic_bytes_per_launch")
+        lines += ["", f"Untraced bench line of the same command (same box, just before the trace): value {line.get('value')} "
+                  f"GiB/s, roofline.frac {line.get('roofline', {}).get('frac')}, in-step frac {line.get('in_step_frac')}"]
+        for kind, pref in (("encode", ("rs_wg_encode_tk", "rs_bs_encode")), ("decode", ("rs_wg_decode_tk", "rs_bs_decode"))):
+            for k, v in latest.items():
+                if k.startswith(pref) and km.get(kind) and alg and "avg_launch_ns_in_step" in v:
+                    ri = v["avg_launch_ns_in_step"] / 1e6
+                    lines.append(f"- {kind}: untraced in-step {km[kind] * 1e3:.2f} us (frac {alg / (km[kind] * 1e-3) / 8e12:.4f}) vs "
+                                 f"rocprofv3 in-step-launch avg {ri * 1e3:.2f} us (frac {alg / (ri * 1e-3) / 8e12:.4f}); "
+                                 f"ratio {km[kind] / ri:.4f}")
     # the traced run's own bench line (tools/profile_box.sh bench_line.json): its in-step kernel
     # times (dispatch packets) against the rocprofv3 averages of the same invocation
     bl = os.path.join(d, "bench_line.json")

@@ -9,7 +9,7 @@ for r in 1 2; do
         python3 -c "import json,sys; [print(sys.argv[1], sys.argv[2], json.dumps({'lib': sys.argv[1], 'round': int(sys.argv[2]), **json.loads(l)})) for l in open(sys.argv[3])]" $(basename $L) $r gpurun_out/${TAG}_cfg4_tmp.jsonl | tee -a gpurun_out/${TAG}_cfg4_ab.txt | cut -c1-400
     done
 done
-timeout -k 10 400 bash tools/pmc_py.sh ${TAG}_ham tools/run_one.py hamming 4096 5 err || exit 1
-timeout -k 10 400 bash tools/pmc_py.sh ${TAG}_crc tools/run_one.py crc || exit 1
+timeout -k 10 400 bash tools/pmc_py.sh ${TAG}_ham $PWD/tools/run_one.py hamming 4096 5 err || exit 1
+timeout -k 10 400 bash tools/pmc_py.sh ${TAG}_crc $PWD/tools/run_one.py crc || exit 1
 python3 tools/pmc_table.py gpurun_out/pmc_${TAG}_ham > gpurun_out/${TAG}_ham_pmc.txt && python3 tools/pmc_table.py gpurun_out/pmc_${TAG}_crc > gpurun_out/${TAG}_crc_pmc.txt
 cat gpurun_out/${TAG}_ham_pmc.txt gpurun_out/${TAG}_crc_pmc.txt

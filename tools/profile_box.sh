@@ -12,6 +12,10 @@ mkdir -p $OUT $RAW
 sha256sum $ROOTDIR/paritypartyfs_amd/_lib/libppfs_ecc.so | cut -d' ' -f1 > $OUT/lib.sha256
 cd /tmp && export TMPDIR=/tmp
 B="python3 $ROOTDIR/bench.py --steps 50 --warmup 5 --prewarm-s 0.3 --no-cpu-baseline --no-host-inclusive $*"
+# the same bench command untraced first: its line is what the trace's averages must reproduce (the
+# tracer adds ~4 us to every dispatch-packet interval the bench itself measures under it)
+timeout -k 10 300 $B > $OUT/untraced.log 2>&1 || { echo "untraced bench failed"; tail -20 $OUT/untraced.log; exit 1; }
+grep '^{"metric"' $OUT/untraced.log | tail -1 > $OUT/bench_line_untraced.json || true
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $RAW/trace -o trace --output-format csv -- $B > $OUT/trace.log 2>&1 || { echo "trace failed"; tail -20 $OUT/trace.log; exit 1; }
 cp $RAW/trace/trace_kernel_stats.csv $OUT/
 python3 $ROOTDIR/tools/trace_reduce.py $RAW/trace/trace_kernel_trace.csv $OUT/trace_durations.json || echo "trace_reduce failed"
