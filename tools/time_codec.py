@@ -2,7 +2,7 @@
 """Kernel-time A/B helper: median encode / clean-decode / 1-error-decode times of one codec over
 2^20 blocks with the library named by PPFS_ECC_LIB (no correctness checks: ablation builds may
 compute wrong bytes on purpose).  Prints one JSON line.
-usage: python3 tools/time_codec.py {rs3,rs16,hamming,crc} [reps]"""
+usage: python3 tools/time_codec.py {rs3,rs16,hamming,crc,parity} [reps]"""
 import json
 import os
 import sys
@@ -10,11 +10,11 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
-from paritypartyfs_amd import ECC_CRC, ECC_HAMMING, ECC_REED_SOLOMON, EccEngine, crc_implicit_to_explicit
+from paritypartyfs_amd import ECC_CRC, ECC_HAMMING, ECC_PARITY, ECC_REED_SOLOMON, EccEngine, crc_implicit_to_explicit
 
 name = sys.argv[1]
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-args = {"hamming": (ECC_HAMMING, 4096, 0, 0), "crc": (ECC_CRC, 4096, 0, crc_implicit_to_explicit(0x9960034C)),
+args = {"hamming": (ECC_HAMMING, 4096, 0, 0), "parity": (ECC_PARITY, 4096, 0, 0), "crc": (ECC_CRC, 4096, 0, crc_implicit_to_explicit(0x9960034C)),
         "rs3": (ECC_REED_SOLOMON, 512, 3, 0), "rs16": (ECC_REED_SOLOMON, 4096, 16, 0)}[name]
 eng = EccEngine(args[0], args[1], args[2], crc_polynomial_explicit=args[3])
 nb = 1 << 20
