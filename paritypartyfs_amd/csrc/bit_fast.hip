@@ -96,9 +96,6 @@ constexpr int WAVES = 4;
 constexpr bool BF_PREFETCH = PPFS_BF_PREFETCH;
 // Blocks per wave of the Hamming / parity kernels: a workgroup walks BF_BPW consecutive 4-block
 // groups (one contiguous range, so the grid keeps its address order).
-#ifndef PPFS_HAM_WB64
-#define PPFS_HAM_WB64 0 // Hamming decode write-back: the corrected byte's 64-byte region (A/B)
-#endif
 #ifndef PPFS_BF_BPW
 #define PPFS_BF_BPW 1
 #endif
@@ -486,18 +483,11 @@ __global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restric
             if (owner) {
                 __hip_atomic_fetch_xor((uint32_t*)(img + ((S >> 5) << 2)), 0x80u << (8 * ((S >> 3) & 3u)) >> (S & 7u),
                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (!PPFS_HAM_WB64 && write_back && PPFS_DBG_OK(rb + (S >> 3), 1, raw, nblocks_all * a.bs))
+                if (write_back && PPFS_DBG_OK(rb + (S >> 3), 1, raw, nblocks_all * a.bs))
                     rb[S >> 3] = img[S >> 3]; // the corrected byte (same lane: after its flip)
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            if (PPFS_HAM_WB64 && par && write_back && lane < 4u) {
-                // the corrected byte's whole 64-byte aligned region, 16 B per lane from the corrected
-                // image: full sectors, where a lone byte store is a partial-sector write
-                const uint32_t q = (((S >> 3) & ~63u) >> 4) + lane;
-                if (PPFS_DBG_OK(rb + 16u * q, 16, raw, nblocks_all * a.bs))
-                    gst16(rb + 16u * q, *(const uint4*)(img + 16u * q));
-            }
             // payload row [blk ds, +ds) as 16-byte pieces of the global 16-byte grid
             const uint64_t start = blk * a.ds, a0 = start & ~15ull;
             const uint32_t m = (uint32_t)(start - a0);

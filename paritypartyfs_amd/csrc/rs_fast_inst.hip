@@ -11,7 +11,6 @@
 #include "rs_wg_tk.hpp"
 #include "rs_pair.hpp"
 #include "rs_bs.hpp"
-#include "rs_bs4.hpp"
 #include "launch.hpp"
 
 #ifndef PPFS_T2
@@ -69,20 +68,6 @@ constexpr int ENC_WPC_STATIC = fit_wpc(wg::lds_bytes<PPFS_T2, false, ENC_NBUF>()
 #define PPFS_BS_DEC_NBUF 0 // register prefetch of the next tile (rs_bs.hpp load_wave); 1 = single LDS image
 #endif
 constexpr int BS_ENC_NW = 12, BS_DEC_NW = PPFS_BS_DEC_NW, BS_DEC_TLDS = PPFS_BS_DEC_TLDS, BS_DEC_NBUF = PPFS_BS_DEC_NBUF;
-#ifndef PPFS_BS_QUAD
-#define PPFS_BS_QUAD 0 // decode: rs_bs4.hpp, four lanes per block, 16 waves (round 4)
-#endif
-#ifndef PPFS_BS4_DEC_NW
-#define PPFS_BS4_DEC_NW 16
-#endif
-#ifndef PPFS_BS_QUAD_ENC
-#define PPFS_BS_QUAD_ENC 0 // encode: rs_bs4.hpp, four lanes per block
-#endif
-#ifndef PPFS_BS4_ENC_NW
-#define PPFS_BS4_ENC_NW 16
-#endif
-constexpr bool BS_QUAD = PPFS_BS_QUAD != 0, BS_QUAD_ENC = PPFS_BS_QUAD_ENC != 0;
-constexpr int BS4_DEC_NW = PPFS_BS4_DEC_NW, BS4_ENC_NW = PPFS_BS4_ENC_NW;
 #else
 // 8 < 2t <= 16: rs_fast.hpp lane-per-block kernels; 2t = 16 encodes with the solo image kernel
 constexpr bool SOLO_IMG = PPFS_T2 == 16;
@@ -110,12 +95,8 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
         PPFS_LAUNCH((wg::rs_wg_encode_kernel<PPFS_T2, ENC_NBUF, ENC_WPC_STATIC, 3, 1, false>), dim3(rs_tile_grid(nb, ENC_WPC_STATIC)),
             dim3(256), 0, s, d, r, nb, tab);
 #elif PPFS_T2 == 32
-    if constexpr (BS_QUAD_ENC)
-        PPFS_LAUNCH((bs4::rs_bs4_encode_kernel<PPFS_T2, BS4_ENC_NW, 1>), dim3(rs_tile_grid(nb, 1, bs4::TBQ * BS4_ENC_NW)),
-            dim3(64 * BS4_ENC_NW), 0, s, d, r, nb, tab);
-    else
-        PPFS_LAUNCH((bs::rs_bs_encode_kernel<PPFS_T2, BS_ENC_NW, 1>), dim3(rs_tile_grid(nb, 1, bs::TBW * BS_ENC_NW)),
-            dim3(64 * BS_ENC_NW), 0, s, d, r, nb, tab);
+    PPFS_LAUNCH((bs::rs_bs_encode_kernel<PPFS_T2, BS_ENC_NW, 1>), dim3(rs_tile_grid(nb, 1, bs::TBW * BS_ENC_NW)),
+        dim3(64 * BS_ENC_NW), 0, s, d, r, nb, tab);
 #else
     if constexpr (SOLO_IMG)
         PPFS_LAUNCH((pair::rs_solo_encode_img_kernel<PPFS_T2, SOLO_WPC, SOLO_NW>),
@@ -150,12 +131,8 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
         PPFS_LAUNCH((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC, 7, 1>), dim3(rs_tile_grid(nb, DEC_WPC)),
             dim3(256), 0, s, r, d, st, nb, tab, wb);
 #elif PPFS_T2 == 32
-    if constexpr (BS_QUAD)
-        PPFS_LAUNCH((bs4::rs_bs4_decode_kernel<PPFS_T2, BS4_DEC_NW, 1>), dim3(rs_tile_grid(nb, 1, bs4::TBQ * BS4_DEC_NW)),
-            dim3(64 * BS4_DEC_NW), 0, s, r, d, st, nb, tab, wb);
-    else
-        PPFS_LAUNCH((bs::rs_bs_decode_kernel<PPFS_T2, BS_DEC_NW, BS_DEC_NBUF, 1, BS_DEC_TLDS>),
-            dim3(rs_tile_grid(nb, 1, bs::TBW * BS_DEC_NW)), dim3(64 * BS_DEC_NW), 0, s, r, d, st, nb, tab, wb);
+    PPFS_LAUNCH((bs::rs_bs_decode_kernel<PPFS_T2, BS_DEC_NW, BS_DEC_NBUF, 1, BS_DEC_TLDS>),
+        dim3(rs_tile_grid(nb, 1, bs::TBW * BS_DEC_NW)), dim3(64 * BS_DEC_NW), 0, s, r, d, st, nb, tab, wb);
 #else
     PPFS_LAUNCH(rs255_decode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, r, d, st, nb, tab, wb);
 #endif

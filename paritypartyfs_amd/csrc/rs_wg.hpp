@@ -39,9 +39,6 @@ constexpr int TB = 64;      // blocks per tile
 constexpr int NTHR = 256;   // threads per workgroup
 constexpr int PAD = 16;     // front pad of a tile buffer (emission reads up to 2t bytes before row 0)
 constexpr int BUF = 16368;  // PAD + 64*255 + 32: decode emission reads up to 28 B past a piece start
-#ifndef PPFS_RS_WB64
-#define PPFS_RS_WB64 0 // t <= 4 ticket decode: single-error write-back as the fix's 64-byte region (A/B)
-#endif
 
 
 __device__ __forceinline__ void barrier_lds()
@@ -417,13 +414,10 @@ __device__ __forceinline__ void stage_bytes(uint8_t* dst, const uint8_t* __restr
 
 // Decode phase 2 (wave 0, lane = block): the reference correction for blocks with r' != 0.
 // fix(pos, e) patches codeword byte pos of the lane's row (LDS) and, with write-back, in HBM.
-// DEFER (PPFS_RS_WB64): with write-back on, a single-error fix patches the LDS row only and returns
-// its position + 1 in bits 8-15 (0: none) for the caller's write-back; bit 0 = error
-template <int T2, bool DEFER = false>
+template <int T2>
 __device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, uint32_t par, uint32_t r, bool valid,
     uint8_t* __restrict__ raw_g, uint64_t blk, bool wb, [[maybe_unused]] uint64_t raw_bytes)
 {
-    uint32_t deferred = 0;
     using L = RsWgLayout<T2>;
     const uint64_t rem = *(const uint64_t*)(lds + par + 8u * r);
     const bool err = valid && rem != 0;
@@ -460,26 +454,18 @@ __device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, ui
             if (wb && PPFS_DBG_OK(raw_g + blk * 255u + pos, 1, raw_g, raw_bytes))
                 wb_byte(raw_g + blk * 255u + pos, fixed);
         };
-        auto fix_geo = [&](uint32_t pos, uint32_t e) {
-            if (DEFER && wb) {
-                lds[row + pos] = (uint8_t)(lds[row + pos] ^ e);
-                deferred = (pos + 1u) << 8;
-            } else {
-                fix(pos, e);
-            }
-        };
         if (__builtin_amdgcn_ballot_w64(err && !geo)) {
             if (err) {
                 if (geo)
-                    fix_geo(gpos, ge);
+                    fix(gpos, ge);
                 else
                     rs_correct_general<T2>(S, gf, fix);
             }
         } else if (err && geo) {
-            fix_geo(gpos, ge);
+            fix(gpos, ge);
         }
     }
-    return (err ? 1u : 0u) | deferred;
+    return err ? 1u : 0u;
 }
 
 // ------------------------------------------------------------------------------------

@@ -448,25 +448,12 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         PPFS_TK_MARK(2);
         barrier_lds(); // B: remainders complete
         PPFS_TK_MARK(3);
-        uint32_t dpos = 0; // PPFS_RS_WB64: the deferred single-error position + 1
         if (wave == 0) {
-            const uint32_t st = phase_correct<T2, PPFS_RS_WB64 != 0>(lds, buf, par, row, true, raw, q0 * TB + row, wb,
-                nblocks * 255u);
-            dpos = st >> 8;
+            const uint32_t st = phase_correct<T2>(lds, buf, par, row, true, raw, q0 * TB + row, wb, nblocks * 255u);
             if (status && PPFS_DBG_OK(status + q0 * TB + row, 1, status, nblocks))
-                status[q0 * TB + row] = (uint8_t)(st & 1u);
+                status[q0 * TB + row] = (uint8_t)st;
         }
         barrier_lds(); // C: corrections patched into the LDS rows
-        if (PPFS_RS_WB64 && dpos != 0u) {
-            // the single-error fix's whole 64-byte region of the corrected tile (tiles are 16,320 =
-            // 255 x 64 B, so regions never leave the tile): full sectors, not a lone byte
-            const uint32_t region = (255u * row + dpos - 1u) & ~63u;
-            uint8_t* gdst = raw + q0 * (TB * 255) + region;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (PPFS_DBG_OK(gdst + 16 * i, 16, raw, nblocks * 255u))
-                    *(uint4*)(gdst + 16 * i) = *(const uint4*)(lds + buf + PAD + region + 16 * i);
-        }
         PPFS_TK_MARK(4);
         if (want) {
             uint8_t* dst = data + q0 * (TB * K);
