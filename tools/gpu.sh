@@ -1,5 +1,7 @@
 #!/bin/bash
 # One parameterised GPU-box script (round 4; replaces the one-off tools/gpu_*.sh lease scripts).
+# Kernel-time A/Bs of one codec: tools/ab_codec.sh (tools/time_codec.py); profiles:
+# tools/profile_box.sh (RS bench), tools/prof_cfg4.sh (cfg4), tools/prof_r4.sh (all three).
 #   bash tools/gpu.sh TAG STEP [STEP ...]
 # Steps run in order, each under its own time limit; the script stops at the first failure (a GPU
 # fault, abort or time limit ends the call -- nothing is retried).  Outputs: gpurun_out/TAG_*.
