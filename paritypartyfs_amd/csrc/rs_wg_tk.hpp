@@ -11,10 +11,11 @@
 // the host alternates the two.  So no workgroup has to find out that it is the last one to reset
 // the counters after the grid's final tiles (one more atomic round trip at the end of every launch).
 //
-// Startup (round 3): a workgroup's first two tiles are static (its rank among the workgroups of its
-// XCD, and that plus their number), so the DMA waves issue them first thing, before any table byte
-// or ticket arrives; wave 0 brings the tables into LDS by LDS-DMA meanwhile and takes the first
-// dynamic ticket.  Tickets continue after the 2 G_x static tiles of the XCD.
+// Startup (round 3): a workgroup's first tiles are static (its rank among the workgroups of its
+// XCD, plus multiples of their number: encode 3, decode 1), so the DMA waves issue the first ones
+// right away, before any table byte or ticket arrives; wave 0 brings the tables into LDS by LDS-DMA
+// meanwhile and takes the first dynamic ticket.  Tickets continue after the static tiles of the XCD.
+// A workgroup's tiles increase, so it stops at its first tile past the batch without skipping one.
 #include "rs_wg.hpp"
 
 namespace ppfs {
@@ -221,7 +222,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
     uint64_t tlast_ = clock64();
     const uint64_t t0_ = tlast_;
 #endif
-    // the first two tiles are static: local tickets rank and rank + gx
+    // the first three tiles are static: local tickets rank, rank + gx, rank + 2 gx
     uint64_t q0 = tk_tile(g.rank, g, nfull), q1 = tk_tile(g.rank + g.gx, g, nfull);
     uint32_t hist = 0;
     if (dmaw) {
@@ -241,8 +242,9 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
         if (tk_lane) {
             if (blockIdx.x == 0)
                 tk_clear(ctr_clear);
-            const uint32_t t2 = atomicInc(my_ctr, 0xFFFFFFFFu) + 2u * g.gx; // the tile of iteration 2
-            s_tk[2] = (uint32_t)tk_tile(t2, g, nfull);
+            s_tk[2] = (uint32_t)tk_tile(g.rank + 2u * g.gx, g, nfull); // the tile of iteration 2 (static)
+            const uint32_t t3 = atomicInc(my_ctr, 0xFFFFFFFFu) + 3u * g.gx; // the tile of iteration 3
+            s_tk[3] = (uint32_t)tk_tile(t3, g, nfull);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // tables landed, ticket returned
     }
@@ -267,19 +269,21 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
     }
     PPFS_TK_MARK(0);
     uint32_t cur = 0, pc = 0, iter = 0;
+    // Tickets (round 4): wave 0, lane 0 takes one at the END of an iteration, after the tile's stores,
+    // and publishes it after barrier B of the next (the tile of iteration + 4 of the taking one): the
+    // compiler's wait for the atomic then covers only operations a phase old.  (Taken at the top and
+    // published at the end, the wait drained the tile's fresh stores: ~700 cycles per tile of wave 0,
+    // and waves 1-3 behind it at barrier A.)  No initial value: writing the register outside wave
+    // 0's branch would make every wave wait for the ticket (the compiler tracks it per register).
+    uint32_t tk;
     while (q0 < nfull) {
         // A: tile q0 in LDS, the last emission reads done, the next ticket published (the first
-        // pass: tables, parity slots and the iteration-2 ticket in place)
+        // pass: tables, parity slots and the iteration-2 and -3 tiles in place)
         if (iter) {
             barrier_lds();
             PPFS_TK_MARK(6);
         }
         const uint64_t ahead = __builtin_amdgcn_readfirstlane(s_tk[(iter + 2u) & 3u]);
-        // no initial value: writing the register outside wave 0's branch would make every wave wait
-        // for the previous ticket (the compiler tracks its pending write per register)
-        uint32_t tk;
-        if (tk_lane)
-            tk = atomicInc(my_ctr, 0xFFFFFFFFu); // the tile of iteration iter + 3
         const uint32_t buf = D::OFF_BUF + cur * BUF, par = D::OFF_PAR + pc * 512u;
         const bool go = ahead < nfull;
         if (dmaw && go)
@@ -293,6 +297,8 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
         PPFS_TK_MARK(2);
         barrier_lds(); // B: parity slots complete
         PPFS_TK_MARK(3);
+        if (tk_lane && iter)
+            s_tk[(iter + 3u) & 3u] = (uint32_t)tk_tile(tk + 3u * g.gx, g, nfull); // the tile of iteration iter + 3
         uint8_t* dst = raw + q0 * (TB * 255);
         { // rounds 0-2, interior pieces: 4 funnel shifts each, the 3 windows read together
             const uint32_t lb = lds_addr(lds) + buf;
@@ -333,7 +339,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
             vm_wait_exact(st + kd * (hist & 1u));
         }
         if (tk_lane)
-            s_tk[(iter + 2u) & 3u] = (uint32_t)tk_tile(tk + 2u * g.gx, g, nfull); // the tile of (iteration iter - 1) + 3
+            tk = atomicInc(my_ctr, 0xFFFFFFFFu); // the tile of (iteration iter - 1) + 4, published next iteration
         PPFS_TK_MARK(5);
         cur = ring_add(cur, 1, NBUF);
         pc ^= 1u;
@@ -434,6 +440,9 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
             PPFS_TK_MARK(7);
         }
         const uint64_t q1 = __builtin_amdgcn_readfirstlane(s_tk[(iter + 1u) & 3u]);
+        // taken at the top, published at the end (round 4: taken at the end and published after the
+        // next barrier B, as the encode does, the decode ran ~1 % slower -- its wave 0 then waits for
+        // the contended atomic right before the corrections, r4q)
         uint32_t tk; // no initial value (see the encode)
         if (tk_lane)
             tk = atomicInc(my_ctr, 0xFFFFFFFFu); // the tile of iteration iter + 2
