@@ -281,6 +281,24 @@ template <int T2> std::vector<uint8_t> build_rs_wg_tables_t()
     std::memcpy(out.data() + L::OFF_DSCHED, ds.data(), ds.size() * sizeof(uint16_t));
     const std::vector<uint8_t> rm = ppfs::sched::row_map(L::K);
     std::memcpy(out.data() + L::OFF_ROWMAP, rm.data(), rm.size());
+    // SL5 / SLX5 from the nibble tables by linearity: bit m of the 64-bit chunk (byte m / 8, nibble
+    // half (m % 8) / 4, bit m % 4) contributes nibble table 2 (m / 8) + (m % 8) / 4, entry 1 << (m % 4)
+    auto five = [&](int nib_off, int five_off) {
+        for (int i = 0; i < 13; ++i)
+            for (int v = 0; v < 32; ++v)
+                for (int k = 0; k < 5; ++k) {
+                    const int m = 5 * i + k;
+                    if (!(v >> k & 1) || m >= 64)
+                        continue;
+                    const size_t src = (size_t)nib_off + (size_t)(2 * (m / 8) + (m % 8) / 4) * L::TBL + (size_t)(1 << (m % 4)) * L::ES;
+                    const size_t dst = (size_t)five_off + (size_t)i * 32 * L::ES + (size_t)v * L::ES;
+                    for (int b = 0; b < L::ES; ++b)
+                        out[dst + (size_t)b] ^= out[src + (size_t)b];
+                }
+    };
+    five(L::OFF_SL, L::OFF_SL5);
+    for (int m = 0; m < 3; ++m)
+        five(L::OFF_SLX + m * 16 * L::TBL, L::OFF_SLX5 + m * L::SL5_BYTES);
     return out;
 }
 

@@ -43,13 +43,21 @@ template <int T2> struct RsWgLayout {
     static constexpr int OFF_DSCHED = OFF_ESCHED + SCHED_BYTES;
     // ROWMAP (round 4): the encode's lane -> payload row of phase 1 (rs_sched.hpp row_map), 64 bytes
     static constexpr int OFF_ROWMAP = OFF_DSCHED + SCHED_BYTES;
-    static constexpr int BLOB_BYTES = OFF_ROWMAP + 64;
+    // SL5 / SLX5 (round 4): SL and SLX as 5-bit field tables for the encode's phase 1: table i (of
+    // 13), value v -> the contribution of v at bits [5i, 5i+5) of the 64-bit chunk; 32 entries x 8 B
+    // = 256 B, the 64 banks of a ds_read_b64 lane group (conflict-free), 13 lookups per step not 16
+    static constexpr int SL5_BYTES = 13 * 32 * ES;
+    static constexpr int OFF_SL5 = OFF_ROWMAP + 64;
+    static constexpr int OFF_SLX5 = OFF_SL5 + SL5_BYTES;
+    static constexpr int SLX5_BYTES = 3 * SL5_BYTES;
+    static constexpr int BLOB_BYTES = OFF_SLX5 + SLX5_BYTES;
     static_assert(TABLE_BYTES % 16 == 0 && BLOB_BYTES % 16 == 0, "tables are copied in 16-byte pieces");
 };
 
 constexpr int rs_wg_table_bytes(int t2)
 {
-    return 16 * 128 + 3 * 2 * t2 * 128 + 2 * t2 * 128 + GF_BYTES + 7 * 2 * t2 * 128 + 3 * 16 * 128 + 4096;
+    return t2 == 2 ? RsWgLayout<2>::BLOB_BYTES : t2 == 4 ? RsWgLayout<4>::BLOB_BYTES
+         : t2 == 6 ? RsWgLayout<6>::BLOB_BYTES : RsWgLayout<8>::BLOB_BYTES;
 }
 
 // Pair RS path (rs_pair.hpp), 16 < 2t <= 32: the same 32-byte top-aligned state, two lanes per

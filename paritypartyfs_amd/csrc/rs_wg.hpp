@@ -152,11 +152,39 @@ __device__ __forceinline__ void step8(uint32_t (&s)[2], uint32_t lo, uint32_t hi
     xor_entries<2 * NL>(s, e);
 }
 
+// The same step through the 5-bit field tables (rs_layout.hpp SL5): field i = bits [5i, 5i+5) of the
+// 64-bit chunk lo | hi << 32 (field 6 straddles the two words, field 12 has 4 bits)
+template <bool FIRST, int NB>
+__device__ __forceinline__ void step13(uint32_t (&s)[2], uint32_t lo, uint32_t hi, const uint8_t* t5)
+{
+    if constexpr (!FIRST) {
+        lo ^= s[0];
+        hi ^= s[1];
+    }
+    constexpr int NF = FIRST ? (8 * NB + 4) / 5 : 13;
+    uint2 e[NF];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+        uint32_t f;
+        if (5 * i + 5 <= 32)
+            f = __builtin_amdgcn_ubfe(lo, 5 * i, 5);
+        else if (5 * i >= 32)
+            f = __builtin_amdgcn_ubfe(hi, 5 * i - 32, 5);
+        else
+            f = __builtin_amdgcn_alignbit(hi, lo, 30) & 31u;
+        e[i] = ld8(t5 + i * 256 + f * 8u);
+    }
+    s[0] = 0;
+    s[1] = 0;
+    xor_entries<NF>(s, e);
+}
+
 // r = sum_j B[SEG S + j] x^(2t + j) mod g over segment S (SEG bytes) of a LEN-byte row at LDS byte `row`.
 // XOFF > 0 (the SLX layout, round 3): the LAST slicing step (bottom chunk) reads the segment's own
 // tables at LDS byte XOFF + 2048 (S - 1), SL with x^(64 S) folded in.  That step maps the whole
 // folded state, so the result is already r x^(64 S) mod g: no x^(64 S) map round after the chain.
-template <int T2, int LEN, int S, int SEG = 64, int XOFF = 0>
+// T5: the 5-bit field tables, SL5 at LDS 0 and the segment's SLX5 at XOFF + SL5_BYTES (S - 1)
+template <int T2, int LEN, int S, int SEG = 64, int XOFF = 0, bool T5 = false>
 __device__ __forceinline__ void seg_remainder(uint32_t (&s)[2], const uint8_t* lds, uint32_t row)
 {
     constexpr int LO = SEG * S;
@@ -173,7 +201,9 @@ __device__ __forceinline__ void seg_remainder(uint32_t (&s)[2], const uint8_t* l
         R[q] = w[q];
 #pragma unroll
     for (int c = NC - 1; c >= 0; --c) {
-        const uint8_t* sl = (XOFF > 0 && S > 0 && c == 0) ? lds + XOFF + 2048 * (S > 0 ? S - 1 : 0) : lds + RsWgLayout<T2>::OFF_SL;
+        constexpr int XSTRIDE = T5 ? RsWgLayout<T2>::SL5_BYTES : 2048;
+        const uint8_t* sl = (XOFF > 0 && S > 0 && c == 0) ? lds + XOFF + XSTRIDE * (S > 0 ? S - 1 : 0)
+                                                          : lds + (T5 ? 0 : RsWgLayout<T2>::OFF_SL);
         uint32_t lo = __builtin_amdgcn_alignbit(R[2 * c + 1], R[2 * c], sh);
         uint32_t hi = __builtin_amdgcn_alignbit(R[2 * c + 2], R[2 * c + 1], sh);
         if (c == NC - 1) {
@@ -185,9 +215,15 @@ __device__ __forceinline__ void seg_remainder(uint32_t (&s)[2], const uint8_t* l
             } else if constexpr (TOPN < 8) {
                 hi &= (1u << (8 * (TOPN - 4))) - 1u;
             }
-            step8<true, TOPN>(s, lo, hi, sl);
+            if constexpr (T5)
+                step13<true, TOPN>(s, lo, hi, sl);
+            else
+                step8<true, TOPN>(s, lo, hi, sl);
         } else {
-            step8<false, 8>(s, lo, hi, sl);
+            if constexpr (T5)
+                step13<false, 8>(s, lo, hi, sl);
+            else
+                step8<false, 8>(s, lo, hi, sl);
         }
     }
 }
@@ -218,38 +254,39 @@ template <int T2, int S> __device__ __forceinline__ void seg_map(uint32_t (&s)[2
 __device__ __forceinline__ uint32_t lane_row(uint32_t lane) { return ((lane & 31u) << 1) | (lane >> 5); }
 
 // Phase 1 for this wave's segment of block `blk`: XOR its remainder into the block's slot
-template <int T2, int LEN, int NMAP = 3, int XOFF = 0>
+template <int T2, int LEN, int NMAP = 3, int XOFF = 0, bool T5 = false>
 __device__ __forceinline__ void phase_remainder_row(uint8_t* lds, uint32_t row, uint32_t par, uint32_t wave, uint32_t blk);
 
 // NMAP = x^(64 s) maps in LDS: 3 (one per segment), or 2 (x^64, x^128; segment 3 applies both,
 // which frees 2t x 256 B of LDS for the compact encode layout); 1 = no maps: the SLX last-step
 // tables at LDS byte XOFF (seg_remainder)
-template <int T2, int LEN, int NMAP = 3, int XOFF = 0>
+template <int T2, int LEN, int NMAP = 3, int XOFF = 0, bool T5 = false>
 __device__ __forceinline__ void phase_remainder(uint8_t* lds, uint32_t buf, uint32_t par, uint32_t wave, uint32_t blk)
 {
-    phase_remainder_row<T2, LEN, NMAP, XOFF>(lds, buf + PAD + (uint32_t)LEN * blk, par, wave, blk);
+    phase_remainder_row<T2, LEN, NMAP, XOFF, T5>(lds, buf + PAD + (uint32_t)LEN * blk, par, wave, blk);
 }
 
 // the same for a LEN-byte row at LDS byte `row` (any row layout)
-template <int T2, int LEN, int NMAP, int XOFF>
+template <int T2, int LEN, int NMAP, int XOFF, bool T5>
 __device__ __forceinline__ void phase_remainder_row(uint8_t* lds, uint32_t row, uint32_t par, uint32_t wave, uint32_t blk)
 {
+    static_assert(!T5 || NMAP == 1, "5-bit tables: the SLX layout");
     static_assert(NMAP == 1 || NMAP == 2 || NMAP == 3, "x^(64 s) maps, or SLX tables");
     static_assert(NMAP != 1 || XOFF > 0, "SLX tables need their LDS offset");
     uint32_t s[2];
     if constexpr (NMAP == 1) {
         switch (wave) {
         case 0:
-            seg_remainder<T2, LEN, 0>(s, lds, row);
+            seg_remainder<T2, LEN, 0, 64, XOFF, T5>(s, lds, row);
             break;
         case 1:
-            seg_remainder<T2, LEN, 1, 64, XOFF>(s, lds, row);
+            seg_remainder<T2, LEN, 1, 64, XOFF, T5>(s, lds, row);
             break;
         case 2:
-            seg_remainder<T2, LEN, 2, 64, XOFF>(s, lds, row);
+            seg_remainder<T2, LEN, 2, 64, XOFF, T5>(s, lds, row);
             break;
         default:
-            seg_remainder<T2, LEN, 3, 64, XOFF>(s, lds, row);
+            seg_remainder<T2, LEN, 3, 64, XOFF, T5>(s, lds, row);
             break;
         }
     } else switch (wave) {
@@ -506,14 +543,16 @@ __device__ __forceinline__ void vm_wait_newer(uint32_t n)
 // COMPACT (encode only): 2 maps (phase_remainder NMAP = 2) and tile buffers sized for the 64
 // payload rows (PAD + 64 K + 32) instead of 64 codewords, so 3 ring buffers fit 3 workgroups / CU
 // MAPS = 1: the SLX last-step tables (3 x 2 KiB, seg_remainder) instead of the maps: the encode holds
-// SL + SLX (OFF_SLX = L::OFF_MAP), the decode the whole decode table prefix + SLX after it
+// SL + SLX (OFF_SLX = L::OFF_MAP), the decode the whole decode table prefix + SLX after it.
+// MAPS = 2 (encode): the 5-bit field tables SL5 + SLX5 (OFF_SLX = L::SL5_BYTES)
 template <int T2, bool DEC, int NBUF, bool COMPACT = false, int MAPS = 0> struct Lds {
     using L = RsWgLayout<T2>;
     static_assert(!(DEC && COMPACT), "compact layout: encode only");
-    static_assert(MAPS == 0 || MAPS == 1, "x^(64 s) maps or SLX tables");
-    static constexpr int NMAP = MAPS ? MAPS : COMPACT ? 2 : 3;
-    static constexpr int OFF_SLX = MAPS == 1 ? (DEC ? L::TABLE_BYTES : L::OFF_MAP) : 0;
-    static constexpr int TBL = MAPS == 1 ? OFF_SLX + L::SLX_BYTES
+    static_assert(MAPS >= 0 && MAPS <= 2, "x^(64 s) maps, SLX tables, or (encode) SL5 + SLX5");
+    static_assert(MAPS != 2 || !DEC, "5-bit tables: encode only");
+    static constexpr int NMAP = MAPS ? 1 : COMPACT ? 2 : 3;
+    static constexpr int OFF_SLX = MAPS == 2 ? L::SL5_BYTES : MAPS == 1 ? (DEC ? L::TABLE_BYTES : L::OFF_MAP) : 0;
+    static constexpr int TBL = MAPS == 2 ? OFF_SLX + L::SLX5_BYTES : MAPS == 1 ? OFF_SLX + L::SLX_BYTES
         : DEC ? L::TABLE_BYTES : L::OFF_MAP + NMAP * L::MAP_STRIDE; // encode: SL + MAP only
     static constexpr int OFF_PAR = TBL;                              // 2 x 64 x 8 B remainder slots
     static constexpr int OFF_BUF = OFF_PAR + 1024 + 64;             // + slack: par[b+1] over-read
