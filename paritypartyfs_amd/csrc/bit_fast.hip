@@ -575,15 +575,30 @@ __device__ __forceinline__ uint4 shift_pieces(uint4 own, uint4 nxt, uint32_t m)
     return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
-__device__ __forceinline__ uint4 shfl_down1(uint4 v)
+// The neighbour pieces of a wave's 16-byte pieces by whole-wave DPP moves (VALU; round 4 replaced
+// ds_bpermute + v_readlane: CRC check -0.5 %, the rest unchanged, r4w): next_piece gives lane l
+// own[l + 1] and lane 63 nxt[0] (wave_rol:1 of nxt, then wave_shl:1 of own over it -- lane 63 has
+// no wave_shl source and keeps the rotated value); prev_piece the mirror (wave_ror:1, wave_shr:1:
+// lane 0 gets prv[63], or zero for the first piece)
+__device__ __forceinline__ uint32_t next_lane(uint32_t own, uint32_t nxt)
 {
-    return make_uint4(__shfl_down(v.x, 1, 64), __shfl_down(v.y, 1, 64), __shfl_down(v.z, 1, 64), __shfl_down(v.w, 1, 64));
+    const int r = __builtin_amdgcn_mov_dpp((int)nxt, 0x134, 0xF, 0xF, false);        // wave_rol:1
+    return (uint32_t)__builtin_amdgcn_update_dpp(r, (int)own, 0x130, 0xF, 0xF, false); // wave_shl:1
 }
-
-__device__ __forceinline__ uint4 readlane0(uint4 v)
+__device__ __forceinline__ uint32_t prev_lane(uint32_t own, uint32_t prv)
 {
-    return make_uint4(__builtin_amdgcn_readlane(v.x, 0), __builtin_amdgcn_readlane(v.y, 0),
-        __builtin_amdgcn_readlane(v.z, 0), __builtin_amdgcn_readlane(v.w, 0));
+    const int r = __builtin_amdgcn_mov_dpp((int)prv, 0x13C, 0xF, 0xF, false);        // wave_ror:1
+    return (uint32_t)__builtin_amdgcn_update_dpp(r, (int)own, 0x138, 0xF, 0xF, false); // wave_shr:1
+}
+__device__ __forceinline__ uint4 next_piece(uint4 own, uint4 nxt)
+{
+    return make_uint4(next_lane(own.x, nxt.x), next_lane(own.y, nxt.y), next_lane(own.z, nxt.z), next_lane(own.w, nxt.w));
+}
+template <bool FIRST> __device__ __forceinline__ uint4 prev_piece(uint4 own, uint4 prv)
+{
+    if constexpr (FIRST)
+        prv = make_uint4(0, 0, 0, 0);
+    return make_uint4(prev_lane(own.x, prv.x), prev_lane(own.y, prv.y), prev_lane(own.z, prv.z), prev_lane(own.w, prv.w));
 }
 
 struct ParFast {
@@ -617,10 +632,7 @@ __global__ __launch_bounds__(256) void parity_fast_encode_kernel(const uint8_t* 
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
             // next piece: lane + 1 of this group, or lane 0 of the next group (or the extra piece)
-            uint4 nb = shfl_down1(cur.v[k]);
-            const uint4 first_next = readlane0(cur.v[k + 1]);
-            if (lane == 63)
-                nb = first_next;
+            const uint4 nb = next_piece(cur.v[k], cur.v[k + 1]);
             uint4 o = shift_pieces(cur.v[k], nb, m);
             if (k == NP - 1 && lane == 63)
                 o.w = (o.w & 0x00FFFFFFu) | (old_last << 24); // raw byte bs-1: old contents
@@ -683,16 +695,7 @@ __global__ __launch_bounds__(256) void parity_fast_check_kernel(const uint8_t* _
             for (int k = 0; k <= NP; ++k) {
                 const uint32_t p = 64u * k + lane;
                 const uint4 own = k < NP ? R[k] : make_uint4(0, 0, 0, 0);
-                uint4 prev = make_uint4(__shfl_up(own.x, 1, 64), __shfl_up(own.y, 1, 64), __shfl_up(own.z, 1, 64),
-                    __shfl_up(own.w, 1, 64));
-                if (lane == 0) {
-                    const uint4 l63 = k > 0 ? make_uint4(__builtin_amdgcn_readlane(R[k > 0 ? k - 1 : 0].x, 63),
-                                                  __builtin_amdgcn_readlane(R[k > 0 ? k - 1 : 0].y, 63),
-                                                  __builtin_amdgcn_readlane(R[k > 0 ? k - 1 : 0].z, 63),
-                                                  __builtin_amdgcn_readlane(R[k > 0 ? k - 1 : 0].w, 63))
-                                            : make_uint4(0, 0, 0, 0);
-                    prev = l63;
-                }
+                const uint4 prev = k == 0 ? prev_piece<true>(own, own) : prev_piece<false>(own, R[k > 0 ? k - 1 : 0]);
                 // bytes [16 - m, 16) of prev then [0, 16 - m) of own
                 const uint4 o = shift_pieces(prev, own, (16u - m) & 15u);
                 const uint4 oo = m == 0 ? own : o;
@@ -931,10 +934,7 @@ __global__ __launch_bounds__(256) PPFS_CRC_ENC_ATTR void crc_fast_encode_kernel(
                 old_last = rb[a.ds + a.nbc - 1];
 #pragma unroll
             for (int k = 0; k < NP; ++k) {
-                uint4 nb = shfl_down1(cur.v[k]);
-                const uint4 first_next = readlane0(cur.v[k + 1]);
-                if (lane == 63)
-                    nb = first_next;
+                const uint4 nb = next_piece(cur.v[k], cur.v[k + 1]);
                 uint4 o = shift_pieces(cur.v[k], nb, m);
                 if (k == NP - 1 && lane == 63) {
                     // the field is the block's last nbc (<= 4) bytes (bs = ds + nbc), i.e. the top nbc
@@ -1016,14 +1016,7 @@ __global__ __launch_bounds__(256) PPFS_CRC_ATTR void crc_fast_check_kernel(const
             for (int k = 0; k <= NP; ++k) {
                 const uint32_t p = 64u * k + lane;
                 const uint4 own = k < NP ? R[k] : make_uint4(0, 0, 0, 0);
-                uint4 prev = make_uint4(__shfl_up(own.x, 1, 64), __shfl_up(own.y, 1, 64), __shfl_up(own.z, 1, 64),
-                    __shfl_up(own.w, 1, 64));
-                if (lane == 0)
-                    prev = k > 0 ? make_uint4(__builtin_amdgcn_readlane(R[k > 0 ? k - 1 : 0].x, 63),
-                                       __builtin_amdgcn_readlane(R[k > 0 ? k - 1 : 0].y, 63),
-                                       __builtin_amdgcn_readlane(R[k > 0 ? k - 1 : 0].z, 63),
-                                       __builtin_amdgcn_readlane(R[k > 0 ? k - 1 : 0].w, 63))
-                                 : make_uint4(0, 0, 0, 0);
+                const uint4 prev = k == 0 ? prev_piece<true>(own, own) : prev_piece<false>(own, R[k > 0 ? k - 1 : 0]);
                 const uint4 oo = m == 0 ? own : shift_pieces(prev, own, (16u - m) & 15u);
                 const int32_t b0 = (int32_t)(16 * p) - (int32_t)m;
                 uint8_t* dst = data + a0 + 16ull * p;
@@ -1065,20 +1058,38 @@ template <typename K> static uint32_t bf_grid(K, uint64_t nb)
     return (uint32_t)(want < cap ? (want ? want : 1) : cap);
 }
 
+// Workgroups per CU of the streaming kernels, enforced by dynamic LDS (0 = as many as registers and
+// static LDS allow).  One 4 KiB block per wave is in flight per wave; round 4 (r4x, cfg4): the parity
+// encode at 6 waves per SIMD and the Hamming decode at 9 workgroups per CU ran 2.5 % / 1.5-2 %
+// slower than at 4 workgroups per CU (16 waves); the parity check, CRC encode (5) and the kernels
+// already at 4 (registers) showed no difference.
+static constexpr uint32_t bf_occ_lds(int wg, uint32_t static_lds)
+{
+    return wg <= 0 ? 0u : (163840u / (uint32_t)(wg + 1) + 256u > static_lds ? 163840u / (uint32_t)(wg + 1) + 256u - static_lds : 0u);
+}
+constexpr int BF_PAR_ENC_WG = 4, BF_HAM_DEC_WG = 4;
+template <int NP> static constexpr uint32_t par_enc_dyn_lds() { return bf_occ_lds(BF_PAR_ENC_WG, 0); }
+template <int NP> static constexpr uint32_t ham_dec_dyn_lds()
+{
+    return bf_occ_lds(BF_HAM_DEC_WG, bf::WAVES * (NP * 1024 + 16)); // ham_fast_decode_kernel's lds[]
+}
+template <int NP> static constexpr uint32_t no_dyn_lds() { return 0; }
+
 extern "C" int ppfs_bitfast_supported(uint32_t bs) { return bs == 1024 || bs == 2048 || bs == 4096; }
 
-#define PPFS_NP_DISPATCH(bs, KERNEL, nb, ...)                                                                         \
+#define PPFS_NP_DISPATCH_SH(bs, KERNEL, nb, SH, ...)                                                                  \
     switch (bs) {                                                                                                      \
     case 1024:                                                                                                         \
-        PPFS_LAUNCH(KERNEL<1>, dim3(bf_grid(KERNEL<1>, nb)), dim3(256), 0, __VA_ARGS__);                        \
+        PPFS_LAUNCH(KERNEL<1>, dim3(bf_grid(KERNEL<1>, nb)), dim3(256), SH<1>(), __VA_ARGS__);                  \
         break;                                                                                                         \
     case 2048:                                                                                                         \
-        PPFS_LAUNCH(KERNEL<2>, dim3(bf_grid(KERNEL<2>, nb)), dim3(256), 0, __VA_ARGS__);                        \
+        PPFS_LAUNCH(KERNEL<2>, dim3(bf_grid(KERNEL<2>, nb)), dim3(256), SH<2>(), __VA_ARGS__);                  \
         break;                                                                                                         \
     default:                                                                                                           \
-        PPFS_LAUNCH(KERNEL<4>, dim3(bf_grid(KERNEL<4>, nb)), dim3(256), 0, __VA_ARGS__);                        \
+        PPFS_LAUNCH(KERNEL<4>, dim3(bf_grid(KERNEL<4>, nb)), dim3(256), SH<4>(), __VA_ARGS__);                  \
         break;                                                                                                         \
     }
+#define PPFS_NP_DISPATCH(bs, KERNEL, nb, ...) PPFS_NP_DISPATCH_SH(bs, KERNEL, nb, no_dyn_lds, __VA_ARGS__)
 
 extern "C" hipError_t ppfs_ham_fast_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs,
     uint32_t ds, uint32_t L, hipStream_t s)
@@ -1098,7 +1109,8 @@ extern "C" hipError_t ppfs_ham_fast_decode(uint8_t* r, uint8_t* d, uint8_t* st, 
         return hipErrorInvalidValue;
     if (L < 32u * (bs / 4u - 1u) || L >= 8u * bs) // the kernel masks the last word only (true for 1-4 KiB)
         return hipErrorInvalidValue;
-    PPFS_NP_DISPATCH(bs, bf::ham_fast_decode_kernel, (nb + bf::BF_BPW - 1) / bf::BF_BPW, s, r, d, st, nb, wb, a)
+    PPFS_NP_DISPATCH_SH(bs, bf::ham_fast_decode_kernel, (nb + bf::BF_BPW - 1) / bf::BF_BPW,
+        ham_dec_dyn_lds, s, r, d, st, nb, wb, a)
     return hipGetLastError();
 }
 
@@ -1132,7 +1144,8 @@ extern "C" hipError_t ppfs_parity_fast_encode(const uint8_t* d, uint8_t* r, cons
     const bf::ParFast a { bs, nb * (uint64_t)(bs - 1) };
     if ((nb + 4ull * bf::BF_BPW - 1) / (4ull * bf::BF_BPW) > (1ull << 30))
         return hipErrorInvalidValue;
-    PPFS_NP_DISPATCH(bs, bf::parity_fast_encode_kernel, (nb + bf::BF_BPW - 1) / bf::BF_BPW, s, d, r, skip, nb, a)
+    PPFS_NP_DISPATCH_SH(bs, bf::parity_fast_encode_kernel, (nb + bf::BF_BPW - 1) / bf::BF_BPW,
+        par_enc_dyn_lds, s, d, r, skip, nb, a)
     return hipGetLastError();
 }
 
