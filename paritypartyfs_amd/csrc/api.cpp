@@ -499,12 +499,12 @@ std::vector<uint8_t> build_crc_fast_tables(uint64_t P, int n, uint32_t ds, uint3
             for (int v = 0; v < 16; ++v)
                 lt[(16 * i + v) * NL + b] = (uint32_t)c.mul(c.mod((uint64_t)v << (4 * i)), C);
     }
-    // 6-bit tables of the hot maps (bit_fast.hip PPFS_CRC_SIX): x^0, x^32, x^64, x^96, x^8192,
-    // x^2048, x^4096; sub-table j < 5 = 64 entries (v << 6j) C, then 4 entries (v << 30) C
-    if (ppfs_crc_fast_six_maps() > 0) {
+    // 6-bit tables of the lane-tree maps x^2048, x^4096 (bit_fast.hip CF_MAP6): sub-table j < 5 = 64
+    // entries (v << 6j) C, then 4 entries (v << 30) C
+    {
         uint8_t* st = (uint8_t*)(lt + 8 * 16 * NL);
-        const long sx[7] = { ex[0], ex[1], ex[2], ex[3], ex[4], ex[9], ex[10] };
-        for (int q = 0; q < 7; ++q, st += 5 * 256 + 16) {
+        const long sx[2] = { ex[9], ex[10] };
+        for (int q = 0; q < 2; ++q, st += 5 * 256 + 16) {
             const uint64_t C = c.xpow(sx[q]);
             uint32_t* e = (uint32_t*)st;
             for (int j = 0; j < 5; ++j)
@@ -512,6 +512,21 @@ std::vector<uint8_t> build_crc_fast_tables(uint64_t P, int n, uint32_t ds, uint3
                     e[64 * j + v] = (uint32_t)c.mul(c.mod((uint64_t)v << (6 * j)), C);
             for (int v = 0; v < 4; ++v)
                 e[320 + v] = (uint32_t)c.mul(c.mod((uint64_t)v << 30), C);
+        }
+    }
+    // 8-bit tables (bit_fast.hip CF_EIGHT) after the 6-bit ones: x^0, x^32, x^64, x^96 indexed by
+    // the bytes of the payload dword in memory order (table k = byte 3 - k of the value), x^8192 by
+    // the bytes of a value
+    {
+        uint32_t* e8 = (uint32_t*)(out.data() + out.size() - 5 * 4096);
+        const long ex8[5] = { ex[0], ex[1], ex[2], ex[3], ex[4] };
+        for (int q = 0; q < 5; ++q) {
+            const uint64_t C = c.xpow(ex8[q]);
+            for (int k = 0; k < 4; ++k) {
+                const int vb = q < 4 ? 3 - k : k; // the value byte that input byte k holds
+                for (int v = 0; v < 256; ++v)
+                    e8[q * 1024 + k * 256 + v] = (uint32_t)c.mul(c.mod((uint64_t)v << (8 * vb)), C);
+            }
         }
     }
     return out;

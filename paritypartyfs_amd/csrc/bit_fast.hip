@@ -744,18 +744,41 @@ constexpr int CF_M0 = 0, CF_K = 4, CF_L = 5, CF_FENC = 11, CF_FCHK = 27, CF_NMAP
 // tree's 6 dependent maps become 1 + 2; 64 per-lane maps, 32 KiB, cost a workgroup per CU.)
 constexpr int CF_LANES = 16;
 constexpr int CF_LANE_OFF = CF_NMAPS * CF_MAP;
-// The encode's hot maps (piece dwords, Horner, the two tree levels) also as 6-bit tables (5 x 64
-// entries + 4): 6 LDS lookups per map instead of 8.  (ds_read_b32 conflicts between dwords 32
-// apart, so a 64-entry table is 2-way conflicted -- PMC, DESIGN 4.0 -- and still wins.)  Stored after the lane maps, CF_MAP6 bytes each, in the order
-// M0..M3, K, L+4, L+5.  (r3zc A/B: encode -1 %; the check kernel, 5 waves per SIMD with them, ran
-// 0.8 % slower, so it keeps the nibble maps and stages only the first CF_SIX_OFF bytes.)
-#ifndef PPFS_CRC_SIX
-#define PPFS_CRC_SIX 1
-#endif
+// The two lane-tree maps (x^2048, x^4096) also as 6-bit tables (5 x 64 entries + 4): 6 LDS lookups
+// per map instead of 8 (a 64-entry table is 2-way conflicted for ds_read_b32 and still wins, r3zc).
 constexpr int CF_MAP6 = 5 * 256 + 16;
-constexpr int CF_NSIX = PPFS_CRC_SIX ? 7 : 0;
+constexpr int CF_NSIX = 2;
 constexpr int CF_SIX_OFF = CF_NMAPS * CF_MAP + CF_LANES * CF_MAP;
-constexpr int CF_BYTES = CF_SIX_OFF + CF_NSIX * CF_MAP6; // 22 KiB (+ 8.9 KiB)
+// 8-bit tables of the encode's hot maps (round 4): M0..M3, K as 4 x 256 u32 entries each: table k
+// (entries v << 2 at byte k of the input word).  The piece maps M0..M3 take the payload dword in
+// memory order (table k = (v << 8 (3 - k)) C, no byte swap), K takes values (table k = (v << 8k) C).
+// 4 lookups per map, each address one SDWA shift of a byte; 1 KiB tables put 32 random lanes on
+// 32 banks with ~3.5-way worst groups, about what the 6-bit tables' 2-way aliasing costs over 6
+// lookups, for a third of the VALU (r4z: encode 1.603 vs 1.625 ms against the 6-bit maps).
+constexpr int CF_EIGHT = 4096, CF_NEIGHT = 5;
+constexpr int CF_EIGHT_OFF = CF_SIX_OFF + CF_NSIX * CF_MAP6;
+constexpr int CF_BYTES = CF_EIGHT_OFF + CF_NEIGHT * CF_EIGHT; // 22 KiB + 2.5 KiB + 20 KiB
+// The encode's LDS image: the 16 placement maps FENC (one per payload misalignment), the lane maps,
+// the 6-bit tree maps, the 8-bit maps -- 39,456 B, 4 workgroups per CU.  (The check keeps the nibble
+// maps: on the 8-bit maps it ran the same, r4za.)
+template <int NPLACE> struct CrcLds {
+    static constexpr int PLACE = 0, LANE = NPLACE * CF_MAP, SIX = LANE + CF_LANES * CF_MAP, EIGHT = SIX + CF_NSIX * CF_MAP6;
+    static constexpr int BYTES = EIGHT + CF_NEIGHT * CF_EIGHT;
+    static_assert(SIX % 16 == 0 && EIGHT % 16 == 0 && CF_EIGHT_OFF % 16 == 0, "16-byte staging");
+    // copy the image's parts from the blob (placement maps from blob map `place0`)
+    __device__ static void stage(uint8_t* tbl, const uint8_t* __restrict__ tables, int place0)
+    {
+        auto part = [&](int dst, int src, int bytes) {
+            for (uint32_t p = threadIdx.x; p < (uint32_t)bytes / 16; p += 256)
+                *(uint4*)(tbl + dst + 16 * p) = *(const uint4*)(tables + src + 16 * p);
+        };
+        part(PLACE, place0 * CF_MAP, NPLACE * CF_MAP);
+        part(LANE, CF_LANE_OFF, CF_LANES * CF_MAP);
+        part(SIX, CF_SIX_OFF, CF_NSIX * CF_MAP6);
+        part(EIGHT, CF_EIGHT_OFF, CF_NEIGHT * CF_EIGHT);
+    }
+};
+using CE = CrcLds<16>;
 // Blocks per wave of the CRC kernels: a workgroup stages the 14 KiB of maps once and then walks
 // CRC_BPW consecutive 4-block groups (one contiguous range, so the full grid keeps its address
 // order); with one group per workgroup the map staging read as much L2 as the blocks themselves.
@@ -800,7 +823,7 @@ __device__ __forceinline__ uint32_t cmap(const uint8_t* tb, uint32_t v)
         __builtin_amdgcn_bitop3_b32(e[3], e[4], e[5], 0x96), e[6] ^ e[7], 0x96);
 }
 
-// v(x) * C mod P from C's 6-bit tables (PPFS_CRC_SIX)
+// v(x) * C mod P from C's 6-bit tables (the lane-tree maps)
 __device__ __forceinline__ uint32_t cmap6(const uint8_t* tb, uint32_t v)
 {
     uint32_t e[6];
@@ -810,16 +833,26 @@ __device__ __forceinline__ uint32_t cmap6(const uint8_t* tb, uint32_t v)
     e[5] = *(const uint32_t*)(tb + 1280 + ((v >> 30) << 2));
     return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(e[0], e[1], e[2], 0x96), e[3], e[4] ^ e[5], 0x96);
 }
-// a hot map: mi = CF_M0 .. CF_M0 + 3, CF_K, CF_L + 4, CF_L + 5
-template <int MI, bool SIX> __device__ __forceinline__ uint32_t hmap(const uint8_t* tbl, uint32_t v)
+// byte K of w, times 4 (a table entry's byte offset): one SDWA shift
+template <int K> __device__ __forceinline__ uint32_t byte4(uint32_t w)
 {
-    if constexpr (SIX && CF_NSIX > 0) {
-        constexpr int SI = MI <= CF_K ? MI : MI - CF_L + 1; // 0..4, then 5, 6
-        static_assert(SI >= 0 && SI < 7, "hot maps only");
-        return cmap6(tbl + CF_SIX_OFF + SI * CF_MAP6, v);
-    } else {
-        return cmap(tbl + MI * CF_MAP, v);
-    }
+    uint32_t r;
+    if constexpr (K == 0)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(w));
+    else if constexpr (K == 1)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(w));
+    else if constexpr (K == 2)
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(w));
+    else
+        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(w));
+    return r;
+}
+// w * C mod P from C's 8-bit tables at tb (memory-order or value-order input, see CF_EIGHT)
+__device__ __forceinline__ uint32_t cmap8(const uint8_t* tb, uint32_t w)
+{
+    const uint32_t e0 = *(const uint32_t*)(tb + byte4<0>(w)), e1 = *(const uint32_t*)(tb + 1024 + byte4<1>(w));
+    const uint32_t e2 = *(const uint32_t*)(tb + 2048 + byte4<2>(w)), e3 = *(const uint32_t*)(tb + 3072 + byte4<3>(w));
+    return __builtin_amdgcn_bitop3_b32(e0, e1, e2, 0x96) ^ e3;
 }
 
 struct CrcFast {
@@ -828,7 +861,6 @@ struct CrcFast {
 };
 
 // 16 payload bytes (memory order) -> piece value mod P; bytes outside [lo, hi) count as zero
-template <bool SIX>
 __device__ __forceinline__ uint32_t crc_piece(const uint8_t* tbl, uint4 v, uint32_t lo, uint32_t hi, bool n32)
 {
     uint32_t w[4] = { v.x, v.y, v.z, v.w };
@@ -843,15 +875,34 @@ __device__ __forceinline__ uint32_t crc_piece(const uint8_t* tbl, uint4 v, uint3
         w[3] &= (uint32_t)(m1 >> 32);
     }
     const uint32_t d3 = bswap(w[3]);
-    return __builtin_amdgcn_bitop3_b32(hmap<CF_M0 + 3, SIX>(tbl, bswap(w[0])), hmap<CF_M0 + 2, SIX>(tbl, bswap(w[1])),
-               hmap<CF_M0 + 1, SIX>(tbl, bswap(w[2])), 0x96)
-        ^ (n32 ? d3 : hmap<CF_M0, SIX>(tbl, d3));
+    return __builtin_amdgcn_bitop3_b32(cmap(tbl + (CF_M0 + 3) * CF_MAP, bswap(w[0])),
+               cmap(tbl + (CF_M0 + 2) * CF_MAP, bswap(w[1])), cmap(tbl + (CF_M0 + 1) * CF_MAP, bswap(w[2])), 0x96)
+        ^ (n32 ? d3 : cmap(tbl + CF_M0 * CF_MAP, d3));
 }
 
-// value * x^(128 (15 - lane % 16)) mod P from the transposed lane maps
+// crc_piece through the 8-bit maps (te: the LDS image's CE_EIGHT): the dwords in memory order
+__device__ __forceinline__ uint32_t crc_piece8(const uint8_t* te, uint4 v, uint32_t lo, uint32_t hi, bool n32)
+{
+    uint32_t w[4] = { v.x, v.y, v.z, v.w };
+    if (lo > 0 || hi < 16) {
+        auto ge = [](uint32_t b) { return b >= 8u ? 0ull : (~0ull << (8u * b)); };
+        const uint64_t m0 = ge(lo) & ~ge(hi);
+        const uint64_t m1 = ge(lo > 8u ? lo - 8u : 0u) & ~ge(hi > 8u ? hi - 8u : 0u);
+        w[0] &= (uint32_t)m0;
+        w[1] &= (uint32_t)(m0 >> 32);
+        w[2] &= (uint32_t)m1;
+        w[3] &= (uint32_t)(m1 >> 32);
+    }
+    return __builtin_amdgcn_bitop3_b32(cmap8(te + 3 * CF_EIGHT, w[0]), cmap8(te + 2 * CF_EIGHT, w[1]),
+               cmap8(te + CF_EIGHT, w[2]), 0x96)
+        ^ (n32 ? bswap(w[3]) : cmap8(te, w[3]));
+}
+
+// value * x^(128 (15 - lane % 16)) mod P from the transposed lane maps (at tbl + LOFF)
+template <int LOFF = CF_LANE_OFF>
 __device__ __forceinline__ uint32_t lane_cmap(const uint8_t* tbl, uint32_t v, uint32_t lane)
 {
-    const uint8_t* tb = tbl + CF_LANE_OFF + 4u * (lane & (CF_LANES - 1));
+    const uint8_t* tb = tbl + LOFF + 4u * (lane & (CF_LANES - 1));
     uint32_t e[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -863,10 +914,11 @@ __device__ __forceinline__ uint32_t lane_cmap(const uint8_t* tbl, uint32_t v, ui
 // Sum over the wave of value_l * x^(128 (63 - l)) -> wave-uniform: each lane's row factor, the row
 // XOR (DPP butterfly: every lane of row r ends with R_r), then R_0 x^6144 + R_1 x^4096 + R_2 x^2048 + R_3
 // by two tree levels (the maps x^(128 2^j), j = 4, 5)
-template <bool SIX>
+// LOFF: the lane maps; SOFF: the 6-bit tree maps, or < 0: the nibble maps CF_L + 4, CF_L + 5
+template <int LOFF, int SOFF>
 __device__ __forceinline__ uint32_t crc_lane_sum(const uint8_t* tbl, uint32_t acc, uint32_t lane)
 {
-    uint32_t v = lane_cmap(tbl, acc, lane);
+    uint32_t v = lane_cmap<LOFF>(tbl, acc, lane);
     v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
     v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
     v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false); // row_half_mirror
@@ -874,7 +926,10 @@ __device__ __forceinline__ uint32_t crc_lane_sum(const uint8_t* tbl, uint32_t ac
 #pragma unroll
     for (int j = 4; j < 6; ++j) {
         const uint32_t other = __shfl_down(v, 1 << j, 64);
-        v = (j == 4 ? hmap<CF_L + 4, SIX>(tbl, v) : hmap<CF_L + 5, SIX>(tbl, v)) ^ other;
+        if constexpr (SOFF >= 0)
+            v = cmap6(tbl + SOFF + (j - 4) * CF_MAP6, v) ^ other;
+        else
+            v = cmap(tbl + (CF_L + j) * CF_MAP, v) ^ other;
     }
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
@@ -892,9 +947,8 @@ __global__ __launch_bounds__(256) PPFS_CRC_ENC_ATTR void crc_fast_encode_kernel(
     uint8_t* __restrict__ raw, const uint8_t* __restrict__ skip, uint64_t nblocks_all, CrcFast a,
     const uint8_t* __restrict__ tables)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t tbl[CF_BYTES];
-    for (uint32_t p = threadIdx.x; p < CF_BYTES / 16; p += 256)
-        *(uint4*)(tbl + 16 * p) = *(const uint4*)(tables + 16 * p);
+    __shared__ __attribute__((aligned(16))) uint8_t tbl[CE::BYTES];
+    CE::stage(tbl, tables, CF_FENC);
     __syncthreads();
     const uint32_t lane = lane_id(), wave = wave_id();
     const HamFast ha { a.bs, a.ds, 0, a.data_bytes };
@@ -920,11 +974,11 @@ __global__ __launch_bounds__(256) PPFS_CRC_ENC_ATTR void crc_fast_encode_kernel(
             const int32_t lo = (int32_t)m - q16, hi = (int32_t)(m + a.ds) - q16;
             const uint32_t lo_c = lo < 0 ? 0u : (lo > 16 ? 16u : (uint32_t)lo);
             const uint32_t hi_c = hi < 0 ? 0u : (hi > 16 ? 16u : (uint32_t)hi);
-            const uint32_t pv = crc_piece<true>(tbl, cur.v[k], lo_c, hi_c > lo_c ? hi_c : lo_c, n32);
-            acc = k == 0 ? pv : (hmap<CF_K, true>(tbl, acc) ^ pv);
+            const uint32_t pv = crc_piece8(tbl + CE::EIGHT, cur.v[k], lo_c, hi_c > lo_c ? hi_c : lo_c, n32);
+            acc = k == 0 ? pv : (cmap8(tbl + CE::EIGHT + 4 * CF_EIGHT, acc) ^ pv);
         }
-        const uint32_t Vs = crc_lane_sum<true>(tbl, acc, lane);
-        const uint32_t V = cmap(tbl + (CF_FENC + m) * CF_MAP, Vs);
+        const uint32_t Vs = crc_lane_sum<CE::LANE, CE::SIX>(tbl, acc, lane);
+        const uint32_t V = cmap(tbl + CE::PLACE + m * CF_MAP, Vs);
         const uint32_t st = (V << 1) & a.mask;
         if (!(skip && PPFS_DBG_OK(skip + blk, 1, skip, nblocks_all) && skip[blk] == 5)) {
             // raw bytes [ds, ds + nbc): the n CRC bits MSB first (a partial last byte keeps its old
@@ -990,10 +1044,10 @@ __global__ __launch_bounds__(256) PPFS_CRC_ATTR void crc_fast_check_kernel(const
             const int32_t q16 = 16 * (64 * k + (int32_t)lane);
             const int32_t hi = (int32_t)ds - q16;
             const uint32_t hi_c = hi < 0 ? 0u : (hi > 16 ? 16u : (uint32_t)hi);
-            const uint32_t pv = crc_piece<false>(tbl, R[k], 0u, hi_c, n32);
-            acc = k == 0 ? pv : (hmap<CF_K, false>(tbl, acc) ^ pv);
+            const uint32_t pv = crc_piece(tbl, R[k], 0u, hi_c, n32);
+            acc = k == 0 ? pv : (cmap(tbl + CF_K * CF_MAP, acc) ^ pv);
         }
-        const uint32_t Vs = crc_lane_sum<false>(tbl, acc, lane);
+        const uint32_t Vs = crc_lane_sum<CF_LANE_OFF, -1>(tbl, acc, lane);
         const uint32_t V = cmap(tbl + CF_FCHK * CF_MAP, Vs);
         const uint32_t st = (V << 1) & a.mask;
         // stored field: n bits MSB first from byte ds (in the last raw piece, lane 63)
