@@ -1112,21 +1112,41 @@ template <typename K> static uint32_t bf_grid(K, uint64_t nb)
     return (uint32_t)(want < cap ? (want ? want : 1) : cap);
 }
 
-// Workgroups per CU of the streaming kernels, enforced by dynamic LDS (0 = as many as registers and
-// static LDS allow).  One 4 KiB block per wave is in flight per wave; round 4 (r4x, cfg4): the parity
-// encode at 6 waves per SIMD and the Hamming decode at 9 workgroups per CU ran 2.5 % / 1.5-2 %
-// slower than at 4 workgroups per CU (16 waves); the parity check, CRC encode (5) and the kernels
-// already at 4 (registers) showed no difference.
+// Workgroups per CU of the streaming kernels (PPFS_BF_*_WG), enforced by dynamic LDS (0 = as many as
+// registers and static LDS allow).  One 4 KiB block per wave is in flight per wave.  Round 4 (cfg4,
+// r4x / r4zc): parity encode 6 -> 4 -> 3 workgroups -2.5 % / -0.7 %, parity check at 3 -3.3 %
+// (at 4 and 2 no gain), Hamming decode 9 -> 4 -1.5-2 % (3: +7 %), Hamming encode (4 by registers)
+// and the CRC kernels: no gain at 3 or 4.
 static constexpr uint32_t bf_occ_lds(int wg, uint32_t static_lds)
 {
     return wg <= 0 ? 0u : (163840u / (uint32_t)(wg + 1) + 256u > static_lds ? 163840u / (uint32_t)(wg + 1) + 256u - static_lds : 0u);
 }
-constexpr int BF_PAR_ENC_WG = 4, BF_HAM_DEC_WG = 4;
-template <int NP> static constexpr uint32_t par_enc_dyn_lds() { return bf_occ_lds(BF_PAR_ENC_WG, 0); }
+#ifndef PPFS_BF_PAR_ENC_WG
+#define PPFS_BF_PAR_ENC_WG 3
+#endif
+#ifndef PPFS_BF_HAM_DEC_WG
+#define PPFS_BF_HAM_DEC_WG 4
+#endif
+#ifndef PPFS_BF_HAM_ENC_WG
+#define PPFS_BF_HAM_ENC_WG 0
+#endif
+#ifndef PPFS_BF_PAR_CHK_WG
+#define PPFS_BF_PAR_CHK_WG 3
+#endif
+#ifndef PPFS_BF_CRC_CHK_WG
+#define PPFS_BF_CRC_CHK_WG 0
+#endif
+template <int NP> static constexpr uint32_t par_enc_dyn_lds() { return bf_occ_lds(PPFS_BF_PAR_ENC_WG, 0); }
 template <int NP> static constexpr uint32_t ham_dec_dyn_lds()
 {
-    return bf_occ_lds(BF_HAM_DEC_WG, bf::WAVES * (NP * 1024 + 16)); // ham_fast_decode_kernel's lds[]
+    return bf_occ_lds(PPFS_BF_HAM_DEC_WG, bf::WAVES * (NP * 1024 + 16)); // ham_fast_decode_kernel's lds[]
 }
+template <int NP> static constexpr uint32_t ham_enc_dyn_lds()
+{
+    return bf_occ_lds(PPFS_BF_HAM_ENC_WG, bf::WAVES * ((NP + 1) * 1024 + 32)); // ham_fast_encode_kernel's lds[]
+}
+template <int NP> static constexpr uint32_t par_chk_dyn_lds() { return bf_occ_lds(PPFS_BF_PAR_CHK_WG, 0); }
+template <int NP> static constexpr uint32_t crc_chk_dyn_lds() { return bf_occ_lds(PPFS_BF_CRC_CHK_WG, bf::CF_SIX_OFF); }
 template <int NP> static constexpr uint32_t no_dyn_lds() { return 0; }
 
 extern "C" int ppfs_bitfast_supported(uint32_t bs) { return bs == 1024 || bs == 2048 || bs == 4096; }
@@ -1151,7 +1171,8 @@ extern "C" hipError_t ppfs_ham_fast_encode(const uint8_t* d, uint8_t* r, const u
     const bf::HamFast a { bs, ds, L, nb * (uint64_t)ds };
     if ((nb + 4ull * bf::BF_BPW - 1) / (4ull * bf::BF_BPW) > (1ull << 30))
         return hipErrorInvalidValue;
-    PPFS_NP_DISPATCH(bs, bf::ham_fast_encode_kernel, (nb + bf::BF_BPW - 1) / bf::BF_BPW, s, d, r, skip, nb, a)
+    PPFS_NP_DISPATCH_SH(bs, bf::ham_fast_encode_kernel, (nb + bf::BF_BPW - 1) / bf::BF_BPW, ham_enc_dyn_lds, s, d, r,
+        skip, nb, a)
     return hipGetLastError();
 }
 
@@ -1188,7 +1209,8 @@ extern "C" hipError_t ppfs_crc_fast_check(const uint8_t* r, uint8_t* d, uint8_t*
     const bf::CrcFast a { bs, ds, n, bs - ds, (uint32_t)mask, nb * (uint64_t)ds };
     if ((nb + 4ull * bf::CRC_BPW - 1) / (4ull * bf::CRC_BPW) > (1ull << 30))
         return hipErrorInvalidValue;
-    PPFS_NP_DISPATCH(bs, bf::crc_fast_check_kernel, (nb + bf::CRC_BPW - 1) / bf::CRC_BPW, s, r, d, st, nb, a, tab)
+    PPFS_NP_DISPATCH_SH(bs, bf::crc_fast_check_kernel, (nb + bf::CRC_BPW - 1) / bf::CRC_BPW, crc_chk_dyn_lds, s, r, d,
+        st, nb, a, tab)
     return hipGetLastError();
 }
 
@@ -1209,7 +1231,8 @@ extern "C" hipError_t ppfs_parity_fast_check(const uint8_t* r, uint8_t* d, uint8
     const bf::ParFast a { bs, nb * (uint64_t)(bs - 1) };
     if ((nb + 4ull * bf::BF_BPW - 1) / (4ull * bf::BF_BPW) > (1ull << 30))
         return hipErrorInvalidValue;
-    PPFS_NP_DISPATCH(bs, bf::parity_fast_check_kernel, (nb + bf::BF_BPW - 1) / bf::BF_BPW, s, r, d, st, nb, a)
+    PPFS_NP_DISPATCH_SH(bs, bf::parity_fast_check_kernel, (nb + bf::BF_BPW - 1) / bf::BF_BPW, par_chk_dyn_lds, s, r, d,
+        st, nb, a)
     return hipGetLastError();
 }
 
