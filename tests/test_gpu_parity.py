@@ -327,7 +327,7 @@ def test_crc_encode_check_match_oracle(oracle, imp, bs):
     assert (eng.raw_block_size, eng.data_size) == (bs, ds)
     nb = 257 if bs >= 1024 else 1001
     if (imp, bs) == (0x9960034c, 4096):
-        nb = 5003  # workgroups walk 32 blocks (CRC_BPW = 8): a ragged last workgroup
+        nb = 5003  # workgroups walk 32 / 16 blocks (CRC_BPW = 8 encode, 4 check): ragged last workgroups
     rng = rng_for("crc", imp, bs)
     data = rng.integers(0, 256, nb * ds, dtype=np.uint8)
     old = rng.integers(0, 256, nb * bs, dtype=np.uint8)  # tail bits must survive
