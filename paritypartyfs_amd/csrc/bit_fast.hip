@@ -1121,7 +1121,7 @@ template <typename K> static uint32_t bf_grid(K, uint64_t nb)
 // registers and static LDS allow).  One 4 KiB block per wave is in flight per wave.  Round 4 (cfg4,
 // r4x / r4zc): parity encode 6 -> 4 -> 3 workgroups -2.5 % / -0.7 %, parity check at 3 -3.3 %
 // (at 4 and 2 no gain), Hamming decode 9 -> 4 -1.5-2 % (3: +7 %), Hamming encode (4 by registers)
-// and the CRC kernels: no gain at 3 or 4.
+// and the CRC kernels: no gain at 4, slower at 3 (CRC encode +1 %, check +4 %, r4zh).
 static constexpr uint32_t bf_occ_lds(int wg, uint32_t static_lds)
 {
     return wg <= 0 ? 0u : (163840u / (uint32_t)(wg + 1) + 256u > static_lds ? 163840u / (uint32_t)(wg + 1) + 256u - static_lds : 0u);
@@ -1141,6 +1141,9 @@ static constexpr uint32_t bf_occ_lds(int wg, uint32_t static_lds)
 #ifndef PPFS_BF_CRC_CHK_WG
 #define PPFS_BF_CRC_CHK_WG 0
 #endif
+#ifndef PPFS_BF_CRC_ENC_WG
+#define PPFS_BF_CRC_ENC_WG 0
+#endif
 template <int NP> static constexpr uint32_t par_enc_dyn_lds() { return bf_occ_lds(PPFS_BF_PAR_ENC_WG, 0); }
 template <int NP> static constexpr uint32_t ham_dec_dyn_lds()
 {
@@ -1152,6 +1155,7 @@ template <int NP> static constexpr uint32_t ham_enc_dyn_lds()
 }
 template <int NP> static constexpr uint32_t par_chk_dyn_lds() { return bf_occ_lds(PPFS_BF_PAR_CHK_WG, 0); }
 template <int NP> static constexpr uint32_t crc_chk_dyn_lds() { return bf_occ_lds(PPFS_BF_CRC_CHK_WG, bf::CF_SIX_OFF); }
+template <int NP> static constexpr uint32_t crc_enc_dyn_lds() { return bf_occ_lds(PPFS_BF_CRC_ENC_WG, bf::CE::BYTES); }
 template <int NP> static constexpr uint32_t no_dyn_lds() { return 0; }
 
 extern "C" int ppfs_bitfast_supported(uint32_t bs) { return bs == 1024 || bs == 2048 || bs == 4096; }
@@ -1204,7 +1208,8 @@ extern "C" hipError_t ppfs_crc_fast_encode(const uint8_t* d, uint8_t* r, const u
     const bf::CrcFast a { bs, ds, n, bs - ds, (uint32_t)mask, nb * (uint64_t)ds };
     if ((nb + 4ull * bf::CRC_BPW - 1) / (4ull * bf::CRC_BPW) > (1ull << 30))
         return hipErrorInvalidValue;
-    PPFS_NP_DISPATCH(bs, bf::crc_fast_encode_kernel, (nb + bf::CRC_BPW - 1) / bf::CRC_BPW, s, d, r, skip, nb, a, tab)
+    PPFS_NP_DISPATCH_SH(bs, bf::crc_fast_encode_kernel, (nb + bf::CRC_BPW - 1) / bf::CRC_BPW, crc_enc_dyn_lds, s, d, r,
+        skip, nb, a, tab)
     return hipGetLastError();
 }
 
