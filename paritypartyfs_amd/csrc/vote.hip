@@ -115,7 +115,8 @@ extern "C" hipError_t ppfs_copy_launch(uint8_t* dst, const uint8_t* src, uint64_
 // corrupt every codeword of a step: torch's index_put_ of the same bytes reads 8-byte indices and
 // costs ~2x this kernel.  Each thread takes 4 consecutive blocks: one
 // 4-byte load of their positions and one of their values, then four byte stores.  (Round 4: store
-// instructions over 64 consecutive blocks instead, 16 KiB spans: 33 vs 30 us, r4zj.)
+// instructions over 64 consecutive blocks instead, 16 KiB spans: 33 vs 30 us, r4zj; 8 or 16 blocks
+// per thread with byte loads: 31.3 vs 30.0 us, r4zk.)
 #ifndef PPFS_INJECT_NT
 #define PPFS_INJECT_NT 0 // ablation builds: non-temporal byte stores
 #endif
