@@ -966,10 +966,6 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
         int pw = 0;
         while ((1u << (pw + 1)) <= p.block_size)
             pw++;
-        if (pw < 3) {
-            delete c;
-            return fail(PPFS_ECC_EINVAL, "Hamming block must be >= 8 bytes");
-        }
         c->raw = 1u << pw;
         c->data = c->raw - (uint32_t)((3 * pw + 1 + 7) / 8);
         // raw index of the last payload bit (HammingDataBitsIterator, hamming_block_device.cpp:180-198)
@@ -979,14 +975,11 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
                 idx++;
             c->ham_L = idx++;
         }
-        c->kname = ppfs_bitfast_supported(c->raw) ? "hamming-stream-wave" : "hamming-funnel";
+        c->kname = ppfs_bitfast_supported(c->raw) ? "hamming-stream-wave"
+                                                  : (c->raw < 8 ? "hamming-tiny" : "hamming-funnel");
         break;
     }
-    case PPFS_ECC_PARITY:
-        if (p.block_size < 2) {
-            delete c;
-            return fail(PPFS_ECC_EINVAL, "parity block must be >= 2 bytes");
-        }
+    case PPFS_ECC_PARITY: // block_size 1: no payload, the block's own parity (parity_block_device.cpp:9-15)
         c->raw = p.block_size;
         c->data = p.block_size - 1;
         c->kname = ppfs_bitfast_supported(c->raw) ? "parity-stream-wave" : "parity-popcount";
@@ -1189,7 +1182,7 @@ static int sync_check(int r, void* stream, const char* what)
 static int ppfs_ecc_encode_device_impl(ppfs_ecc_ctx* c, const uint8_t* d_data, uint8_t* d_raw, size_t nblocks,
     void* stream)
 {
-    if (!c || (nblocks && (!d_data || !d_raw)))
+    if (!c || (nblocks && ((!d_data && c->data) || !d_raw)))
         return fail(PPFS_ECC_EINVAL, "encode: null argument");
     if (nblocks == 0)
         return 0;
@@ -1215,7 +1208,7 @@ static int ppfs_ecc_encode_device_impl(ppfs_ecc_ctx* c, const uint8_t* d_data, u
                              c->crc_mask, c->d_tables, s),
             "crc encode");
     case PPFS_ECC_HAMMING:
-        if (!aligned16(d_raw))
+        if (c->raw >= 8 && !aligned16(d_raw))
             return fail(PPFS_ECC_EINVAL, "hamming: raw pointer must be 16-byte aligned");
         return check_hip(ppfs_ham_encode(d_data, d_raw, nullptr, nblocks, c->raw, c->data, c->ham_L, s),
             "hamming encode");
@@ -1266,7 +1259,7 @@ static int ppfs_ecc_decode_device_impl(ppfs_ecc_ctx* c, uint8_t* d_raw, uint8_t*
                              c->crc_mask, c->d_tables, s),
             "crc check");
     case PPFS_ECC_HAMMING:
-        if (!aligned16(d_raw))
+        if (c->raw >= 8 && !aligned16(d_raw))
             return fail(PPFS_ECC_EINVAL, "hamming: raw pointer must be 16-byte aligned");
         return check_hip(ppfs_ham_decode(d_raw, d_data, d_status, nblocks, write_back, c->raw, c->data, c->ham_L, s),
             "hamming decode");
@@ -1295,7 +1288,7 @@ static int ensure_scratch(ppfs_ecc_ctx* c, size_t bytes, hipStream_t s)
 static int ppfs_ecc_write_device_impl(ppfs_ecc_ctx* c, const uint8_t* d_data, uint8_t* d_raw, uint8_t* d_status,
     size_t nblocks, void* stream)
 {
-    if (!c || (nblocks && (!d_data || !d_raw)))
+    if (!c || (nblocks && ((!d_data && c->data) || !d_raw)))
         return fail(PPFS_ECC_EINVAL, "write: null argument");
     if (nblocks == 0)
         return 0;
@@ -1663,7 +1656,8 @@ static bool server_eligible(ppfs_ecc_ctx* c)
         const bool off = e && e[0] == '0';
         const bool rs = c->p.ecc_type == PPFS_ECC_REED_SOLOMON
             && (!c->rs_fast || c->rs_t2 <= 8 || c->rs_t2 == 10 || c->rs_t2 == 16 || c->rs_t2 == 32);
-        const bool bit = c->p.ecc_type == PPFS_ECC_CRC || c->p.ecc_type == PPFS_ECC_HAMMING
+        // Hamming blocks < 8 bytes run thread-per-block kernels the bit server does not carry
+        const bool bit = c->p.ecc_type == PPFS_ECC_CRC || (c->p.ecc_type == PPFS_ECC_HAMMING && c->raw >= 8)
             || c->p.ecc_type == PPFS_ECC_PARITY;
         c->srv_ok = (!off && (rs || bit)) ? 1 : 0;
     }

@@ -579,6 +579,111 @@ __global__ __launch_bounds__(256) void ham_decode_kernel(uint8_t* __restrict__ r
 }
 
 // ------------------------------------------------------------------------------------
+// Hamming blocks of 1, 2 and 4 bytes (block_size_power 0-2; hamming_block_device.cpp:11-19 takes
+// any power): one thread per block over a 32-bit register image of the block (MSB-first bit q at
+// register bit 31 - q), walking the reference's iterators literally.  Power 0 has no payload, and
+// its used bits are the parity positions 1, 2, 4 only (HammingUsedBitsIterator :209-219 starts in
+// its parity branch), not bit 0.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t tiny_load(const uint8_t* __restrict__ p, uint32_t n)
+{
+    uint32_t v = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        v |= (uint32_t)p[i] << (24 - 8 * i);
+    return v;
+}
+
+__device__ __forceinline__ void tiny_store(uint8_t* __restrict__ p, uint32_t n, uint32_t v)
+{
+    for (uint32_t i = 0; i < n; ++i)
+        p[i] = (uint8_t)(v >> (24 - 8 * i));
+}
+
+__device__ __forceinline__ uint32_t qbit(uint32_t q) { return 0x80000000u >> q; }
+
+// HammingDataBitsIterator::next (:188-198): the next integer that is neither 0 nor a power of two
+__device__ __forceinline__ uint32_t tiny_next_data(uint32_t& cur)
+{
+    while ((cur & (cur - 1)) == 0)
+        cur++;
+    return cur++;
+}
+
+__global__ __launch_bounds__(256) void ham_tiny_encode_kernel(const uint8_t* __restrict__ data,
+    uint8_t* __restrict__ raw, const uint8_t* __restrict__ skip, uint64_t nblocks, uint32_t bs, uint32_t ds)
+{
+    for (uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x; b < nblocks; b += (uint64_t)gridDim.x * 256) {
+        if (skip && skip[b] == 5)
+            continue;
+        const uint32_t D = ds ? tiny_load(data + b * ds, ds) : 0u;
+        uint32_t R = tiny_load(raw + b * bs, bs); // unused tail bits keep their contents
+        uint32_t parity = 1, pxor = 0, cur = 0;
+        for (uint32_t i = 0; i < 8 * ds; ++i) { // _encodeData :85-94
+            const uint32_t idx = tiny_next_data(cur);
+            const uint32_t v = (D >> (31 - i)) & 1u;
+            parity ^= v;
+            pxor ^= v ? idx : 0u;
+            R = v ? (R | qbit(idx)) : (R & ~qbit(idx));
+        }
+        for (uint32_t pi = 1; pi < 8 * bs; pi <<= 1) { // :96-105
+            const bool pv = (pxor & pi) != 0;
+            parity ^= pv ? 1u : 0u;
+            R = pv ? (R | qbit(pi)) : (R & ~qbit(pi));
+        }
+        R = parity ? (R & ~qbit(0)) : (R | qbit(0)); // bit 0 = !parity (:107-108)
+        tiny_store(raw + b * bs, bs, R);
+    }
+}
+
+__global__ __launch_bounds__(256) void ham_tiny_decode_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
+    uint8_t* __restrict__ status, uint64_t nblocks, int write_back, uint32_t bs, uint32_t ds)
+{
+    for (uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x; b < nblocks; b += (uint64_t)gridDim.x * 256) {
+        uint32_t R = tiny_load(raw + b * bs, bs);
+        // HammingUsedBitsIterator (:209-230) over the block, _readAndFixBlock :30-39
+        const uint32_t lim = 8 * ds, bits = 8 * bs;
+        uint32_t cur = 0, next_par = 1, ret = 0, epos = 0, parity = 1;
+        for (;;) {
+            uint32_t idx;
+            if (ret >= lim && next_par >= bits)
+                break;
+            if (ret >= lim) {
+                idx = next_par;
+                next_par <<= 1;
+            } else {
+                const bool pow2 = cur && (cur & (cur - 1)) == 0;
+                if (pow2)
+                    next_par = cur << 1;
+                if (cur && !pow2)
+                    ret++;
+                idx = cur++;
+            }
+            if (R & qbit(idx)) {
+                epos ^= idx;
+                parity ^= 1u;
+            }
+        }
+        uint32_t st = 0;
+        if (!parity) { // :41-57: flip, write back only that byte
+            R ^= qbit(epos);
+            st = 1;
+            if (write_back)
+                raw[b * bs + epos / 8] = (uint8_t)(R >> (24 - 8 * (epos / 8)));
+        } else if (epos != 0) {
+            st = 5; // :58-61
+        }
+        if (status)
+            status[b] = (uint8_t)st;
+        if (data && ds && st != 5) { // _extractData :67-74
+            uint32_t D = 0, c2 = 0;
+            for (uint32_t i = 0; i < 8 * ds; ++i)
+                D |= (R & qbit(tiny_next_data(c2))) ? qbit(i) : 0u;
+            tiny_store(data + b * ds, ds, D);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // Parity (even parity over the whole raw block; the LSB of the last byte is the fix bit)
 // ------------------------------------------------------------------------------------
 // per-wave body of parity_encode_kernel (also run by bit_server_kernel): blocks first, first + stride, ...
@@ -755,6 +860,13 @@ static uint32_t bk_grid(uint64_t nb)
     return (uint32_t)(g > 8192 ? 8192 : (g ? g : 1));
 }
 
+// thread-per-block kernels (Hamming blocks < 8 bytes)
+static uint32_t tiny_grid(uint64_t nb)
+{
+    uint64_t g = (nb + 255) / 256;
+    return (uint32_t)(g > 8192 ? 8192 : (g ? g : 1));
+}
+
 extern "C" int ppfs_crc_tables_bytes(void) { return CRC_TBL_BYTES; }
 
 extern "C" hipError_t ppfs_crc_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs,
@@ -782,6 +894,10 @@ extern "C" hipError_t ppfs_ham_encode(const uint8_t* d, uint8_t* r, const uint8_
 {
     if (ppfs_bitfast_supported(bs))
         return ppfs_ham_fast_encode(d, r, skip, nb, bs, ds, L, s);
+    if (bs < 8) {
+        hipLaunchKernelGGL(ham_tiny_encode_kernel, dim3(tiny_grid(nb)), dim3(256), 0, s, d, r, skip, nb, bs, ds);
+        return hipGetLastError();
+    }
     HamArgs a { bs, ds, 8 * bs, L };
     hipLaunchKernelGGL(ham_encode_kernel, dim3(bk_grid(nb)), dim3(256), 0, s, d, r, skip, nb, a);
     return hipGetLastError();
@@ -792,6 +908,10 @@ extern "C" hipError_t ppfs_ham_decode(uint8_t* r, uint8_t* d, uint8_t* st, uint6
 {
     if (ppfs_bitfast_supported(bs))
         return ppfs_ham_fast_decode(r, d, st, nb, wb, bs, ds, L, s);
+    if (bs < 8) {
+        hipLaunchKernelGGL(ham_tiny_decode_kernel, dim3(tiny_grid(nb)), dim3(256), 0, s, r, d, st, nb, wb, bs, ds);
+        return hipGetLastError();
+    }
     HamArgs a { bs, ds, 8 * bs, L };
     hipLaunchKernelGGL(ham_decode_kernel, dim3(bk_grid(nb)), dim3(256), 0, s, r, d, st, nb, wb, a);
     return hipGetLastError();

@@ -401,7 +401,7 @@ template <int T2> __device__ __forceinline__ uint4 dec_piece(const uint8_t* lds,
     const uint32_t S = buf + PAD + 255u * b + T2 + off;
     const uint32_t sh = (S & 3u) * 8u;
     uint32_t d[7];
-lds_window(d, lds, S);
+    lds_window(d, lds, S);
     uint32_t X[6];
 #pragma unroll
     for (int m = 0; m < 6; ++m)

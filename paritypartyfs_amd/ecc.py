@@ -108,8 +108,13 @@ class EccEngine:
         _need("status", status, n, kind)
         _need("spill", spill, n * self.spill_bytes_per_block(), kind)
 
+    def _nblocks(self, data, raw) -> int:
+        """Blocks a call covers when nblocks is not given: from the payloads, or from the raw
+        blocks for codecs without payload bytes (Hamming power 0, 1-byte parity blocks)."""
+        return _size(data) // self.data_size if self.data_size else _size(raw) // self.raw_block_size
+
     def encode(self, data, raw, nblocks: Optional[int] = None, stream=None) -> None:
-        n = nblocks if nblocks is not None else data.numel() // self.data_size
+        n = nblocks if nblocks is not None else self._nblocks(data, raw)
         self._check("device", n, data, raw)
         check(lib().ppfs_ecc_encode_device(self._h, _ptr(data), _ptr(raw), n, _stream_handle(stream)))
 
@@ -121,14 +126,14 @@ class EccEngine:
                                            _ptr(spill), _stream_handle(stream)))
 
     def write(self, data, raw, status=None, nblocks: Optional[int] = None, stream=None) -> None:
-        n = nblocks if nblocks is not None else data.numel() // self.data_size
+        n = nblocks if nblocks is not None else self._nblocks(data, raw)
         self._check("device", n, data, raw, status)
         check(lib().ppfs_ecc_write_device(self._h, _ptr(data), _ptr(raw), _ptr(status), n,
                                           _stream_handle(stream)))
 
     # ---------------- host-memory batches (numpy uint8) ----------------
     def encode_host(self, data: np.ndarray, raw: np.ndarray) -> None:
-        n = _host_blocks(data, self.data_size, "data")
+        n = _host_blocks(data, self.data_size, "data") if self.data_size else _host_blocks(raw, self.raw_block_size, "raw")
         self._check("host", n, data, raw)
         check(lib().ppfs_ecc_encode_host(self._h, _ptr(data), _ptr(raw), n))
 
@@ -140,7 +145,7 @@ class EccEngine:
                                          _ptr(spill)))
 
     def write_host(self, data: np.ndarray, raw: np.ndarray, status: Optional[np.ndarray] = None) -> None:
-        n = _host_blocks(data, self.data_size, "data")
+        n = _host_blocks(data, self.data_size, "data") if self.data_size else _host_blocks(raw, self.raw_block_size, "raw")
         self._check("host", n, data, raw, status)
         check(lib().ppfs_ecc_write_host(self._h, _ptr(data), _ptr(raw), _ptr(status), n))
 

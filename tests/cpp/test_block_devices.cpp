@@ -372,7 +372,10 @@ template <class D> static void differential(const Cfg& c, uint64_t seed, int nop
     std::vector<int32_t> olog(1 << 16);
     void* od = oracle_dev_create(c.type, c.bs, c.t, c.poly, odisk.data(), odisk.size(), olog.data(), olog.size());
     std::mt19937_64 rng(seed);
-    auto rnd = [&](uint64_t n) { return (uint64_t)(rng() % n); };
+    auto rnd = [&](uint64_t n) { // n = 0 (no payload: Hamming power 0, 1-byte parity) gives 0
+        const uint64_t v = rng();
+        return n ? v % n : (uint64_t)0;
+    };
     auto same_disk = [&]() { return std::memcmp(disk.image(), odisk.data(), odisk.size()) == 0; };
     auto same_log = [&]() {
         if (lg->events.size() != oracle_dev_log_len(od))
@@ -500,9 +503,14 @@ static const Cfg kCfgs[] = {
     { "crc512_0xc1acf", PPFS_ECC_CRC, 512, 0, (0xc1acfull << 1) + 1 },
     { "crc100_deg3", PPFS_ECC_CRC, 100, 0, 0xb },
     { "crc4096_deg32", PPFS_ECC_CRC, 4096, 0, (0x9960034cull << 1) + 1 },
+    { "hamming1_pow0", PPFS_ECC_HAMMING, 1, 0, 0 },
+    { "hamming2_pow1", PPFS_ECC_HAMMING, 2, 0, 0 },
+    { "hamming4_pow2", PPFS_ECC_HAMMING, 4, 0, 0 },
+    { "hamming8", PPFS_ECC_HAMMING, 8, 0, 0 },
     { "hamming16", PPFS_ECC_HAMMING, 16, 0, 0 },
     { "hamming512", PPFS_ECC_HAMMING, 512, 0, 0 },
     { "hamming4096", PPFS_ECC_HAMMING, 4096, 0, 0 },
+    { "parity1", PPFS_ECC_PARITY, 1, 0, 0 },
     { "parity256", PPFS_ECC_PARITY, 256, 0, 0 },
     { "parity4096", PPFS_ECC_PARITY, 4096, 0, 0 },
     { "raw512", PPFS_ECC_NONE, 512, 0, 0 },

@@ -180,7 +180,7 @@ class Oracle:
     def ham_encode(self, bs, data, raw_old=None):
         ds = self.ham_data_size(bs)
         data = np.ascontiguousarray(data, np.uint8)
-        nb = data.size // ds
+        nb = data.size // ds if ds else np.asarray(raw_old).size // bs  # power 0: no payload
         raw = np.zeros(nb * bs, np.uint8) if raw_old is None else np.array(raw_old, np.uint8, copy=True)
         self.L.oracle_hamming_encode(bs, _p(data), _p(raw), nb)
         return raw
@@ -199,7 +199,7 @@ class Oracle:
     # ---------------- Parity ----------------
     def parity_encode(self, bs, data, raw_old=None):
         data = np.ascontiguousarray(data, np.uint8)
-        nb = data.size // (bs - 1)
+        nb = data.size // (bs - 1) if bs > 1 else np.asarray(raw_old).size  # 1-byte blocks: no payload
         raw = np.zeros(nb * bs, np.uint8) if raw_old is None else np.array(raw_old, np.uint8, copy=True)
         self.L.oracle_parity_encode(bs, _p(data), _p(raw), nb)
         return raw

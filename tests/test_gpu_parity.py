@@ -362,12 +362,15 @@ def test_crc_encode_check_match_oracle(oracle, imp, bs):
 # ------------------------------------------------------------------------------------
 # Hamming
 # ------------------------------------------------------------------------------------
-@pytest.mark.parametrize("bs,nb", [(8, 1000), (16, 1000), (32, 1000), (64, 1000), (128, 1000),
+@pytest.mark.parametrize("bs,nb", [(1, 999), (2, 1000), (4, 1000), (8, 1000), (16, 1000), (32, 1000), (64, 1000), (128, 1000),
                                    (256, 1000), (512, 1000), (1024, 1000),
                                    (2048, 700), (4096, 300), (4096, 5003)])
 def test_hamming_matches_oracle(oracle, bs, nb):
     """bs >= 1024 runs the streaming kernels of bit_fast.hip; 5003 blocks of 4 KiB make every
-    persistent wave walk several blocks (next-block prefetch) and end on a ragged last block."""
+    persistent wave walk several blocks (next-block prefetch) and end on a ragged last block.
+    bs 1, 2, 4 (block_size_power 0-2, hamming_block_device.cpp:11-19) run the thread-per-block
+    kernels: 0 / 8 / 24 payload bits, tail bits 13-15 / 30-31 kept from the old block, and at
+    power 0 used bits {1, 2, 4} only."""
     eng = EccEngine(ECC_HAMMING, bs)
     ds = oracle.ham_data_size(bs)
     assert (eng.raw_block_size, eng.data_size) == (bs, ds)
@@ -400,7 +403,7 @@ def test_hamming_matches_oracle(oracle, bs, nb):
 # ------------------------------------------------------------------------------------
 # Parity and raw
 # ------------------------------------------------------------------------------------
-@pytest.mark.parametrize("bs,nb", [(2, 999), (16, 999), (255, 999), (256, 999), (1024, 999), (2048, 999),
+@pytest.mark.parametrize("bs,nb", [(1, 999), (2, 999), (16, 999), (255, 999), (256, 999), (1024, 999), (2048, 999),
                                    (4096, 999), (4096, 5003)])
 def test_parity_matches_oracle(oracle, bs, nb):
     eng = EccEngine(ECC_PARITY, bs)

@@ -64,3 +64,85 @@ def test_hot_kernels_use_no_scratch(tmp_path):
         for n, d in k.items():
             if frag in n:
                 assert d.get("private_segment_fixed_size", 0) <= limit and d.get("vgpr_spill_count", 0) == 0, (n, d)
+
+
+# ------------------------------------------------------------------------------------------------
+# Inline-asm hazard guard (round 4's r4b failure): a multi-instruction asm block that issues several
+# memory reads from input address registers must mark its outputs early-clobber ("=&v").  Without
+# it the register allocator may give a result the register of an address that a LATER read of the
+# same block still needs -- the first read's data then overwrites the address before the next read
+# issues (the t = 3 encode mismatched the oracle at 147,493 blocks on fc6e8df).
+# ------------------------------------------------------------------------------------------------
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "paritypartyfs_amd", "csrc")
+READ_INSN = re.compile(r"\b(ds_read\w*|ds_load\w*|global_load\w*|buffer_load\w*|flat_load\w*|scratch_load\w*)")
+
+
+def _asm_blocks(src):
+    """(start line, template text, output constraints) of every asm statement in a source text."""
+    out = []
+    for m in re.finditer(r"\basm\s+(?:volatile\s*)?\(", src):
+        i, depth, in_str, parts, cur = m.end(), 1, False, [], []
+        while i < len(src) and depth:
+            ch = src[i]
+            if in_str:
+                cur.append(ch)
+                if ch == "\\":
+                    cur.append(src[i + 1])
+                    i += 1
+                elif ch == '"':
+                    in_str = False
+            elif ch == '"':
+                in_str = True
+                cur.append(ch)
+            elif ch == "(":
+                depth += 1
+                cur.append(ch)
+            elif ch == ")":
+                depth -= 1
+                if depth:
+                    cur.append(ch)
+            elif ch == ":" and depth == 1:
+                parts.append("".join(cur))
+                cur = []
+            else:
+                cur.append(ch)
+            i += 1
+        parts.append("".join(cur))
+        template = "".join(re.findall(r'"((?:[^"\\]|\\.)*)"', parts[0]))
+        template = template.replace("\\n", "\n").replace("\\t", "\t")  # instruction separators
+        outputs = re.findall(r'"(=[^"]*|\+[^"]*)"', parts[1]) if len(parts) > 1 else []
+        out.append((src.count("\n", 0, m.start()) + 1, template, outputs))
+    return out
+
+
+def asm_clobber_violations(src):
+    bad = []
+    for line, template, outputs in _asm_blocks(src):
+        if len(READ_INSN.findall(template)) < 2:
+            continue
+        late = [o for o in outputs if o.startswith("=") and not o.startswith("=&")]
+        if late:
+            bad.append((line, late))
+    return bad
+
+
+def _sources():
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".hip", ".cpp")))
+
+
+def test_multi_read_asm_blocks_use_early_clobber_outputs():
+    seen = 0
+    for path in _sources():
+        src = open(path).read()
+        seen += sum(len(READ_INSN.findall(t)) >= 2 for _, t, _ in _asm_blocks(src))
+        assert not asm_clobber_violations(src), (os.path.basename(path), asm_clobber_violations(src))
+    assert seen >= 2, "the multi-read asm blocks (rs_wg_tk.hpp win5x1 / win5x3) were not found"
+
+
+def test_clobber_guard_catches_the_r4b_regression():
+    """Positive control: win5x3 with its outputs reverted to plain "=v" is flagged."""
+    src = open(os.path.join(CSRC, "rs_wg_tk.hpp")).read()
+    assert not asm_clobber_violations(src)
+    start = src.index("void win5x3(")
+    broken = src[:start] + src[start:].replace('"=&v"', '"=v"', 9)
+    assert asm_clobber_violations(broken)

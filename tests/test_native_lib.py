@@ -56,7 +56,8 @@ def test_param_validation_without_gpu(lib):
     from paritypartyfs_amd._native import EccParams
     h = ctypes.c_void_p()
     bad = [EccParams(4, 0, 3, 0, 0), EccParams(4, 8192, 3, 0, 0), EccParams(9, 512, 3, 0, 0),
-           EccParams(1, 512, 0, 0, 1), EccParams(2, 4, 0, 0, 0), EccParams(3, 1, 0, 0, 0)]
+           EccParams(1, 512, 0, 0, 1), EccParams(1, 4, 0, 0, 0x1EDC6F41 | (1 << 32)),
+           EccParams(1, 1, 0, 0, 0x107)]  # CRC degree 32 on 4 B / degree 8 on 1 B: no payload byte
     for p in bad:
         assert lib.ppfs_ecc_create(ctypes.byref(p), 0, ctypes.byref(h)) == -22
         assert lib.ppfs_ecc_last_error()

@@ -259,8 +259,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
         dim3(rs_tile_grid(nb, PPFS_WG_RP)), dim3(256), 0, s, d, r, nb, tab);
 #elif PPFS_WG_DYN & 1
     hipLaunchKernelGGL((wg::rs_wg_encode_dyn_kernel<PPFS_T2, ENC_NBUF, ENC_WPC, PPFS_ENC_MODE, PPFS_ENC_NTST, (PPFS_WG_DYN & 4) != 0>),
-        dim3(rs_tile_grid(nb, ENC_WPC)), dim3(320), 0, s, d, r, nb, tab,
-        (uint32_t*)(const_cast<uint8_t*>(tab) + RsWgLayout<PPFS_T2>::OFF_CTR));
+        dim3(rs_tile_grid(nb, ENC_WPC)), dim3(320), 0, s, d, r, nb, tab, ctr); // the caller's counter set
 #elif PPFS_WG_ENC_W8
     hipLaunchKernelGGL((wg::rs_wg_encode8_kernel<PPFS_T2, (PPFS_T2 > 6 ? 3 : PPFS_WG_ENC_W8), 2, PPFS_ENC_NTST>),
         dim3(rs_tile_grid(nb, 2)), dim3(512), 0, s, d, r, nb, tab);

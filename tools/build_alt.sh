@@ -6,7 +6,14 @@
 #       tools/ablations/)
 #   tools/build_alt.sh --product <name> '<extra hipcc flags>'  the shipped dispatch with extra flags
 #       (e.g. the bounds-checked build: --product debug -DPPFS_ECC_DEBUG=1)
+# _lib/alt/ stays on this machine (.gpurunignore); a leading --lease puts the library into
+# _lib/lease/ instead, which travels to the GPU box (A/B baselines, trace builds a lease loads).
 set -e
+DIR=alt
+if [ "$1" = "--lease" ]; then
+    DIR=lease
+    shift
+fi
 INST=../../tools/ablations/rs_fast_inst_ablate.hip
 INC="-I. -I../../tools/ablations"
 if [ "$1" = "--product" ]; then
@@ -16,5 +23,5 @@ if [ "$1" = "--product" ]; then
 fi
 N=$1; shift
 cd "$(dirname "$0")/../paritypartyfs_amd/csrc"
-make -j8 OUT=../_lib/alt/libppfs_ecc_$N.so OBJDIR=../_lib/alt/obj_$N RS_INST=$INST EXTRA="$INC $*" >/dev/null
-echo "built _lib/alt/libppfs_ecc_$N.so ($INST $*)"
+make -j8 OUT=../_lib/$DIR/libppfs_ecc_$N.so OBJDIR=../_lib/alt/obj_$N RS_INST=$INST EXTRA="$INC $*" >/dev/null
+echo "built _lib/$DIR/libppfs_ecc_$N.so ($INST $*)"

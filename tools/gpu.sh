@@ -72,7 +72,7 @@ for step in "$@"; do
             done
         done ;;
     tktrace)
-        T=$PWD/paritypartyfs_amd/_lib/alt/libppfs_ecc_trace.so
+        T=$PWD/paritypartyfs_amd/_lib/lease/libppfs_ecc_trace.so
         PPFS_ECC_LIB=$T timeout -k 10 120 python tools/tk_trace.py 2> /dev/null > ${O}_tktrace.jsonl || { tail ${O}_tktrace.jsonl; exit 1; }
         cat ${O}_tktrace.jsonl ;;
     lds | lds=*)
