@@ -315,6 +315,85 @@ def load_traffic(kernel, nblocks, path=os.path.join(ROOT, "profiles", "pmc_lates
     return round(kp["hbm_bytes_per_launch"]), f"rocprofv3 PMC {pmc.get('tag')} (same library build)"
 
 
+def host_link_ceilings(dev, nb, k, n, reps=3):
+    """The host link measured on this box: page-locked hipMemcpyAsync H2D only, D2H
+    only, and both at once on two streams, over the bytes the host entry points move -- encode: k B in,
+    n B out per block; 1-error decode with write-back: n B in, k + n B out (payload + every changed
+    codeword).  Best of `reps`; rates in GB/s of bytes moved, ceilings in algorithmic GiB/s (k + n B
+    per block, the unit of the *_host rates)."""
+    import torch
+
+    def best(fn):
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return min(ts)
+
+    big = (k + n) * nb
+    h_in = torch.empty(big, dtype=torch.uint8, pin_memory=True)
+    h_out = torch.empty(big, dtype=torch.uint8, pin_memory=True)
+    d_in = torch.empty(big, dtype=torch.uint8, device=dev)
+    d_out = torch.empty(big, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def h2d(nbytes):
+        with torch.cuda.stream(s1):
+            d_in[:nbytes].copy_(h_in[:nbytes], non_blocking=True)
+
+    def d2h(nbytes):
+        with torch.cuda.stream(s2):
+            h_out[:nbytes].copy_(d_out[:nbytes], non_blocking=True)
+
+    def both(bin_, bout):
+        h2d(bin_)
+        d2h(bout)
+
+    t_h2d = best(lambda: h2d(k * nb))
+    t_d2h = best(lambda: d2h(n * nb))
+    t_enc = best(lambda: both(k * nb, n * nb))
+    t_dec = best(lambda: both(n * nb, (k + n) * nb))
+    del h_in, h_out, d_in, d_out
+    alg = (k + n) * nb
+    return {
+        "h2d_GBps": round(k * nb / t_h2d / 1e9, 2),
+        "d2h_GBps": round(n * nb / t_d2h / 1e9, 2),
+        "bidir_encode_bytes_GBps": round((k + n) * nb / t_enc / 1e9, 2),
+        "bidir_decode_bytes_GBps": round((k + 2 * n) * nb / t_dec / 1e9, 2),
+        "encode_ceiling_GiBps": round(alg / t_enc / GIB, 3),
+        "decode_1err_ceiling_GiBps": round(alg / t_dec / GIB, 3),
+        "method": "torch page-locked tensors, copy_(non_blocking) = hipMemcpyAsync, H2D and D2H on two streams, "
+                  f"best of {reps}",
+    }
+
+
+def rank_fields(mine, alg_step_bytes, world, elapsed_s, steps):
+    """SURVEY 8(e) fields of an N-rank line, made on every rank (all_gather over the default group;
+    the ranks reach this point together, after the timed region):
+      per_rank_kernels_ms: every rank's in-step kernel means (min / max over ranks, and each rank's),
+        so one SCALE run shows whether a slow GPU or the launch path set the max-over-ranks time;
+      aggregate_frac: sum over ranks of the algorithmic bytes of the timed steps / the timed region
+        (max over ranks) / (N x the per-GPU HBM peak) -- the job's fraction of N GPUs' bandwidth."""
+    import torch.distributed as dist
+
+    gathered = [mine]
+    if dist.is_available() and dist.is_initialized():
+        gathered = [None] * dist.get_world_size()
+        dist.all_gather_object(gathered, mine)
+    gathered = sorted(gathered, key=lambda g: g["rank"])
+    per = {}
+    for key in ("encode", "decode"):
+        vals = [g[key] for g in gathered]
+        per[key] = {"min": round(min(vals), 5), "max": round(max(vals), 5), "by_rank": [round(v, 5) for v in vals]}
+    total = alg_step_bytes * world * steps
+    agg = total / elapsed_s / 1e9 / (world * HBM_PEAK_GBS)
+    return per, {"aggregate_frac": round(agg, 4), "aggregate_peak_GBps": world * HBM_PEAK_GBS,
+                 "aggregate_bytes": total, "ranks_reporting": len(gathered)}
+
+
 # ------------------------------------------------------------------------------------------
 # dry run: the launch / timing path with a CPU stand-in for the engine (tests only)
 # ------------------------------------------------------------------------------------------
@@ -325,24 +404,34 @@ def dry_run(args, world, rank):
         dist.init_process_group("gloo")
     buf = np.zeros(1 << 16, np.uint8)
 
-    def step():  # stand-in work: no ECC, no GPU
+    part_s = {"encode": [], "decode": []}
+
+    def step():  # stand-in work: no ECC, no GPU ("encode" = the XOR, "decode" = the sleep)
+        t0 = time.perf_counter()
         np.bitwise_xor(buf, 1, out=buf)
+        t1 = time.perf_counter()
         time.sleep(0.001 * (rank + 1))
+        part_s["encode"].append(t1 - t0)
+        part_s["decode"].append(time.perf_counter() - t1)
 
     for _ in range(args.warmup):
         step()
     elapsed = timed_steps(step, args.steps, world, lambda: None, None)
-    mine = {"rank": rank, "block_size": args.block_size, "t": args.t, "blocks": args.blocks}
+    mine = {"rank": rank, "block_size": args.block_size, "t": args.t, "blocks": args.blocks,
+            "encode": float(np.mean(part_s["encode"])) * 1e3, "decode": float(np.mean(part_s["decode"])) * 1e3}
     gathered = [mine]
     if dist.is_initialized():
         gathered = [None] * dist.get_world_size()
         dist.all_gather_object(gathered, mine)
+    # the N-rank fields of the real line, over the stand-in's times and the RS(255,249) byte count
+    per_rank, agg = rank_fields(mine, 2 * 504 * args.blocks, world, elapsed, args.steps)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "dry_run": True, "value": None, "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
                           "scaling": "weak", "note": "CPU stand-in for the engine: launcher / timing test only",
+                          "per_rank_kernels_ms": per_rank, **agg,
                           # what every rank parsed: the driver's argv must reach the ranks unchanged
-                          "rank_args": gathered}),
+                          "rank_args": [{k: g[k] for k in ("rank", "block_size", "t", "blocks")} for g in gathered]}),
               flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
@@ -533,6 +622,9 @@ def main(argv=None):
     hk.close()
     enc_avg, dec_avg, inj_avg = float(np.mean(enc_ms)), float(np.mean(dec_ms)), float(np.mean(inj_ms))
     enc_ev_avg, dec_ev_avg = float(np.mean(enc_ev)), float(np.mean(dec_ev))
+    # every rank's kernel means (min / max over ranks) and the job's fraction of N x peak
+    per_rank, agg = rank_fields({"rank": rank, "encode": enc_avg, "decode": dec_avg}, 2 * (k + n) * nb, world,
+                                elapsed, args.steps)
     # device time of the timed region's launch form (same K steps again, two events around them)
     he.record(4 * K, stream)
     run_steps(K)
@@ -680,8 +772,17 @@ def main(argv=None):
             ok = bool(np.array_equal(hout, hd)) and int(hst.min()) == 1
             host_incl[mode] = {"encode_GiBps": round(alg_launch / (t2 - t1) / GIB, 3),
                                "decode_1err_GiBps": round(alg_launch / (t4 - t3) / GIB, 3), "verified": ok}
+        host_incl["link"] = host_link_ceilings(dev, nb, k, n)
+        lk = host_incl["link"]
+        for mode in ("pageable", "pinned"):
+            # each call's copies alone, both directions at once over page-locked memory: the ceiling
+            # the host path can reach (decode with write-back also returns every changed codeword)
+            host_incl[mode]["encode_frac_of_link"] = round(host_incl[mode]["encode_GiBps"] / lk["encode_ceiling_GiBps"], 3)
+            host_incl[mode]["decode_1err_frac_of_link"] = round(host_incl[mode]["decode_1err_GiBps"]
+                                                                / lk["decode_1err_ceiling_GiBps"], 3)
         host_incl["note"] = ("ppfs_ecc_{encode,decode}_host over the same 2^20 blocks: H2D + kernel + D2H wall "
-                             "time, algorithmic bytes; never `value`")
+                             "time, algorithmic bytes; never `value`; *_frac_of_link = rate / the same call's "
+                             "copies alone over page-locked memory (link)")
 
     # (5) the other BASELINE configs (driver-visible per-config kernel rates): configs[3] Hamming and
     # CRC 0x9960034c at block_size 4096 and configs[4] RS(255,223), 2^20 blocks each, back-to-back
@@ -752,6 +853,10 @@ def main(argv=None):
             "configs": cfg_lines,
             "kernels_ms": {"encode": round(enc_avg, 5), "inject": round(inj_avg, 5), "decode": round(dec_avg, 5)},
             "in_step_frac": {"encode": frac(enc_avg), "decode": frac(dec_avg)},
+            # the timed region's algorithmic bytes over all ranks / (N x 8 TB/s), and the
+            # in-step kernel means of every rank (rank 0's are kernels_ms)
+            **agg,
+            "per_rank_kernels_ms": per_rank,
             "kernels_ms_stream_events": {"encode": round(enc_ev_avg, 5), "decode": round(dec_ev_avg, 5),
                                          "in_step_frac_encode": frac(enc_ev_avg), "in_step_frac_decode": frac(dec_ev_avg)},
             "standalone": {

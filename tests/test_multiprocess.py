@@ -64,6 +64,15 @@ def test_bench_gpus2_launches_two_ranks():
     line = lines[0]
     assert line["n_gpus"] == 2 and line["dry_run"] and line["steps"] == 5
     assert line["ms_per_step"] >= 2.0 * 0.95  # rank 1's stand-in sleeps 2 ms per step
+    # SURVEY 8(e) fields of the N-rank line: every rank's kernel times, the job's fraction of N x peak
+    per = line["per_rank_kernels_ms"]
+    assert line["ranks_reporting"] == 2 and len(per["decode"]["by_rank"]) == 2
+    assert per["decode"]["min"] <= per["decode"]["max"] and per["decode"]["max"] >= 2.0 * 0.95
+    assert per["decode"]["by_rank"][1] > per["decode"]["by_rank"][0]  # rank 1 sleeps twice as long
+    assert line["aggregate_peak_GBps"] == 2 * 8000.0
+    exp = line["aggregate_bytes"] / (line["ms_per_step"] * 1e-3 * 5) / 1e9 / (2 * 8000.0)
+    assert line["aggregate_bytes"] == 2 * 504 * (1 << 20) * 2 * 5
+    assert abs(line["aggregate_frac"] - exp) <= 1e-3 * exp + 1e-4
 
 
 def test_bench_gpus2_argv_reaches_every_rank():
