@@ -51,9 +51,7 @@ hipError_t ppfs_rs_generic_encode(const uint8_t* d, uint8_t* r, uint64_t nb, int
 hipError_t ppfs_rs_generic_decode(uint8_t* r, uint8_t* d, uint8_t* st, uint8_t* spill, uint64_t nb, int n, int t2,
     int wb, const uint8_t* tab, hipStream_t s);
 int ppfs_crc_tables_bytes(void);
-int ppfs_crc_fast_tables_bytes(void);
-int ppfs_crc_fast_lane_maps(void);
-int ppfs_crc_fast_six_maps(void);
+int ppfs_crc_fast_layout(int32_t* v, int n);
 int ppfs_crc_fast_supported(uint32_t bs, uint32_t n);
 int ppfs_bitfast_supported(uint32_t bs);
 hipError_t ppfs_crc_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs, uint32_t ds,
@@ -465,14 +463,25 @@ std::vector<uint8_t> build_crc_tables(uint64_t P, int n, uint32_t ds)
     return out;
 }
 
-// Maps of the CRC fast path (bit_fast.hip, n <= 32): 8 nibble tables x 16 u32 entries each,
-// T[i][v] = (v << 4i) * C mod P for a constant C = x^e mod P.  Maps: x^0, x^32, x^64, x^96 (piece
-// dwords), x^8192 (one lane's pieces, 1 KiB apart), x^(128 2^j) j < 6 (lane tree; the kernels use
-// j = 4, 5 after the lane maps below), then the final
-// factor placing the zero-padded 16-byte grid: encode x^(8 (ds + m - 1024 (NP + 1)) + n - 1) for
-// each payload misalignment m < 16, check x^(8 (ds - bs) + n - 1).
+// Maps of the CRC fast path (bit_fast.hip, n <= 32), at the offsets bit_fast.hip reports
+// (ppfs_crc_fast_layout): nibble maps (8 nibble tables x 16 u32 entries, T[i][v] = (v << 4i) * C mod
+// P for a constant C = x^e mod P): x^0, x^32, x^64, x^96 (piece dwords), x^8192 (one lane's pieces,
+// 1 KiB apart), x^(128 2^j) j < 6 (lane tree; the kernels use j = 4, 5 after the lane maps), the
+// encode's placement factors x^(8 (ds + m - 1024 (NP + 1)) + n - 1) for each payload misalignment
+// m < 16 and the check's x^(8 (ds - bs) + n - 1); the 16 transposed lane maps; the 6-bit tree maps;
+// the 8-bit piece / Horner maps; the per-position piece maps of the check (PPC) and encode (PPE).
 std::vector<uint8_t> build_crc_fast_tables(uint64_t P, int n, uint32_t ds, uint32_t bs)
 {
+    struct Lay {
+        int32_t map, nmaps, lane_off, lanes, six_off, nsix, map6, eight_off, neight, eight, ppc_off, nppc, ppe_off, nppe,
+            bytes;
+    } ly;
+    if (ppfs_crc_fast_layout((int32_t*)&ly, (int)(sizeof(ly) / 4)) != (int)(sizeof(ly) / 4) || ly.map != 8 * 16 * 4
+        || ly.lane_off < ly.nmaps * ly.map || ly.six_off < ly.lane_off + ly.lanes * ly.map
+        || ly.eight_off < ly.six_off + ly.nsix * ly.map6 || ly.ppc_off < ly.eight_off + ly.neight * ly.eight
+        || ly.ppe_off < ly.ppc_off + ly.nppc * ly.map || ly.bytes < ly.ppe_off + ly.nppe * ly.map || ly.neight != 5
+        || ly.nsix != 2 || ly.map6 < 5 * 256 + 16 || ly.eight != 4096)
+        return {}; // the device layout changed under this builder: refuse (create fails) rather than misplace
     CrcHost c { P, n, n == 64 ? ~0ull : ((1ull << n) - 1) };
     const long NP = bs / 1024;
     std::vector<long> ex = { 0, 32, 64, 96, 8192 };
@@ -481,18 +490,22 @@ std::vector<uint8_t> build_crc_fast_tables(uint64_t P, int n, uint32_t ds, uint3
     for (long m = 0; m < 16; ++m)
         ex.push_back(8L * ((long)ds + m - 1024L * (NP + 1)) + n - 1);
     ex.push_back(8L * ((long)ds - (long)bs) + n - 1);
+    if ((int)ex.size() != ly.nmaps || 4 * NP > ly.nppc || 4 * (NP + 1) > ly.nppe)
+        return {};
 
-    std::vector<uint8_t> out((size_t)ppfs_crc_fast_tables_bytes(), 0);
-    uint32_t* t = (uint32_t*)out.data();
-    for (size_t mi = 0; mi < ex.size(); ++mi) {
-        const uint64_t C = c.xpow(ex[mi]);
+    std::vector<uint8_t> out((size_t)ly.bytes, 0);
+    auto nibble_map = [&](uint8_t* dst, long e) {
+        const uint64_t C = c.xpow(e);
+        uint32_t* t = (uint32_t*)dst;
         for (int i = 0; i < 8; ++i)
             for (int v = 0; v < 16; ++v)
-                t[(mi * 8 + i) * 16 + v] = (uint32_t)c.mul(c.mod((uint64_t)v << (4 * i)), C);
-    }
+                t[i * 16 + v] = (uint32_t)c.mul(c.mod((uint64_t)v << (4 * i)), C);
+    };
+    for (size_t mi = 0; mi < ex.size(); ++mi)
+        nibble_map(out.data() + mi * ly.map, ex[mi]);
     // lane maps: lane b of NL = 16 multiplies by x^(128 (NL - 1 - b)), transposed: dword (16 i + v) NL + b
-    const int NL = ppfs_crc_fast_lane_maps();
-    uint32_t* lt = t + ex.size() * 8 * 16;
+    const int NL = ly.lanes;
+    uint32_t* lt = (uint32_t*)(out.data() + ly.lane_off);
     for (int b = 0; b < NL; ++b) {
         const uint64_t C = c.xpow(128L * (NL - 1 - b));
         for (int i = 0; i < 8; ++i)
@@ -501,34 +514,33 @@ std::vector<uint8_t> build_crc_fast_tables(uint64_t P, int n, uint32_t ds, uint3
     }
     // 6-bit tables of the lane-tree maps x^2048, x^4096 (bit_fast.hip CF_MAP6): sub-table j < 5 = 64
     // entries (v << 6j) C, then 4 entries (v << 30) C
-    {
-        uint8_t* st = (uint8_t*)(lt + 8 * 16 * NL);
-        const long sx[2] = { ex[9], ex[10] };
-        for (int q = 0; q < 2; ++q, st += 5 * 256 + 16) {
-            const uint64_t C = c.xpow(sx[q]);
-            uint32_t* e = (uint32_t*)st;
-            for (int j = 0; j < 5; ++j)
-                for (int v = 0; v < 64; ++v)
-                    e[64 * j + v] = (uint32_t)c.mul(c.mod((uint64_t)v << (6 * j)), C);
-            for (int v = 0; v < 4; ++v)
-                e[320 + v] = (uint32_t)c.mul(c.mod((uint64_t)v << 30), C);
+    for (int q = 0; q < 2; ++q) {
+        const uint64_t C = c.xpow(ex[9 + q]);
+        uint32_t* e = (uint32_t*)(out.data() + ly.six_off + q * ly.map6);
+        for (int j = 0; j < 5; ++j)
+            for (int v = 0; v < 64; ++v)
+                e[64 * j + v] = (uint32_t)c.mul(c.mod((uint64_t)v << (6 * j)), C);
+        for (int v = 0; v < 4; ++v)
+            e[320 + v] = (uint32_t)c.mul(c.mod((uint64_t)v << 30), C);
+    }
+    // 8-bit tables (bit_fast.hip CF_EIGHT): x^0, x^32, x^64, x^96 indexed by the bytes of the payload
+    // dword in memory order (table k = byte 3 - k of the value), x^8192 by the bytes of a value
+    uint32_t* e8 = (uint32_t*)(out.data() + ly.eight_off);
+    for (int q = 0; q < 5; ++q) {
+        const uint64_t C = c.xpow(ex[q]);
+        for (int k = 0; k < 4; ++k) {
+            const int vb = q < 4 ? 3 - k : k; // the value byte that input byte k holds
+            for (int v = 0; v < 256; ++v)
+                e8[q * 1024 + k * 256 + v] = (uint32_t)c.mul(c.mod((uint64_t)v << (8 * vb)), C);
         }
     }
-    // 8-bit tables (bit_fast.hip CF_EIGHT) after the 6-bit ones: x^0, x^32, x^64, x^96 indexed by
-    // the bytes of the payload dword in memory order (table k = byte 3 - k of the value), x^8192 by
-    // the bytes of a value
-    {
-        uint32_t* e8 = (uint32_t*)(out.data() + out.size() - 5 * 4096);
-        const long ex8[5] = { ex[0], ex[1], ex[2], ex[3], ex[4] };
-        for (int q = 0; q < 5; ++q) {
-            const uint64_t C = c.xpow(ex8[q]);
-            for (int k = 0; k < 4; ++k) {
-                const int vb = q < 4 ? 3 - k : k; // the value byte that input byte k holds
-                for (int v = 0; v < 256; ++v)
-                    e8[q * 1024 + k * 256 + v] = (uint32_t)c.mul(c.mod((uint64_t)v << (8 * vb)), C);
-            }
-        }
-    }
+    // per-position piece maps: piece k of NPK, dword q -> x^(32 (3 - q) + 8192 (NPK - 1 - k))
+    for (long k = 0; k < NP; ++k)
+        for (int q = 0; q < 4; ++q)
+            nibble_map(out.data() + ly.ppc_off + (4 * k + q) * ly.map, 32L * (3 - q) + 8192L * (NP - 1 - k));
+    for (long k = 0; k <= NP; ++k)
+        for (int q = 0; q < 4; ++q)
+            nibble_map(out.data() + ly.ppe_off + (4 * k + q) * ly.map, 32L * (3 - q) + 8192L * (NP - k));
     return out;
 }
 
@@ -957,6 +969,10 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
         tables = build_crc_tables(p.crc_polynomial, n, c->data);
         if (ppfs_crc_fast_supported(p.block_size, (uint32_t)n)) {
             const std::vector<uint8_t> f = build_crc_fast_tables(p.crc_polynomial, n, c->data, p.block_size);
+            if (f.empty()) {
+                delete c;
+                return fail(PPFS_ECC_EINVAL, "CRC fast tables: device layout mismatch");
+            }
             tables.insert(tables.end(), f.begin(), f.end());
         }
         c->kname = ppfs_crc_fast_supported(p.block_size, (uint32_t)n) ? "crc-piecemap-wave" : "crc-nibble-shift";
