@@ -274,9 +274,8 @@ template <int T2> std::vector<uint8_t> build_rs_wg_tables_t()
                         G.mul((uint8_t)(v << (4 * h)), G.exp[e]);
                 }
     build_gf_block(out.data() + L::OFF_GF);
-    const std::vector<uint16_t> es = ppfs::sched::build_encode(T2), ds = ppfs::sched::build_decode(T2);
+    const std::vector<uint16_t> es = ppfs::sched::build_encode(T2);
     std::memcpy(out.data() + L::OFF_ESCHED, es.data(), es.size() * sizeof(uint16_t));
-    std::memcpy(out.data() + L::OFF_DSCHED, ds.data(), ds.size() * sizeof(uint16_t));
     const std::vector<uint8_t> rm = ppfs::sched::row_map(L::K);
     std::memcpy(out.data() + L::OFF_ROWMAP, rm.data(), rm.size());
     // SL5 / SLX5 from the nibble tables by linearity: bit m of the 64-bit chunk (byte m / 8, nibble

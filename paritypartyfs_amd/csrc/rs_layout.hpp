@@ -36,13 +36,13 @@ template <int T2> struct RsWgLayout {
     // step of segment m, which then needs no x^(64 m) map (rs_wg.hpp seg_remainder)
     static constexpr int OFF_SLX = OFF_MAP32 + 7 * MAP_STRIDE;
     static constexpr int SLX_BYTES = 3 * 16 * TBL;
-    // ESCHED / DSCHED (round 4): the encode / decode emission schedules (rs_sched.hpp), 256 threads
-    // x 4 rounds of u16; the encode DMAs its schedule into the staging buffer once per workgroup
+    // ESCHED (round 4): the encode's emission schedule (rs_sched.hpp), 256 threads x 4 rounds of u16;
+    // the encode DMAs it into the staging buffer once per workgroup (the decode emits in natural
+    // order: its schedule is built only by tests/cpp/test_sched.cpp)
     static constexpr int OFF_ESCHED = OFF_SLX + SLX_BYTES;
     static constexpr int SCHED_BYTES = 2048;
-    static constexpr int OFF_DSCHED = OFF_ESCHED + SCHED_BYTES;
     // ROWMAP (round 4): the encode's lane -> payload row of phase 1 (rs_sched.hpp row_map), 64 bytes
-    static constexpr int OFF_ROWMAP = OFF_DSCHED + SCHED_BYTES;
+    static constexpr int OFF_ROWMAP = OFF_ESCHED + SCHED_BYTES;
     // SL5 / SLX5 (round 4): SL and SLX as 5-bit field tables for the encode's phase 1: table i (of
     // 13), value v -> the contribution of v at bits [5i, 5i+5) of the 64-bit chunk; 32 entries x 8 B
     // = 256 B, the 64 banks of a ds_read_b64 lane group (conflict-free), 13 lookups per step not 16

@@ -1,6 +1,7 @@
 #pragma once
 // rs_sched.hpp -- emission schedules of the t <= 4 RS tile kernels (rs_wg_tk.hpp), built on the host
-// once per context and stored in the table blob (rs_layout.hpp OFF_ESCHED / OFF_DSCHED).
+// once per context and stored in the table blob (rs_layout.hpp OFF_ESCHED; the decode schedule only in
+// tests/cpp/test_sched.cpp).
 //
 // A 64-block tile's output is 1020 (encode: 64 x 255 B) or 64 K / 16 (decode: 64 x K B) 16-byte
 // pieces; the 256 threads emit them in 4 rounds.  Most pieces are "interior": all 16 bytes come from

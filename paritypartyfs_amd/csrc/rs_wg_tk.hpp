@@ -182,12 +182,6 @@ template <int T2> __device__ __forceinline__ uint32_t sched_enc_src(uint32_t p)
     const uint32_t j0 = 16u * p, b = j0 / 255u, off = j0 - 255u * b;
     return (uint32_t)PAD + (255u - T2) * b + off - (uint32_t)T2;
 }
-template <int T2> __device__ __forceinline__ uint32_t sched_dec_src(uint32_t p)
-{
-    constexpr uint32_t K = 255u - T2;
-    const uint32_t j0 = 16u * p, b = j0 / K, off = j0 - K * b;
-    return (uint32_t)PAD + 255u * b + (uint32_t)T2 + off;
-}
 
 template <int T2, int WPC = 2, int NTST = 1>
 __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t* __restrict__ data,

@@ -85,7 +85,7 @@ static void check(int t2, bool dec)
         }
     }
     std::vector<int> seen(npieces, 0);
-    int interior = 0, boundary = 0, cyc_sched = 0, cyc_nat = 0, cyc_stage = 0;
+    int interior = 0, boundary = 0, cyc_sched = 0, cyc_nat = 0, cyc_stage = 0, bnd_waves = 0;
     for (uint32_t k = 0; k < 4; ++k) {
         for (uint32_t w = 0; w < 4; ++w) {
             std::vector<uint32_t> s_lane(64, ~0u), n_lane(64, ~0u);
@@ -125,6 +125,12 @@ static void check(int t2, bool dec)
                 CHECK(std::memcmp(o, &out[16u * p], 16) == 0, "t2 %d dec %d: interior piece %u bytes differ", t2, dec, p);
             }
             CHECK(k < 3 || have > 0, "t2 %d dec %d: wave %u has no round-3 piece", t2, dec, w);
+            if (k == 3)
+                for (uint32_t l = 0; l < 64; ++l)
+                    if (sc[4 * (64 * w + l) + k] != kNone && (sc[4 * (64 * w + l) + k] & kBoundary)) {
+                        ++bnd_waves;
+                        break;
+                    }
             CHECK(k == 3 || have == 64, "t2 %d dec %d: wave %u round %u has %d pieces", t2, dec, w, k, have);
             cyc_sched += window_cycles(s_lane);
             cyc_nat += window_cycles(n_lane);
@@ -149,6 +155,11 @@ static void check(int t2, bool dec)
                 "staging-store group cycles %d (ideal 128)\n",
         t2, dec ? "decode" : "encode", interior, boundary, cyc_sched, cyc_nat, cyc_stage);
     CHECK(cyc_sched <= cyc_nat, "t2 %d dec %d: schedule conflicts more than the natural order", t2, dec);
+    // the boundary pieces (the general byte-mask merge) stay packed at the end of round 3: at most one
+    // wave more than they fill runs the merge path (the polish swaps boundary slots with boundary /
+    // empty slots only); spread over every wave, each wave would run both emission paths
+    const int need = (boundary + 63) / 64;
+    CHECK(bnd_waves <= need + 1, "t2 %d dec %d: boundary pieces spread over %d waves (%d needed)", t2, dec, bnd_waves, need);
 }
 
 static void check_rows(uint32_t len)
