@@ -134,6 +134,12 @@ __device__ __forceinline__ void bs_lookups(uint32_t (&acc)[4], const uint8_t* ld
 
 // Remainder column c of a LEN-byte row at LDS byte `row` (rs_pair.hpp pair_remainder with the
 // byte lookups; the top chunk holds LEN - 8 (NC - 1) bytes)
+// PPFS_BS_SPLITRD: the lanes of a pair read one row dword each per step (lane c dword 2j + c) and
+// swap them by DPP, where both read both (the same addresses): one 2-way ds_read_b32 a step instead
+// of two, for one DPP move and two v_bfi
+#ifndef PPFS_BS_SPLITRD
+#define PPFS_BS_SPLITRD 0
+#endif
 template <int LEN>
 __device__ __forceinline__ void bs_remainder(uint32_t (&s)[4], const uint8_t* lds, uint32_t row, const BsLane& L)
 {
@@ -144,9 +150,18 @@ __device__ __forceinline__ void bs_remainder(uint32_t (&s)[4], const uint8_t* ld
     uint32_t cm = L.c ? ~0u : 0u;
     asm("" : "+v"(cm)); // a mask, not a select: keeps (dpp & cm) one v_and_b32_dpp
     uint32_t up = w[2 * NC];
+#if PPFS_BS_SPLITRD
+    const uint32_t* wc = w + L.c; // lane c's dword of every chunk
+#endif
 #pragma unroll
     for (int j = NC - 1; j >= 0; --j) {
+#if PPFS_BS_SPLITRD
+        const uint32_t mine = wc[2 * j];
+        const uint32_t other = (uint32_t)__builtin_amdgcn_mov_dpp((int)mine, 0xB1, 0xF, 0xF, false); // quad_perm [1,0,3,2]
+        const uint32_t d1 = (cm & mine) | (~cm & other), d0 = (cm & other) | (~cm & mine);
+#else
         const uint32_t d1 = w[2 * j + 1], d0 = w[2 * j];
+#endif
         uint32_t hi = __builtin_amdgcn_alignbit(up, d1, sh); // payload bytes 8j+4 .. 8j+7
         uint32_t lo = __builtin_amdgcn_alignbit(d1, d0, sh); // payload bytes 8j .. 8j+3
         up = d0;

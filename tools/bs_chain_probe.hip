@@ -1,0 +1,112 @@
+// bs_chain_probe.hip -- the 2t = 32 byte-slice remainder chain (rs_bs.hpp) in isolation: no HBM
+// traffic, one workgroup per CU, NW waves each on its own LDS tile image, ILP independent chains per
+// lane (rows of blocks blk, blk ^ 16, ...).  Reports the chip-wide chain throughput (blocks / us)
+// and cycles per chain step, so that the decode's chain can be classified as latency- or
+// LDS-bandwidth-bound and the gain of more chains in flight (waves or ILP) estimated before a
+// kernel is built around it.  Diagnostic, not shipped:  make -C tools bs_chain_probe.bin
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "rs_bs.hpp"
+
+using namespace ppfs;
+using namespace ppfs::bs;
+
+template <int NW, int ILP>
+__global__ __launch_bounds__(64 * NW, 1) void chain_probe(const uint8_t* __restrict__ tab, const uint8_t* __restrict__ img_src,
+    int reps, uint32_t* __restrict__ sink, unsigned long long* __restrict__ cyc)
+{
+    constexpr int NI = NW < 8 ? NW : 8; // images (read-only here: waves w and w + 8 share one)
+    constexpr int BYTES = TAB_BYTES + NI * IMGW + 64;
+    static_assert(BYTES <= 163840, "LDS");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[BYTES];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
+    for (uint32_t p = tid; p < (uint32_t)BYTES / 16; p += 64u * NW)
+        *(uint4*)(lds + 16 * p) = *(const uint4*)(p < TAB_BYTES / 16 ? tab + 16 * p : img_src + 16 * (p % 4096));
+    __syncthreads();
+    const BsLane Ln = bs_lane(lane);
+    const uint32_t img = TAB_BYTES + (wave % NI) * (uint32_t)IMGW;
+    uint32_t acc = 0;
+    const unsigned long long t0 = clock64();
+    for (int r = 0; r < reps; ++r) {
+        uint32_t s[ILP][4];
+        uint32_t rows[ILP];
+#pragma unroll
+        for (int i = 0; i < ILP; ++i)
+            rows[i] = img + 255u * ((Ln.blk ^ (16u * (uint32_t)i)) & 31u) + 32u + (uint32_t)(r & 1);
+        bs_remainder_n<223, ILP>(s, lds, rows, Ln);
+#pragma unroll
+        for (int i = 0; i < ILP; ++i)
+            acc ^= s[i][0] ^ s[i][1] ^ s[i][2] ^ s[i][3];
+    }
+    const unsigned long long t1 = clock64();
+    if (acc == 0x9E3779B9u)
+        sink[blockIdx.x] = acc;
+    if (tid == 0)
+        cyc[blockIdx.x] = t1 - t0;
+}
+
+template <int NW, int ILP> static void run(const uint8_t* tab, const uint8_t* src, uint32_t* sink, unsigned long long* cyc, int cus)
+{
+    const int reps = 64;
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    for (int w = 0; w < 3; ++w)
+        hipLaunchKernelGGL((chain_probe<NW, ILP>), dim3(cus), dim3(64 * NW), 0, 0, tab, src, reps, sink, cyc);
+    (void)hipEventRecord(a, 0);
+    const int L = 10;
+    for (int i = 0; i < L; ++i)
+        hipLaunchKernelGGL((chain_probe<NW, ILP>), dim3(cus), dim3(64 * NW), 0, 0, tab, src, reps, sink, cyc);
+    (void)hipEventRecord(b, 0);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    std::vector<unsigned long long> c(cus);
+    (void)hipMemcpy(c.data(), cyc, cus * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    double cm = 0;
+    for (auto v : c)
+        cm += (double)v;
+    cm /= cus;
+    const double blocks = (double)cus * NW * 32 * ILP * reps; // per launch
+    const double us = ms * 1e3 / L;
+    // 28 steps per chain; cycles per step of one wave (all its ILP chains advance one step)
+    std::printf("{\"nw\": %d, \"ilp\": %d, \"us_per_launch\": %.2f, \"blocks_per_us\": %.1f, \"cycles_per_wave_step\": %.1f, "
+                "\"cycles_per_block_step_per_cu\": %.2f, \"equiv_us_2p20_blocks\": %.1f}\n",
+        NW, ILP, us, blocks / us, cm / (reps * 28.0), cm / (reps * 28.0) / (NW * 32 * ILP), (double)(1 << 20) / (blocks / us));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+}
+
+int main()
+{
+    int cus = 0;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    std::vector<uint8_t> h(TAB_BYTES + 65536);
+    srand(7);
+    for (auto& v : h)
+        v = (uint8_t)rand();
+    uint8_t *tab, *src;
+    uint32_t* sink;
+    unsigned long long* cyc;
+    (void)hipMalloc(&tab, TAB_BYTES);
+    (void)hipMalloc(&src, 65536);
+    (void)hipMalloc(&sink, 4096 * 4);
+    (void)hipMalloc(&cyc, 4096 * 8);
+    (void)hipMemcpy(tab, h.data(), TAB_BYTES, hipMemcpyHostToDevice);
+    (void)hipMemcpy(src, h.data() + TAB_BYTES, 65536, hipMemcpyHostToDevice);
+    run<8, 1>(tab, src, sink, cyc, cus);
+    run<8, 2>(tab, src, sink, cyc, cus);
+    run<4, 1>(tab, src, sink, cyc, cus);
+    run<4, 2>(tab, src, sink, cyc, cus);
+    run<4, 4>(tab, src, sink, cyc, cus);
+    run<12, 1>(tab, src, sink, cyc, cus);
+    run<12, 2>(tab, src, sink, cyc, cus);
+    run<16, 1>(tab, src, sink, cyc, cus);
+    const hipError_t e = hipDeviceSynchronize();
+    std::printf("{\"status\": \"%s\"}\n", hipGetErrorString(e));
+    return e == hipSuccess ? 0 : 1;
+}
