@@ -19,5 +19,9 @@ python3 -c "
 import json
 for l in open('gpurun_out/r5a_cfg4_ab.jsonl'):
     d=json.loads(l); print(d['lib'], d['round'], d.get('name'), {k: v for k, v in d.items() if 'frac' in k})"
-PPFS_ECC_LIB=$L/libppfs_ecc_splitrd.so timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "rs and 4096" > gpurun_out/r5a_splitrd_pytest.log 2>&1; rc=$?; tail -2 gpurun_out/r5a_splitrd_pytest.log; [ $rc -eq 0 ] || exit $rc
-bash tools/ab_codec.sh r5a rs16 3 paritypartyfs_amd/_lib/libppfs_ecc.so $L/libppfs_ecc_splitrd.so $L/libppfs_ecc_n1.so $L/libppfs_ecc_ilp2n1.so || exit 1
+for v in splitrd rp; do
+  PPFS_ECC_LIB=$L/libppfs_ecc_$v.so timeout -k 10 300 $PYT tests/test_gpu_parity.py -k "rs and 4096" > gpurun_out/r5a_${v}_pytest.log 2>&1; rc=$?; tail -2 gpurun_out/r5a_${v}_pytest.log; [ $rc -eq 0 ] || exit $rc
+done
+bash tools/ab_codec.sh r5a rs16 3 paritypartyfs_amd/_lib/libppfs_ecc.so $L/libppfs_ecc_rp.so $L/libppfs_ecc_splitrd.so $L/libppfs_ecc_n1.so $L/libppfs_ecc_ilp2n1.so || exit 1
+# last: unaligned 16-byte global stores (a misaligned-access fault would end the lease here)
+timeout -k 10 120 tools/row_store_probe.bin > gpurun_out/r5a_row_store_probe.jsonl 2>&1; rc=$?; cat gpurun_out/r5a_row_store_probe.jsonl; [ $rc -eq 0 ] || exit $rc
