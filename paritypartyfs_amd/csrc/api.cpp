@@ -468,17 +468,15 @@ std::vector<uint8_t> build_crc_tables(uint64_t P, int n, uint32_t ds)
 // 1 KiB apart), x^(128 2^j) j < 6 (lane tree; the kernels use j = 4, 5 after the lane maps), the
 // encode's placement factors x^(8 (ds + m - 1024 (NP + 1)) + n - 1) for each payload misalignment
 // m < 16 and the check's x^(8 (ds - bs) + n - 1); the 16 transposed lane maps; the 6-bit tree maps;
-// the 8-bit piece / Horner maps; the per-position piece maps of the check (PPC) and encode (PPE).
+// the 8-bit piece / Horner maps.
 std::vector<uint8_t> build_crc_fast_tables(uint64_t P, int n, uint32_t ds, uint32_t bs)
 {
     struct Lay {
-        int32_t map, nmaps, lane_off, lanes, six_off, nsix, map6, eight_off, neight, eight, ppc_off, nppc, ppe_off, nppe,
-            bytes;
+        int32_t map, nmaps, lane_off, lanes, six_off, nsix, map6, eight_off, neight, eight, bytes;
     } ly;
     if (ppfs_crc_fast_layout((int32_t*)&ly, (int)(sizeof(ly) / 4)) != (int)(sizeof(ly) / 4) || ly.map != 8 * 16 * 4
         || ly.lane_off < ly.nmaps * ly.map || ly.six_off < ly.lane_off + ly.lanes * ly.map
-        || ly.eight_off < ly.six_off + ly.nsix * ly.map6 || ly.ppc_off < ly.eight_off + ly.neight * ly.eight
-        || ly.ppe_off < ly.ppc_off + ly.nppc * ly.map || ly.bytes < ly.ppe_off + ly.nppe * ly.map || ly.neight != 5
+        || ly.eight_off < ly.six_off + ly.nsix * ly.map6 || ly.bytes < ly.eight_off + ly.neight * ly.eight || ly.neight != 5
         || ly.nsix != 2 || ly.map6 < 5 * 256 + 16 || ly.eight != 4096)
         return {}; // the device layout changed under this builder: refuse (create fails) rather than misplace
     CrcHost c { P, n, n == 64 ? ~0ull : ((1ull << n) - 1) };
@@ -489,7 +487,7 @@ std::vector<uint8_t> build_crc_fast_tables(uint64_t P, int n, uint32_t ds, uint3
     for (long m = 0; m < 16; ++m)
         ex.push_back(8L * ((long)ds + m - 1024L * (NP + 1)) + n - 1);
     ex.push_back(8L * ((long)ds - (long)bs) + n - 1);
-    if ((int)ex.size() != ly.nmaps || 4 * NP > ly.nppc || 4 * (NP + 1) > ly.nppe)
+    if ((int)ex.size() != ly.nmaps)
         return {};
 
     std::vector<uint8_t> out((size_t)ly.bytes, 0);
@@ -533,13 +531,6 @@ std::vector<uint8_t> build_crc_fast_tables(uint64_t P, int n, uint32_t ds, uint3
                 e8[q * 1024 + k * 256 + v] = (uint32_t)c.mul(c.mod((uint64_t)v << (8 * vb)), C);
         }
     }
-    // per-position piece maps: piece k of NPK, dword q -> x^(32 (3 - q) + 8192 (NPK - 1 - k))
-    for (long k = 0; k < NP; ++k)
-        for (int q = 0; q < 4; ++q)
-            nibble_map(out.data() + ly.ppc_off + (4 * k + q) * ly.map, 32L * (3 - q) + 8192L * (NP - 1 - k));
-    for (long k = 0; k <= NP; ++k)
-        for (int q = 0; q < 4; ++q)
-            nibble_map(out.data() + ly.ppe_off + (4 * k + q) * ly.map, 32L * (3 - q) + 8192L * (NP - k));
     return out;
 }
 

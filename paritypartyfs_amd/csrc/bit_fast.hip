@@ -757,29 +757,14 @@ constexpr int CF_SIX_OFF = CF_NMAPS * CF_MAP + CF_LANES * CF_MAP;
 // lookups, for a third of the VALU (r4z: encode 1.603 vs 1.625 ms against the 6-bit maps).
 constexpr int CF_EIGHT = 4096, CF_NEIGHT = 5;
 constexpr int CF_EIGHT_OFF = CF_SIX_OFF + CF_NSIX * CF_MAP6;
-// Per-position piece maps (round 5): piece k of NPK (the check's NP raw pieces, the encode's NP + 1
-// superset pieces), dword q -> x^(32 (3 - q) + 8192 (NPK - 1 - k)) mod P, nibble tables.  Every piece
-// then reduces straight into the lane's accumulator: no Horner over a lane's pieces (3-4 dependent
-// maps fewer on the critical path), and the encode's lookups are conflict-free nibble tables where
-// its 8-bit maps spent 56 % of LDS cycles in bank conflicts.  Check maps: PPC (k < NP), encode: PPE.
-constexpr int CF_NPPC = 16, CF_NPPE = 20;
-constexpr int CF_PPC_OFF = CF_EIGHT_OFF + CF_NEIGHT * CF_EIGHT;
-constexpr int CF_PPE_OFF = CF_PPC_OFF + CF_NPPC * CF_MAP;
-constexpr int CF_BYTES = CF_PPE_OFF + CF_NPPE * CF_MAP; // 22 KiB + 2.5 KiB + 20 KiB + 18 KiB
-#ifndef PPFS_CRC_CHK_PP
-#define PPFS_CRC_CHK_PP 0
-#endif
-#ifndef PPFS_CRC_ENC_PP
-#define PPFS_CRC_ENC_PP 0
-#endif
+constexpr int CF_BYTES = CF_EIGHT_OFF + CF_NEIGHT * CF_EIGHT; // 22 KiB + 2.5 KiB + 20 KiB
 // The encode's LDS image: the 16 placement maps FENC (one per payload misalignment), the lane maps,
 // the 6-bit tree maps, the 8-bit maps -- 39,456 B, 4 workgroups per CU.  (The check keeps the nibble
 // maps: on the 8-bit maps it ran the same, r4za.)
-template <int NPLACE, bool PP = false> struct CrcLds {
+template <int NPLACE> struct CrcLds {
     static constexpr int PLACE = 0, LANE = NPLACE * CF_MAP, SIX = LANE + CF_LANES * CF_MAP, EIGHT = SIX + CF_NSIX * CF_MAP6;
-    // PP: the per-position encode maps (PPE) where the 8-bit maps sat
-    static constexpr int BYTES = EIGHT + (PP ? CF_NPPE * CF_MAP : CF_NEIGHT * CF_EIGHT);
-    static_assert(SIX % 16 == 0 && EIGHT % 16 == 0 && CF_EIGHT_OFF % 16 == 0 && CF_PPC_OFF % 16 == 0, "16-byte staging");
+    static constexpr int BYTES = EIGHT + CF_NEIGHT * CF_EIGHT;
+    static_assert(SIX % 16 == 0 && EIGHT % 16 == 0 && CF_EIGHT_OFF % 16 == 0, "16-byte staging");
     // copy the image's parts from the blob (placement maps from blob map `place0`)
     __device__ static void stage(uint8_t* tbl, const uint8_t* __restrict__ tables, int place0)
     {
@@ -790,13 +775,10 @@ template <int NPLACE, bool PP = false> struct CrcLds {
         part(PLACE, place0 * CF_MAP, NPLACE * CF_MAP);
         part(LANE, CF_LANE_OFF, CF_LANES * CF_MAP);
         part(SIX, CF_SIX_OFF, CF_NSIX * CF_MAP6);
-        if constexpr (PP)
-            part(EIGHT, CF_PPE_OFF, CF_NPPE * CF_MAP);
-        else
-            part(EIGHT, CF_EIGHT_OFF, CF_NEIGHT * CF_EIGHT);
+        part(EIGHT, CF_EIGHT_OFF, CF_NEIGHT * CF_EIGHT);
     }
 };
-using CE = CrcLds<16, PPFS_CRC_ENC_PP != 0>;
+using CE = CrcLds<16>;
 // Blocks per wave of the CRC kernels: a workgroup stages its maps once and then walks CRC_BPW
 // consecutive 4-block groups (one contiguous range, so the full grid keeps its address order); with
 // one group per workgroup the map staging read as much L2 as the blocks themselves.  Encode 8 (39 KiB
@@ -921,35 +903,6 @@ __device__ __forceinline__ uint32_t crc_piece8(const uint8_t* te, uint4 v, uint3
         ^ (n32 ? bswap(w[3]) : cmap8(te, w[3]));
 }
 
-// crc_piece through per-position maps (tb: the piece's 4 maps, dword q at tb + q CF_MAP); ident3:
-// dword 3's map is x^0 and n = 32 (the value is its own residue)
-// dep: an opaque zero (pp_dep) computed from an earlier piece's value -- the piece's lookups wait for it,
-// so at most two pieces' lookups are in flight (all of them at once need ~40 VGPRs more than the
-// 4-waves-per-SIMD budget and spill)
-__device__ __forceinline__ uint32_t crc_piece_pp(const uint8_t* tb, uint4 v, uint32_t lo, uint32_t hi, bool ident3, uint32_t dep = 0)
-{
-    uint32_t w[4] = { v.x | dep, v.y | dep, v.z | dep, v.w | dep };
-    if (lo > 0 || hi < 16) {
-        auto ge = [](uint32_t b) { return b >= 8u ? 0ull : (~0ull << (8u * b)); };
-        const uint64_t m0 = ge(lo) & ~ge(hi);
-        const uint64_t m1 = ge(lo > 8u ? lo - 8u : 0u) & ~ge(hi > 8u ? hi - 8u : 0u);
-        w[0] &= (uint32_t)m0;
-        w[1] &= (uint32_t)(m0 >> 32);
-        w[2] &= (uint32_t)m1;
-        w[3] &= (uint32_t)(m1 >> 32);
-    }
-    const uint32_t d3 = bswap(w[3]);
-    return __builtin_amdgcn_bitop3_b32(cmap(tb, bswap(w[0])), cmap(tb + CF_MAP, bswap(w[1])), cmap(tb + 2 * CF_MAP, bswap(w[2])), 0x96)
-        ^ (ident3 ? d3 : cmap(tb + 3 * CF_MAP, d3));
-}
-// an opaque 0 that the compiler must compute after v
-__device__ __forceinline__ uint32_t pp_dep(uint32_t v)
-{
-    uint32_t z;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(z) : "v"(v));
-    return z;
-}
-
 // value * x^(128 (15 - lane % 16)) mod P from the transposed lane maps (at tbl + LOFF)
 template <int LOFF = CF_LANE_OFF>
 __device__ __forceinline__ uint32_t lane_cmap(const uint8_t* tbl, uint32_t v, uint32_t lane)
@@ -1023,23 +976,14 @@ __global__ __launch_bounds__(256) PPFS_CRC_ENC_ATTR void crc_fast_encode_kernel(
         uint8_t* rb = raw + blk * a.bs;
         // superset piece q = 64 k + lane holds superset bytes [16 q, +16); payload = [m, m + ds)
         uint32_t acc = 0;
-        [[maybe_unused]] uint32_t pv[NP + 1];
 #pragma unroll
         for (int k = 0; k <= NP; ++k) {
             const int32_t q16 = 16 * (64 * k + (int32_t)lane);
             const int32_t lo = (int32_t)m - q16, hi = (int32_t)(m + a.ds) - q16;
             const uint32_t lo_c = lo < 0 ? 0u : (lo > 16 ? 16u : (uint32_t)lo);
             const uint32_t hi_c = hi < 0 ? 0u : (hi > 16 ? 16u : (uint32_t)hi);
-#if PPFS_CRC_ENC_PP
-            // only piece 0 (lane 0: the payload's start) and pieces NP - 1, NP (its end) can be partial
-            const bool edge = k == 0 || k >= NP - 1;
-            pv[k] = crc_piece_pp(tbl + CE::EIGHT + 4 * k * CF_MAP, cur.v[k], edge ? lo_c : 0u,
-                edge ? (hi_c > lo_c ? hi_c : lo_c) : 16u, n32 && k == NP, k >= 2 ? pp_dep(pv[k >= 2 ? k - 2 : 0]) : 0u);
-            acc ^= pv[k];
-#else
             const uint32_t pv = crc_piece8(tbl + CE::EIGHT, cur.v[k], lo_c, hi_c > lo_c ? hi_c : lo_c, n32);
             acc = k == 0 ? pv : (cmap8(tbl + CE::EIGHT + 4 * CF_EIGHT, acc) ^ pv);
-#endif
         }
         const uint32_t Vs = crc_lane_sum<CE::LANE, CE::SIX>(tbl, acc, lane);
         const uint32_t V = cmap(tbl + CE::PLACE + m * CF_MAP, Vs);
@@ -1080,14 +1024,9 @@ __global__ __launch_bounds__(256) PPFS_CRC_ATTR void crc_fast_check_kernel(const
     uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks_all, CrcFast a,
     const uint8_t* __restrict__ tables)
 {
-    // [0, CF_SIX_OFF): the nibble maps and lane maps; PP: the per-position check maps after them
-    constexpr int CHK_LDS = CF_SIX_OFF + (PPFS_CRC_CHK_PP ? CF_NPPC * CF_MAP : 0);
-    __shared__ __attribute__((aligned(16))) uint8_t tbl[CHK_LDS];
+    __shared__ __attribute__((aligned(16))) uint8_t tbl[CF_SIX_OFF];
     for (uint32_t p = threadIdx.x; p < CF_SIX_OFF / 16; p += 256)
         *(uint4*)(tbl + 16 * p) = *(const uint4*)(tables + 16 * p);
-    if constexpr (PPFS_CRC_CHK_PP)
-        for (uint32_t p = threadIdx.x; p < (uint32_t)(NP * 4 * CF_MAP) / 16; p += 256)
-            *(uint4*)(tbl + CF_SIX_OFF + 16 * p) = *(const uint4*)(tables + CF_PPC_OFF + 16 * p);
     __syncthreads();
     const uint32_t lane = lane_id(), wave = wave_id();
     const bool n32 = a.n == 32;
@@ -1108,21 +1047,13 @@ __global__ __launch_bounds__(256) PPFS_CRC_ATTR void crc_fast_check_kernel(const
             for (int k = 0; k < NP; ++k)
                 N[k] = gld16c(raw + nx * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
         uint32_t acc = 0;
-        [[maybe_unused]] uint32_t pv[NP];
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
             const int32_t q16 = 16 * (64 * k + (int32_t)lane);
             const int32_t hi = (int32_t)ds - q16;
             const uint32_t hi_c = hi < 0 ? 0u : (hi > 16 ? 16u : (uint32_t)hi);
-#if PPFS_CRC_CHK_PP
-            // the payload ends in the last piece (ds >= bs - 4): the others are whole
-            pv[k] = crc_piece_pp(tbl + CF_SIX_OFF + 4 * k * CF_MAP, R[k], 0u, k == NP - 1 ? hi_c : 16u, n32 && k == NP - 1,
-                k >= 2 ? pp_dep(pv[k >= 2 ? k - 2 : 0]) : 0u);
-            acc ^= pv[k];
-#else
             const uint32_t pv = crc_piece(tbl, R[k], 0u, hi_c, n32);
             acc = k == 0 ? pv : (cmap(tbl + CF_K * CF_MAP, acc) ^ pv);
-#endif
         }
         const uint32_t Vs = crc_lane_sum<CF_LANE_OFF, -1>(tbl, acc, lane);
         const uint32_t V = cmap(tbl + CF_FCHK * CF_MAP, Vs);
@@ -1226,10 +1157,7 @@ template <int NP> static constexpr uint32_t ham_enc_dyn_lds()
     return bf_occ_lds(PPFS_BF_HAM_ENC_WG, bf::WAVES * ((NP + 1) * 1024 + 32)); // ham_fast_encode_kernel's lds[]
 }
 template <int NP> static constexpr uint32_t par_chk_dyn_lds() { return bf_occ_lds(PPFS_BF_PAR_CHK_WG, 0); }
-template <int NP> static constexpr uint32_t crc_chk_dyn_lds()
-{
-    return bf_occ_lds(PPFS_BF_CRC_CHK_WG, bf::CF_SIX_OFF + (PPFS_CRC_CHK_PP ? bf::CF_NPPC * bf::CF_MAP : 0));
-}
+template <int NP> static constexpr uint32_t crc_chk_dyn_lds() { return bf_occ_lds(PPFS_BF_CRC_CHK_WG, bf::CF_SIX_OFF); }
 template <int NP> static constexpr uint32_t crc_enc_dyn_lds() { return bf_occ_lds(PPFS_BF_CRC_ENC_WG, bf::CE::BYTES); }
 template <int NP> static constexpr uint32_t no_dyn_lds() { return 0; }
 
@@ -1275,11 +1203,11 @@ extern "C" hipError_t ppfs_ham_fast_decode(uint8_t* r, uint8_t* d, uint8_t* st, 
 
 // The table blob's layout for the host builder (api.cpp build_crc_fast_tables), in this order:
 // map bytes, maps, lane-map offset, lane maps, 6-bit offset, 6-bit maps, 6-bit map bytes, 8-bit
-// offset, 8-bit maps, 8-bit map bytes, PPC offset, PPC maps, PPE offset, PPE maps, total bytes
+// offset, 8-bit maps, 8-bit map bytes, total bytes
 extern "C" int ppfs_crc_fast_layout(int32_t* v, int n)
 {
     const int32_t L[] = { bf::CF_MAP, bf::CF_NMAPS, bf::CF_LANE_OFF, bf::CF_LANES, bf::CF_SIX_OFF, bf::CF_NSIX, bf::CF_MAP6,
-        bf::CF_EIGHT_OFF, bf::CF_NEIGHT, bf::CF_EIGHT, bf::CF_PPC_OFF, bf::CF_NPPC, bf::CF_PPE_OFF, bf::CF_NPPE, bf::CF_BYTES };
+        bf::CF_EIGHT_OFF, bf::CF_NEIGHT, bf::CF_EIGHT, bf::CF_BYTES };
     const int m = (int)(sizeof(L) / sizeof(L[0]));
     for (int i = 0; i < m && i < n; ++i)
         v[i] = L[i];

@@ -134,12 +134,6 @@ __device__ __forceinline__ void bs_lookups(uint32_t (&acc)[4], const uint8_t* ld
 
 // Remainder column c of a LEN-byte row at LDS byte `row` (rs_pair.hpp pair_remainder with the
 // byte lookups; the top chunk holds LEN - 8 (NC - 1) bytes)
-// PPFS_BS_SPLITRD: the lanes of a pair read one row dword each per step (lane c dword 2j + c) and
-// swap them by DPP, where both read both (the same addresses): one 2-way ds_read_b32 a step instead
-// of two, for one DPP move and two v_bfi
-#ifndef PPFS_BS_SPLITRD
-#define PPFS_BS_SPLITRD 0
-#endif
 template <int LEN>
 __device__ __forceinline__ void bs_remainder(uint32_t (&s)[4], const uint8_t* lds, uint32_t row, const BsLane& L)
 {
@@ -150,18 +144,9 @@ __device__ __forceinline__ void bs_remainder(uint32_t (&s)[4], const uint8_t* ld
     uint32_t cm = L.c ? ~0u : 0u;
     asm("" : "+v"(cm)); // a mask, not a select: keeps (dpp & cm) one v_and_b32_dpp
     uint32_t up = w[2 * NC];
-#if PPFS_BS_SPLITRD
-    const uint32_t* wc = w + L.c; // lane c's dword of every chunk
-#endif
 #pragma unroll
     for (int j = NC - 1; j >= 0; --j) {
-#if PPFS_BS_SPLITRD
-        const uint32_t mine = wc[2 * j];
-        const uint32_t other = (uint32_t)__builtin_amdgcn_mov_dpp((int)mine, 0xB1, 0xF, 0xF, false); // quad_perm [1,0,3,2]
-        const uint32_t d1 = (cm & mine) | (~cm & other), d0 = (cm & other) | (~cm & mine);
-#else
         const uint32_t d1 = w[2 * j + 1], d0 = w[2 * j];
-#endif
         uint32_t hi = __builtin_amdgcn_alignbit(up, d1, sh); // payload bytes 8j+4 .. 8j+7
         uint32_t lo = __builtin_amdgcn_alignbit(d1, d0, sh); // payload bytes 8j .. 8j+3
         up = d0;
@@ -198,61 +183,6 @@ __device__ __forceinline__ void bs_remainder(uint32_t (&s)[4], const uint8_t* ld
             s[1] = n[1];
             s[2] = n[2];
             s[3] = n[3];
-        }
-    }
-}
-
-// PPFS_BS_ILP2_ABLATE (ablation builds only): the decode runs a second, independent remainder chain
-// (the row of block blk ^ 16) interleaved with its own, into a sink -- twice the chain's LDS lookups
-// at twice the independent work per lane: measures whether the chain is latency- or LDS-bound.
-#ifndef PPFS_BS_ILP2_ABLATE
-#define PPFS_BS_ILP2_ABLATE 0
-#endif
-template <int LEN, int NR>
-__device__ __forceinline__ void bs_remainder_n(uint32_t (&s)[NR][4], const uint8_t* lds, const uint32_t (&row)[NR], const BsLane& L)
-{
-    constexpr int NC = (LEN + 7) / 8;
-    constexpr int TOPN = LEN - 8 * (NC - 1);
-    uint32_t sh[NR], up[NR];
-    const uint32_t* w[NR];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-        sh[r] = (row[r] & 3u) * 8u;
-        w[r] = (const uint32_t*)(lds + (row[r] & ~3u));
-        up[r] = w[r][2 * NC];
-    }
-    uint32_t cm = L.c ? ~0u : 0u;
-    asm("" : "+v"(cm));
-#pragma unroll
-    for (int j = NC - 1; j >= 0; --j) {
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            const uint32_t d1 = w[r][2 * j + 1], d0 = w[r][2 * j];
-            uint32_t hi = __builtin_amdgcn_alignbit(up[r], d1, sh[r]);
-            uint32_t lo = __builtin_amdgcn_alignbit(d1, d0, sh[r]);
-            up[r] = d0;
-            if (j == NC - 1) {
-                if constexpr (TOPN < 4) {
-                    lo &= (1u << (8 * TOPN)) - 1u;
-                    hi = 0;
-                } else if constexpr (TOPN == 4) {
-                    hi = 0;
-                } else if constexpr (TOPN < 8) {
-                    hi &= (1u << (8 * (TOPN - 4))) - 1u;
-                }
-                s[r][0] = s[r][1] = s[r][2] = s[r][3] = 0;
-                bs_lookups(s[r], lds, L, lo, hi);
-            } else {
-                lo ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)s[r][2], 0xF5, 0xF, 0xF, true);
-                hi ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)s[r][3], 0xF5, 0xF, 0xF, true);
-                uint32_t n[4] = { (uint32_t)__builtin_amdgcn_mov_dpp((int)s[r][2], 0xA0, 0xF, 0xF, true) & cm,
-                    (uint32_t)__builtin_amdgcn_mov_dpp((int)s[r][3], 0xA0, 0xF, 0xF, true) & cm, s[r][0], s[r][1] };
-                bs_lookups(n, lds, L, lo, hi);
-                s[r][0] = n[0];
-                s[r][1] = n[1];
-                s[r][2] = n[2];
-                s[r][3] = n[3];
-            }
         }
     }
 }
@@ -637,7 +567,6 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
     uint64_t t = (uint64_t)blockIdx.x * NW + wave;
     auto src_off = [](uint32_t i) { return (int)(16u * i); };
     [[maybe_unused]] u32x4 pf[KP];
-    [[maybe_unused]] uint32_t ilp_sink = 0;
     if (t < nfull) {
         if constexpr (NBUF == 0) {
             load_wave(pf, raw + t * (TBW * 255), lane, src_off, raw, nblocks * 255u);
@@ -657,21 +586,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
         }
         PPFS_BS_MARK(1);
         uint32_t s[4];
-#if PPFS_BS_ILP2_ABLATE
-        {
-            uint32_t s2[2][4];
-            const uint32_t rows[2] = { row + 32u, img + 255u * (Ln.blk ^ 16u) + 32u };
-            bs_remainder_n<223, 2>(s2, lds, rows, Ln);
-            const uint32_t a = row + 16u * Ln.c, sha = (a & 3u) * 8u;
-            const uint32_t* wa = (const uint32_t*)(lds + (a & ~3u));
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-                s[m] = s2[0][m] ^ __builtin_amdgcn_alignbit(wa[m + 1], wa[m], sha);
-            ilp_sink ^= s2[1][0] ^ s2[1][1] ^ s2[1][2] ^ s2[1][3];
-        }
-#else
         bs_cmodg(s, lds, row, Ln);
-#endif
 #ifdef PPFS_TK_TRACE
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
@@ -762,10 +677,6 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
             }
         }
     }
-#if PPFS_BS_ILP2_ABLATE
-    if (ilp_sink == 0x9E3779B9u && status)
-        status[0] = 0x77; // keeps the second chain alive (never in practice)
-#endif
 #ifdef PPFS_TK_TRACE
     tr_[10] = clock64() - t0_;
     const uint32_t gw = blockIdx.x * NW + wave;

@@ -11,7 +11,6 @@
 #include "rs_wg_tk.hpp"
 #include "rs_pair.hpp"
 #include "rs_bs.hpp"
-#include "rs_bs_rp.hpp"
 #include "launch.hpp"
 
 #ifndef PPFS_T2
@@ -67,13 +66,6 @@ constexpr int ENC_WPC_STATIC = fit_wpc(wg::lds_bytes<PPFS_T2, false, ENC_NBUF>()
 #endif
 #ifndef PPFS_BS_DEC_NBUF
 #define PPFS_BS_DEC_NBUF 0 // register prefetch of the next tile (rs_bs.hpp load_wave); 1 = single LDS image
-#endif
-// round 5: the decode with the rows in registers (rs_bs_rp.hpp); 0 = rs_bs.hpp's image decode
-#ifndef PPFS_BS_DEC_RP
-#define PPFS_BS_DEC_RP 0
-#endif
-#ifndef PPFS_BS_RP_NTST
-#define PPFS_BS_RP_NTST 0
 #endif
 constexpr int BS_ENC_NW = 12, BS_DEC_NW = PPFS_BS_DEC_NW, BS_DEC_TLDS = PPFS_BS_DEC_TLDS, BS_DEC_NBUF = PPFS_BS_DEC_NBUF;
 #else
@@ -139,12 +131,8 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
         PPFS_LAUNCH((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC, 7, 1>), dim3(rs_tile_grid(nb, DEC_WPC)),
             dim3(256), 0, s, r, d, st, nb, tab, wb);
 #elif PPFS_T2 == 32
-    if constexpr (PPFS_BS_DEC_RP)
-        PPFS_LAUNCH((bs::rs_bs_decode_rp_kernel<PPFS_T2, BS_DEC_NW, PPFS_BS_RP_NTST, BS_DEC_TLDS>),
-            dim3(rs_tile_grid(nb, 1, bs::TBW * BS_DEC_NW)), dim3(64 * BS_DEC_NW), 0, s, r, d, st, nb, tab, wb);
-    else
-        PPFS_LAUNCH((bs::rs_bs_decode_kernel<PPFS_T2, BS_DEC_NW, BS_DEC_NBUF, 1, BS_DEC_TLDS>),
-            dim3(rs_tile_grid(nb, 1, bs::TBW * BS_DEC_NW)), dim3(64 * BS_DEC_NW), 0, s, r, d, st, nb, tab, wb);
+    PPFS_LAUNCH((bs::rs_bs_decode_kernel<PPFS_T2, BS_DEC_NW, BS_DEC_NBUF, 1, BS_DEC_TLDS>),
+        dim3(rs_tile_grid(nb, 1, bs::TBW * BS_DEC_NW)), dim3(64 * BS_DEC_NW), 0, s, r, d, st, nb, tab, wb);
 #else
     PPFS_LAUNCH(rs255_decode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, r, d, st, nb, tab, wb);
 #endif

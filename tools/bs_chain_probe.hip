@@ -15,6 +15,58 @@
 using namespace ppfs;
 using namespace ppfs::bs;
 
+// rs_bs.hpp bs_remainder over NR rows, the NR chains' steps interleaved
+template <int LEN, int NR>
+__device__ __forceinline__ void bs_remainder_n(uint32_t (&s)[NR][4], const uint8_t* lds, const uint32_t (&row)[NR], const BsLane& L)
+{
+    constexpr int NC = (LEN + 7) / 8;
+    constexpr int TOPN = LEN - 8 * (NC - 1);
+    uint32_t sh[NR], up[NR];
+    const uint32_t* w[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        sh[r] = (row[r] & 3u) * 8u;
+        w[r] = (const uint32_t*)(lds + (row[r] & ~3u));
+        up[r] = w[r][2 * NC];
+    }
+    uint32_t cm = L.c ? ~0u : 0u;
+    asm("" : "+v"(cm));
+#pragma unroll
+    for (int j = NC - 1; j >= 0; --j) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const uint32_t d1 = w[r][2 * j + 1], d0 = w[r][2 * j];
+            uint32_t hi = __builtin_amdgcn_alignbit(up[r], d1, sh[r]);
+            uint32_t lo = __builtin_amdgcn_alignbit(d1, d0, sh[r]);
+            up[r] = d0;
+            if (j == NC - 1) {
+                if constexpr (TOPN < 4) {
+                    lo &= (1u << (8 * TOPN)) - 1u;
+                    hi = 0;
+                } else if constexpr (TOPN == 4) {
+                    hi = 0;
+                } else if constexpr (TOPN < 8) {
+                    hi &= (1u << (8 * (TOPN - 4))) - 1u;
+                }
+                s[r][0] = s[r][1] = s[r][2] = s[r][3] = 0;
+                bs_lookups(s[r], lds, L, lo, hi);
+            } else {
+                lo ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)s[r][2], 0xF5, 0xF, 0xF, true);
+                hi ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)s[r][3], 0xF5, 0xF, 0xF, true);
+                uint32_t n[4] = { (uint32_t)__builtin_amdgcn_mov_dpp((int)s[r][2], 0xA0, 0xF, 0xF, true) & cm,
+                    (uint32_t)__builtin_amdgcn_mov_dpp((int)s[r][3], 0xA0, 0xF, 0xF, true) & cm, s[r][0], s[r][1] };
+                bs_lookups(n, lds, L, lo, hi);
+                s[r][0] = n[0];
+                s[r][1] = n[1];
+                s[r][2] = n[2];
+                s[r][3] = n[3];
+            }
+        }
+    }
+}
+
+
+
 template <int NW, int ILP>
 __global__ __launch_bounds__(64 * NW, 1) void chain_probe(const uint8_t* __restrict__ tab, const uint8_t* __restrict__ img_src,
     int reps, uint32_t* __restrict__ sink, unsigned long long* __restrict__ cyc)
