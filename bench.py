@@ -357,10 +357,24 @@ def host_link_ceilings(dev, nb, k, n, reps=3):
                 ts.append(time.perf_counter() - t0)
             return min(ts)
 
+        def both(b_in, b_out, chunk=8 << 20):
+            # the two directions in 8 MiB pieces, issued alternately on their own streams (one copy of
+            # each direction in flight at a time, as the engine's host path overlaps its chunks)
+            o_in = o_out = 0
+            while o_in < b_in or o_out < b_out:
+                if o_in < b_in:
+                    m = min(chunk, b_in - o_in)
+                    copy(vp(d_in.value + o_in), vp(h_in.value + o_in), m, H2D, streams[0])
+                    o_in += m
+                if o_out < b_out:
+                    m = min(chunk, b_out - o_out)
+                    copy(vp(h_out.value + o_out), vp(d_out.value + o_out), m, D2H, streams[1])
+                    o_out += m
+
         t_h2d = best(lambda: copy(d_in, h_in, k * nb, H2D, streams[0]))
         t_d2h = best(lambda: copy(h_out, d_out, n * nb, D2H, streams[1]))
-        t_enc = best(lambda: (copy(d_in, h_in, k * nb, H2D, streams[0]), copy(h_out, d_out, n * nb, D2H, streams[1])))
-        t_dec = best(lambda: (copy(d_in, h_in, n * nb, H2D, streams[0]), copy(h_out, d_out, (k + n) * nb, D2H, streams[1])))
+        t_enc = best(lambda: both(k * nb, n * nb))
+        t_dec = best(lambda: both(n * nb, (k + n) * nb))
     finally:
         for st in streams:
             if st.value:
@@ -379,8 +393,8 @@ def host_link_ceilings(dev, nb, k, n, reps=3):
         "bidir_decode_bytes_GBps": round((k + 2 * n) * nb / t_dec / 1e9, 2),
         "encode_ceiling_GiBps": round(alg / t_enc / GIB, 3),
         "decode_1err_ceiling_GiBps": round(alg / t_dec / GIB, 3),
-        "method": "hipMemcpyAsync between hipHostMalloc'd and hipMalloc'd buffers, H2D and D2H on two non-blocking "
-                  f"streams, best of {reps}",
+        "method": "hipMemcpyAsync between hipHostMalloc'd and hipMalloc'd buffers; both directions at once: 8 MiB "
+                  f"pieces issued alternately on two non-blocking streams; best of {reps}",
     }
 
 

@@ -67,6 +67,9 @@ constexpr int ENC_WPC_STATIC = fit_wpc(wg::lds_bytes<PPFS_T2, false, ENC_NBUF>()
 #ifndef PPFS_BS_DEC_NBUF
 #define PPFS_BS_DEC_NBUF 0 // register prefetch of the next tile (rs_bs.hpp load_wave); 1 = single LDS image
 #endif
+#ifndef PPFS_BS_ENC_NBUF
+#define PPFS_BS_ENC_NBUF 1 // single LDS image, the next tile's DMA after the emission; 0 = register prefetch
+#endif
 constexpr int BS_ENC_NW = 12, BS_DEC_NW = PPFS_BS_DEC_NW, BS_DEC_TLDS = PPFS_BS_DEC_TLDS, BS_DEC_NBUF = PPFS_BS_DEC_NBUF;
 #else
 // 8 < 2t <= 16: rs_fast.hpp lane-per-block kernels; 2t = 16 encodes with the solo image kernel
@@ -95,7 +98,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
         PPFS_LAUNCH((wg::rs_wg_encode_kernel<PPFS_T2, ENC_NBUF, ENC_WPC_STATIC, 3, 1, false>), dim3(rs_tile_grid(nb, ENC_WPC_STATIC)),
             dim3(256), 0, s, d, r, nb, tab);
 #elif PPFS_T2 == 32
-    PPFS_LAUNCH((bs::rs_bs_encode_kernel<PPFS_T2, BS_ENC_NW, 1>), dim3(rs_tile_grid(nb, 1, bs::TBW * BS_ENC_NW)),
+    PPFS_LAUNCH((bs::rs_bs_encode_kernel<PPFS_T2, BS_ENC_NW, PPFS_BS_ENC_NBUF>), dim3(rs_tile_grid(nb, 1, bs::TBW * BS_ENC_NW)),
         dim3(64 * BS_ENC_NW), 0, s, d, r, nb, tab);
 #else
     if constexpr (SOLO_IMG)
