@@ -67,6 +67,7 @@ def parse(argv=None):
     ap.add_argument("--cpu-faithful-blocks", type=int, default=1 << 18)
     ap.add_argument("--no-host-inclusive", dest="host_inclusive", action="store_false",
                     help="skip the H2D + kernel + D2H leg (rank 0, N=1)")
+    ap.add_argument("--host-reps", type=int, default=3, help="host_inclusive: calls per (mode, op); best reported")
     ap.add_argument("--dry-run-cpu", action="store_true", help="CPU stand-in for the engine (launcher tests)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal on a box with fewer GPUs than ranks: rank r uses GPU r %% count and the "
@@ -785,21 +786,25 @@ def main(argv=None):
             ctx = pinned(hd, hraw, hout, hst) if mode == "pinned" else None
             if ctx:
                 ctx.__enter__()
+            t_enc, t_dec, ok = [], [], True
+            pos = np.arange(nb) * n + (np.arange(nb) * 37) % n
             try:
                 eng.encode_host(hd, hraw)  # staging warm
-                t1 = time.perf_counter()
-                eng.encode_host(hd, hraw)
-                t2 = time.perf_counter()
-                hraw[np.arange(nb) * n + (np.arange(nb) * 37) % n] ^= 0x5A  # one error per block
-                t3 = time.perf_counter()
-                eng.decode_host(hraw, hout, hst, write_back=True)
-                t4 = time.perf_counter()
+                for _ in range(args.host_reps):  # best of host_reps: one ~20 ms call is at the mercy of the host
+                    t1 = time.perf_counter()
+                    eng.encode_host(hd, hraw)
+                    t_enc.append(time.perf_counter() - t1)
+                    hraw[pos] ^= 0x5A  # one error per block
+                    t1 = time.perf_counter()
+                    eng.decode_host(hraw, hout, hst, write_back=True)
+                    t_dec.append(time.perf_counter() - t1)
+                    ok = ok and bool(np.array_equal(hout, hd)) and int(hst.min()) == 1
             finally:
                 if ctx:
                     ctx.__exit__(None, None, None)
-            ok = bool(np.array_equal(hout, hd)) and int(hst.min()) == 1
-            host_incl[mode] = {"encode_GiBps": round(alg_launch / (t2 - t1) / GIB, 3),
-                               "decode_1err_GiBps": round(alg_launch / (t4 - t3) / GIB, 3), "verified": ok}
+            host_incl[mode] = {"encode_GiBps": round(alg_launch / min(t_enc) / GIB, 3),
+                               "decode_1err_GiBps": round(alg_launch / min(t_dec) / GIB, 3), "verified": ok,
+                               "reps": args.host_reps}
         host_incl["link"] = host_link_ceilings(dev, nb, k, n)
         lk = host_incl["link"]
         for mode in ("pageable", "pinned"):
@@ -809,8 +814,8 @@ def main(argv=None):
             host_incl[mode]["decode_1err_frac_of_link"] = round(host_incl[mode]["decode_1err_GiBps"]
                                                                 / lk["decode_1err_ceiling_GiBps"], 3)
         host_incl["note"] = ("ppfs_ecc_{encode,decode}_host over the same 2^20 blocks: H2D + kernel + D2H wall "
-                             "time, algorithmic bytes; never `value`; *_frac_of_link = rate / the same call's "
-                             "copies alone over page-locked memory (link)")
+                             "time (best of reps calls), algorithmic bytes; never `value`; *_frac_of_link = rate / "
+                             "the same call's copies alone over page-locked memory (link)")
 
     # (5) the other BASELINE configs (driver-visible per-config kernel rates): configs[3] Hamming and
     # CRC 0x9960034c at block_size 4096 and configs[4] RS(255,223), 2^20 blocks each, back-to-back

@@ -582,11 +582,21 @@ struct ppfs_ecc_ctx {
     // scratch for write_device status when the caller passes none
     uint8_t* d_scratch = nullptr;
     size_t scratch_bytes = 0;
-    // host staging
-    hipStream_t hs[2] = { nullptr, nullptr };
-    uint8_t* h_pin[2] = { nullptr, nullptr };
-    uint8_t* d_stage[2] = { nullptr, nullptr };
+    // host staging (round 5): a stream per link direction, so that chunk i + 1's H2D runs beside
+    // chunk i's D2H (with a stream per slot the slots fell into lockstep: both H2Ds, then both
+    // D2Hs, one link direction idle at a time); an event per slot orders its kernel after its H2D.
+    // hs[0]: H2D copies (SDMA), the small-batch path and decode write-back fix-ups; hs[1]: kernels
+    // and D2H copies (the runtime's D2H into page-locked memory is a blit kernel anyway).  Two, not
+    // one per stage: a process gets few hardware queues (GPU_MAX_HW_QUEUES, 4 by default) and
+    // streams beyond them share queues with torch's -- measured: 4 streams ran slower in bench.py's
+    // process than in a torch-free one
+    static constexpr int kSlots = 3, kHostStreams = 2;
+    hipStream_t hs[kHostStreams] = {};
+    hipEvent_t hev[kSlots][2] = {}; // per slot: inputs landed, outputs landed
+    uint8_t* h_pin[kSlots] = {};
+    uint8_t* d_stage[kSlots] = {};
     size_t stage_bytes = 0;
+    bool host_eager = false; // the last chunked decode's write-back predictor, where the next one starts
     // zero-copy staging for small host batches (the per-block IBlockDevice calls): coherent
     // host memory the kernels read and write in place, no H2D / D2H
     uint8_t* h_zc = nullptr;
@@ -782,6 +792,16 @@ int ev_slot(ppfs_ecc_ctx* c, hipStream_t s, bool create)
     return i;
 }
 
+// The context's own host-path streams -- compared only once they exist: before the host path first
+// runs they are null, which is also the default stream's handle.
+static bool own_stream(const ppfs_ecc_ctx* c, hipStream_t s)
+{
+    for (hipStream_t h : c->hs)
+        if (h && s == h)
+            return true;
+    return false;
+}
+
 // Before a device entry point queues work on caller stream s: order it after the last call queued
 // on the same handle.  For the same stream the runtime returns at once (an event recorded on the
 // waiting stream itself); it matters when s is a new stream created at the address of a destroyed
@@ -793,7 +813,7 @@ void order_caller_stream(ppfs_ecc_ctx* c, hipStream_t s)
         const char* v = std::getenv("PPFS_ECC_NO_ORDER");
         return v && *v && *v != '0';
     }();
-    if (off || (c->hs[0] && s == c->hs[0]) || (c->hs[1] && s == c->hs[1]) || capturing(s))
+    if (off || own_stream(c, s) || capturing(s))
         return;
     const int i = ev_slot(c, s, false);
     if (i >= 0 && c->ev_rec[i] && hipStreamWaitEvent(s, c->ev[i], 0) != hipSuccess)
@@ -880,7 +900,7 @@ void note_caller_stream(ppfs_ecc_ctx* c, hipStream_t s)
     // the context's own streams (destroy drains them) -- compared only once they exist: before the
     // host path first runs they are null, which is also the default stream's handle, and work on
     // the default stream must be tracked like any other caller stream's
-    if ((c->hs[0] && s == c->hs[0]) || (c->hs[1] && s == c->hs[1]) || capturing(s))
+    if (own_stream(c, s) || capturing(s))
         return;
     const int i = ev_slot(c, s, true);
     if (i < 0)
@@ -1089,9 +1109,9 @@ extern "C" void ppfs_ecc_destroy(ppfs_ecc_ctx* c)
     //  - only when more caller streams were used than there are event slots does destroy fall back
     //    to a device-wide synchronize.
     // Other contexts' resident servers and unrelated streams are not waited for.
-    for (int i = 0; i < 2; ++i)
-        if (c->hs[i])
-            (void)hipStreamSynchronize(c->hs[i]);
+    for (hipStream_t h : c->hs)
+        if (h)
+            (void)hipStreamSynchronize(h);
     for (int i = 0; i < c->ev_n; ++i) {
         (void)hipEventSynchronize(c->ev[i]);
         (void)hipEventDestroy(c->ev[i]);
@@ -1109,9 +1129,13 @@ extern "C" void ppfs_ecc_destroy(ppfs_ecc_ctx* c)
         c->h_box = nullptr;
     }
     // frees that never synchronize the device (mem_free, pin_free)
-    for (int i = 0; i < 2; ++i) {
-        if (c->hs[i])
-            (void)hipStreamDestroy(c->hs[i]);
+    for (hipStream_t h : c->hs)
+        if (h)
+            (void)hipStreamDestroy(h);
+    for (int i = 0; i < ppfs_ecc_ctx::kSlots; ++i) {
+        for (hipEvent_t e : c->hev[i])
+            if (e)
+                (void)hipEventDestroy(e);
         pin_free(c->h_pin[i], c->pin_bytes, kPinStage);
         mem_free(c, c->d_stage[i]);
     }
@@ -1402,25 +1426,29 @@ extern "C" const char* ppfs_ecc_stream_kernel_name(ppfs_ecc_ctx* c, void* stream
 }
 
 // ---------------------------------------------------------------------------------------
-// Host-memory paths: chunked, double-buffered pinned staging, H2D / kernel / D2H overlapped.
+// Host-memory paths: chunked, triple-buffered pinned staging, H2D / kernel / D2H overlapped.
 // ---------------------------------------------------------------------------------------
 static int ensure_staging(ppfs_ecc_ctx* c, size_t bytes)
 {
     if (c->stage_bytes >= bytes)
         return 0;
-    for (int i = 0; i < 2; ++i)
-        if (c->hs[i])
-            HIP_TRY(hipStreamSynchronize(c->hs[i]), "staging sync");
-    for (int i = 0; i < 2; ++i) {
+    for (hipStream_t h : c->hs)
+        if (h)
+            HIP_TRY(hipStreamSynchronize(h), "staging sync");
+    for (int i = 0; i < ppfs_ecc_ctx::kSlots; ++i) {
         pin_free(c->h_pin[i], c->pin_bytes, kPinStage);
         mem_free(c, c->d_stage[i]);
         c->h_pin[i] = nullptr;
         c->d_stage[i] = nullptr;
     }
     c->stage_bytes = c->pin_bytes = 0;
-    for (int i = 0; i < 2; ++i) {
-        if (!c->hs[i])
-            HIP_TRY(hipStreamCreateWithFlags(&c->hs[i], hipStreamNonBlocking), "stream");
+    for (hipStream_t& h : c->hs)
+        if (!h)
+            HIP_TRY(hipStreamCreateWithFlags(&h, hipStreamNonBlocking), "stream");
+    for (int i = 0; i < ppfs_ecc_ctx::kSlots; ++i) {
+        for (hipEvent_t& e : c->hev[i])
+            if (!e)
+                HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
         HIP_TRY(pin_alloc((void**)&c->h_pin[i], bytes, kPinStage), "pinned alloc");
         c->pin_bytes = bytes;
         HIP_TRY(mem_alloc(c, (void**)&c->d_stage[i], bytes), "stage alloc");
@@ -1846,9 +1874,9 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
     uint8_t* status, uint8_t* spill, size_t nblocks, int write_back);
 
 // A host call returns only once nothing it queued is still in flight: on an error part-way through
-// (a failed copy or launch in one slot) the other slot's H2D / kernel / D2H may still be running,
-// and its DMA targets the caller's buffers (direct mode) and the staging the next call reuses.
-// Both streams are drained before the error goes back; the first error's message is kept.
+// (a failed copy or launch in one slot) the other slots' H2D / kernel / D2H may still be running,
+// and their DMA targets the caller's buffers (direct mode) and the staging the next call reuses.
+// Every stream is drained before the error goes back; the first error's message is kept.
 static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t* data_out, uint8_t* raw,
     uint8_t* status, uint8_t* spill, size_t nblocks, int write_back)
 {
@@ -1865,9 +1893,9 @@ static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t*
         : host_run_chunks(c, op, data_in, data_out, raw, status, spill, nblocks, write_back);
     if (r) {
         const std::string msg = g_last_error;
-        for (int i = 0; i < 2; ++i)
-            if (c->hs[i])
-                (void)hipStreamSynchronize(c->hs[i]);
+        for (hipStream_t h : c->hs)
+            if (h)
+                (void)hipStreamSynchronize(h);
         g_last_error = msg;
     }
     return r;
@@ -1882,9 +1910,11 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
     if (r)
         return r;
     const size_t spill_b = 256 - std::min<size_t>(c->raw, 255);
-    size_t pending_first[2] = { 0, 0 }, pending_n[2] = { 0, 0 };
+    constexpr int NS = ppfs_ecc_ctx::kSlots;
+    hipStream_t s_in = c->hs[0], s_out = c->hs[1];
+    size_t pending_first[NS] = {}, pending_n[NS] = {};
     // fetched: the chunk's codewords already came back (staging, or the caller's page-locked image)
-    bool busy[2] = { false, false }, fetched[2] = { false, false };
+    bool busy[NS] = {}, fetched[NS] = {};
     // every caller buffer page-locked: DMA straight between it and the device staging buffers
     const bool direct = host_pinned(data_in, nblocks * c->data) && host_pinned(data_out, nblocks * c->data)
         && host_pinned(raw, nblocks * c->raw) && host_pinned(status, nblocks) && host_pinned(spill, nblocks * spill_b);
@@ -1893,12 +1923,16 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
     // (status 1), read from the chunk's status once it has landed
     const bool lazy_raw = op == OP_DECODE && write_back;
     // predictor: the last drained chunk changed many codewords -> fetch the next ones eagerly
-    // (queued behind the kernel, as encode does) instead of after the status has landed
-    bool eager = false;
+    // (queued behind the kernel, as encode does) instead of after the status has landed.  It starts
+    // where the context's previous call left it: the first kSlots chunks are queued before any has
+    // landed
+    bool eager = c->host_eager;
     auto fetch_changed = [&](int i, size_t b0, size_t nb) -> int {
         uint8_t* h = c->h_pin[i];
         uint8_t* d = c->d_stage[i];
-        hipStream_t s = c->hs[i];
+        // the chunk has landed (drain): its staging is idle until reused.  On the H2D stream, whose
+        // queue holds at most the next kSlots - 1 chunks' input copies; the other holds their kernels
+        hipStream_t s = s_in;
         const uint8_t* sts = (direct && status) ? status + b0 : h + L.status;
         uint32_t* ix = (uint32_t*)(h + L.idx);
         size_t nchg = 0;
@@ -1943,7 +1977,7 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
     auto drain = [&](int i) -> int {
         if (!busy[i])
             return 0;
-        HIP_TRY(hipStreamSynchronize(c->hs[i]), "sync");
+        HIP_TRY(hipEventSynchronize(c->hev[i][1]), "sync");
         const size_t b0 = pending_first[i], nb = pending_n[i];
         if (lazy_raw) {
             const int e = fetch_changed(i, b0, nb);
@@ -1967,14 +2001,17 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
         return 0;
     };
 
+    // a slot is reused only after drain() saw its outputs land: its H2D then never overwrites
+    // staging an earlier chunk's kernel or D2H still reads
     int slot = 0;
-    for (size_t b0 = 0; b0 < nblocks; b0 += chunk, slot ^= 1) {
+    for (size_t b0 = 0; b0 < nblocks; b0 += chunk, slot = (slot + 1) % NS) {
         const size_t nb = std::min(chunk, nblocks - b0);
         if ((r = drain(slot)))
             return r;
         uint8_t* h = c->h_pin[slot];
         uint8_t* d = c->d_stage[slot];
-        hipStream_t s = c->hs[slot];
+        hipEvent_t* ev = c->hev[slot];
+        hipStream_t s = s_in;
         // inputs host -> pinned -> device (data and raw regions are adjacent in the layout)
         const bool need_data = op == OP_ENCODE || op == OP_WRITE;
         const bool need_raw = op != OP_ENCODE || raw_is_rmw(c);
@@ -1993,6 +2030,9 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
             const size_t in_hi = need_raw ? L.raw + nb * c->raw : L.data + nb * c->data;
             HIP_TRY(dma_async(d + in_lo, h + in_lo, in_hi - in_lo, hipMemcpyHostToDevice, s), "H2D");
         }
+        HIP_TRY(hipEventRecord(ev[0], s_in), "event");
+        HIP_TRY(hipStreamWaitEvent(s_out, ev[0], 0), "wait");
+        s = s_out;
         switch (op) {
         case OP_ENCODE:
             r = ppfs_ecc_encode_device(c, d + L.data, d + L.raw, nb, s);
@@ -2033,13 +2073,17 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
             if (spill)
                 HIP_TRY(dma_async(o_sp, d + L.spill, nb * spill_b, hipMemcpyDeviceToHost, s), "D2H spill");
         }
+        HIP_TRY(hipEventRecord(ev[1], s_out), "event");
         pending_first[slot] = b0;
         pending_n[slot] = nb;
         busy[slot] = true;
     }
-    if ((r = drain(0)))
-        return r;
-    return drain(1);
+    for (int j = 0; j < NS; ++j) // oldest first
+        if ((r = drain((slot + j) % NS)))
+            return r;
+    if (lazy_raw)
+        c->host_eager = eager;
+    return 0;
 }
 
 extern "C" int ppfs_ecc_encode_host(ppfs_ecc_ctx* c, const uint8_t* data, uint8_t* raw, size_t nblocks)
