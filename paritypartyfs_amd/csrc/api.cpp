@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <functional>
 #include <cstdio>
 #include <map>
@@ -22,6 +23,7 @@
 #include <new>
 #include <string>
 #include <thread>
+#include <unistd.h>
 #include <vector>
 
 #include "../../include/ppfs_ecc.h"
@@ -1461,35 +1463,144 @@ namespace {
 constexpr size_t kChunkBlocks = 1u << 15; // 32 Ki blocks per chunk (~8 MiB of RS codewords)
 
 // Host staging copies of the pageable host path (caller buffer <-> page-locked staging): one CPU
-// thread moves ~10 GB/s, well under the PCIe rate the page-locked path reaches, so copies of
-// >= 2 MiB are split over PPFS_ECC_COPY_THREADS threads (default 4; 1 = single-threaded).
+// thread moves ~10 GB/s, well under the link rate the page-locked path reaches, so copies of
+// >= 2 MiB are split in 512 KiB pieces over PPFS_ECC_COPY_THREADS threads (default 8 -- the
+// calling thread and 7 pool workers; 1 = single-threaded).  The workers persist (a spawn per copy
+// cost ~10-20 us a thread), and one job carries every region of a chunk (payload and codewords).
 int copy_threads()
 {
     static const int n = [] {
         const char* e = std::getenv("PPFS_ECC_COPY_THREADS");
-        const int v = e ? std::atoi(e) : 4;
+        const int v = e ? std::atoi(e) : 8;
         return v < 1 ? 1 : (v > 16 ? 16 : v);
     }();
     return n;
 }
 
-void par_memcpy(void* dst, const void* src, size_t n)
+struct CopySeg {
+    void* dst;
+    const void* src;
+    size_t n;
+};
+
+class CopyPool {
+public:
+    static constexpr size_t kPiece = 512u << 10;
+    static constexpr int kMaxSegs = 4;
+
+    // one pool per process, its workers blocked on cv_ between jobs; leaked at exit (the workers
+    // never touch freed state).  A forked child starts its own (the parent's threads do not exist)
+    static CopyPool& get()
+    {
+        static std::mutex mu;
+        static CopyPool* pool = nullptr;
+        static pid_t owner = 0;
+        std::lock_guard<std::mutex> g(mu);
+        if (!pool || owner != getpid()) {
+            pool = new CopyPool(copy_threads() - 1);
+            owner = getpid();
+        }
+        return *pool;
+    }
+
+    void run(const CopySeg* segs, int nseg)
+    {
+        Job j;
+        for (int i = 0; i < nseg; ++i) {
+            j.seg[i] = segs[i];
+            j.first[i + 1] = j.first[i] + (segs[i].n + kPiece - 1) / kPiece;
+        }
+        j.nseg = nseg;
+        j.total = j.first[nseg];
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &j;
+            ++gen_;
+        }
+        cv_.notify_all();
+        work(j);
+        std::unique_lock<std::mutex> lk(m_);
+        if (job_ == &j) // late wakers find no job (concurrent callers: each one finishes its own job)
+            job_ = nullptr;
+        done_.wait(lk, [&] { return j.finished.load() == j.total && j.users == 0; });
+    }
+
+private:
+    struct Job {
+        CopySeg seg[kMaxSegs] {};
+        size_t first[kMaxSegs + 1] {}; // first piece of each segment
+        int nseg = 0;
+        size_t total = 0;
+        std::atomic<size_t> next { 0 }, finished { 0 };
+        int users = 0; // workers holding the job (guarded by m_)
+    };
+
+    explicit CopyPool(int workers)
+    {
+        for (int i = 0; i < workers; ++i)
+            std::thread([this] { loop(); }).detach();
+    }
+
+    void work(Job& j)
+    {
+        size_t done = 0;
+        for (size_t p; (p = j.next.fetch_add(1)) < j.total; ++done) {
+            int s = 0;
+            while (p >= j.first[s + 1])
+                ++s;
+            const size_t off = (p - j.first[s]) * kPiece;
+            const size_t len = std::min(kPiece, j.seg[s].n - off);
+            std::memcpy((uint8_t*)j.seg[s].dst + off, (const uint8_t*)j.seg[s].src + off, len);
+        }
+        if (done && j.finished.fetch_add(done) + done == j.total) {
+            std::lock_guard<std::mutex> g(m_);
+            done_.notify_all();
+        }
+    }
+
+    void loop()
+    {
+        uint64_t seen = 0;
+        for (;;) {
+            Job* j;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (!(j = job_))
+                    continue;
+                ++j->users;
+            }
+            work(*j);
+            std::lock_guard<std::mutex> g(m_);
+            if (--j->users == 0)
+                done_.notify_all();
+        }
+    }
+
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    uint64_t gen_ = 0;
+    Job* job_ = nullptr;
+};
+
+void par_memcpy_n(const CopySeg* segs, int nseg)
 {
-    const int nt = copy_threads();
-    if (nt == 1 || n < (2u << 20)) {
-        std::memcpy(dst, src, n);
+    size_t total = 0;
+    for (int i = 0; i < nseg; ++i)
+        total += segs[i].n;
+    if (copy_threads() == 1 || total < (2u << 20)) {
+        for (int i = 0; i < nseg; ++i)
+            std::memcpy(segs[i].dst, segs[i].src, segs[i].n);
         return;
     }
-    const size_t part = ((n + nt - 1) / nt + 4095) & ~(size_t)4095;
-    std::thread th[16];
-    int k = 0;
-    for (size_t off = part; off < n; off += part, ++k) {
-        const size_t len = std::min(part, n - off);
-        th[k] = std::thread([=] { std::memcpy((uint8_t*)dst + off, (const uint8_t*)src + off, len); });
-    }
-    std::memcpy(dst, src, std::min(part, n));
-    for (int i = 0; i < k; ++i)
-        th[i].join();
+    CopyPool::get().run(segs, nseg);
+}
+
+void par_memcpy(void* dst, const void* src, size_t n)
+{
+    const CopySeg s { dst, src, n };
+    par_memcpy_n(&s, 1);
 }
 
 struct Layout { // offsets inside one staging buffer
@@ -1989,10 +2100,13 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
             return 0;
         }
         uint8_t* h = c->h_pin[i];
+        CopySeg seg[2];
+        int ns = 0;
         if (op == OP_ENCODE || op == OP_WRITE)
-            par_memcpy(raw + b0 * c->raw, h + L.raw, nb * c->raw);
+            seg[ns++] = { raw + b0 * c->raw, h + L.raw, nb * c->raw };
         if (op == OP_DECODE && data_out)
-            par_memcpy(data_out + b0 * c->data, h + L.data, nb * c->data);
+            seg[ns++] = { data_out + b0 * c->data, h + L.data, nb * c->data };
+        par_memcpy_n(seg, ns);
         if (status)
             std::memcpy(status + b0, h + L.status, nb);
         if (spill)
@@ -2022,10 +2136,13 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
             if (need_raw)
                 HIP_TRY(dma_async(d + L.raw, raw + b0 * c->raw, nb * c->raw, hipMemcpyHostToDevice, s), "H2D raw");
         } else {
+            CopySeg seg[2];
+            int ns = 0;
             if (need_data)
-                par_memcpy(h + L.data, data_in + b0 * c->data, nb * c->data);
+                seg[ns++] = { h + L.data, data_in + b0 * c->data, nb * c->data };
             if (need_raw)
-                par_memcpy(h + L.raw, raw + b0 * c->raw, nb * c->raw);
+                seg[ns++] = { h + L.raw, raw + b0 * c->raw, nb * c->raw };
+            par_memcpy_n(seg, ns);
             const size_t in_lo = need_data ? L.data : L.raw;
             const size_t in_hi = need_raw ? L.raw + nb * c->raw : L.data + nb * c->data;
             HIP_TRY(dma_async(d + in_lo, h + in_lo, in_hi - in_lo, hipMemcpyHostToDevice, s), "H2D");
