@@ -120,14 +120,18 @@ extern "C" hipError_t ppfs_copy_launch(uint8_t* dst, const uint8_t* src, uint64_
 #ifndef PPFS_INJECT_NT
 #define PPFS_INJECT_NT 0 // ablation builds: non-temporal byte stores
 #endif
+#ifndef PPFS_INJECT_REV
+#define PPFS_INJECT_REV 0 // ablation builds: the first workgroups take the last blocks
+#endif
 namespace ppfs {
 template <int MODE>
 __global__ __launch_bounds__(256) void inject_kernel(uint8_t* __restrict__ raw, uint64_t stride, uint64_t nblocks,
     const uint8_t* __restrict__ pos, const uint8_t* __restrict__ val)
 {
-    const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, b0 = 4 * q;
-    if (b0 >= nblocks)
+    const uint64_t nq = (nblocks + 3) / 4, qi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (qi >= nq)
         return;
+    const uint64_t q = PPFS_INJECT_REV ? nq - 1 - qi : qi, b0 = 4 * q;
     uint32_t p4, v4;
     if (b0 + 4 <= nblocks && ((uintptr_t)(pos + b0) & 3u) == 0 && ((uintptr_t)(val + b0) & 3u) == 0) {
         p4 = *(const uint32_t*)(pos + b0);
