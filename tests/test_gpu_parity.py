@@ -496,7 +496,8 @@ def test_write_rmw_matches_oracle(oracle, codec):
 # host-memory path (pinned staging, several chunks)
 # ------------------------------------------------------------------------------------
 def test_host_path_multichunk(oracle):
-    bs, t, nb = 512, 3, 70001
+    # 5 chunks of 32 Ki blocks (the last one ragged): every staging slot is reused at least once
+    bs, t, nb = 512, 3, 4 * 32768 + 8001
     n, k, _ = oracle.rs_sizes(bs, t)
     eng = EccEngine(ECC_REED_SOLOMON, bs, t)
     rng = rng_for("host")
@@ -554,13 +555,17 @@ def test_host_path_pinned_equals_pageable(typ, bs, t, poly):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("prior", ["none", "eager"])
 @pytest.mark.parametrize("kind", ["pageable", "pinned"])
 @pytest.mark.parametrize("codec", ["rs512", "ham1024"])
-def test_host_decode_returns_only_changed_codewords(oracle, kind, codec):
+def test_host_decode_returns_only_changed_codewords(oracle, kind, codec, prior):
     """decode_host with write-back fetches codewords back only where the decode changed them
     (status 1): not at all for a clean chunk, as a packed gather for a few, as the whole range for
     many.  Chunks of 32 Ki blocks: clean / 100 errors / every block / 5,000 blocks / a short tail;
-    every path must leave the caller's image equal to the oracle's write-back."""
+    every path must leave the caller's image equal to the oracle's write-back.  prior="eager": the
+    context's previous call ended on a chunk where every block changed, so this call's first chunks
+    (queued before any has landed: api.cpp host_run_chunks, three staging slots) fetch their
+    codewords eagerly."""
     from paritypartyfs_amd import pinned
 
     ch = 1 << 15
@@ -590,6 +595,15 @@ def test_host_decode_returns_only_changed_codewords(oracle, kind, codec):
         o_data, o_st, o_fixed, _, _ = oracle.rs_decode(512, 3, bad)
     else:
         o_data, o_st, o_fixed, _ = oracle.ham_decode(1024, bad)
+    if prior == "eager":  # two chunks, every codeword corrupted: the predictor ends eager
+        pre = raw[: 2 * ch * n].reshape(2 * ch, n).copy()
+        if codec.startswith("rs"):
+            pre[:, 7] ^= 0x5A
+        else:
+            pre[:, 9] ^= 0x10
+        pre = pre.reshape(-1)
+        eng.decode_host(pre, None, np.zeros(2 * ch, np.uint8), write_back=True)
+        assert np.array_equal(pre, raw[: 2 * ch * n])
     img = bad.copy()
     out = np.zeros(nb * k, np.uint8)
     st = np.full(nb, 77, np.uint8)
