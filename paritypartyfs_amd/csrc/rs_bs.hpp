@@ -63,6 +63,18 @@ __device__ uint64_t g_bs_trace[4096 * BS_TRACE_N];
 #ifndef PPFS_BS_DEC_IDMA
 #define PPFS_BS_DEC_IDMA 0 // decode: next tile's DMA interleaved with the emission rounds
 #endif
+// Wave priorities (round 5): the waves of a CU alternate between the LDS-latency-bound chain and the
+// shorter correction / emission phases; raising a wave's priority (s_setprio 2) outside its chain lets
+// those phases issue ahead of the other waves' chain steps.  Decode: 1 = the correction, 2 = + the
+// emission (shipped: 1-error 131.9-135.3 vs 136.6-139.3 us on two boxes, r5q / r5r), 4 = everything
+// but the chain, 3 = static prio 1 for waves NW/2.. (no gain); 0 = off.  Encode: the emission and
+// the next tile's DMA (1, shipped; 0 = off).
+#ifndef PPFS_BS_PRIO
+#define PPFS_BS_PRIO 2
+#endif
+#ifndef PPFS_BS_EPRIO
+#define PPFS_BS_EPRIO 1
+#endif
 #ifndef PPFS_BS_EMIT_G
 #define PPFS_BS_EMIT_G 4 // decode emission: output pieces read from LDS together (4: +0.5 % cfg5 step, r3p)
 #endif
@@ -466,8 +478,12 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_encode_kernel(const uint8_t*
                 load_wave(pf, data + nx * (TBW * K), lane, src_off, dextent, nblocks * K);
         }
         first = false;
+        if constexpr (PPFS_BS_EPRIO)
+            __builtin_amdgcn_s_setprio(0);
         uint32_t s[4];
         bs_remainder<K>(s, lds, img + 255u * Ln.blk + (uint32_t)T2, Ln);
+        if constexpr (PPFS_BS_EPRIO)
+            __builtin_amdgcn_s_setprio(2);
         put_parity(lds, img, Ln, s);
         uint8_t* dst = raw + t * (TBW * 255);
 #pragma unroll
@@ -576,6 +592,9 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
         }
     }
     PPFS_BS_MARK(0);
+    if constexpr (PPFS_BS_PRIO == 3) // static priority for the second half of the waves (guide: s_setprio)
+        if (wave >= NW / 2)
+            __builtin_amdgcn_s_setprio(1);
     for (; t < nfull; t += S) {
         const uint64_t nx = t + S;
         if constexpr (NBUF == 0) {
@@ -585,18 +604,24 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         PPFS_BS_MARK(1);
+        if constexpr (PPFS_BS_PRIO == 4)
+            __builtin_amdgcn_s_setprio(0);
         uint32_t s[4];
         bs_cmodg(s, lds, row, Ln);
 #ifdef PPFS_TK_TRACE
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
         PPFS_BS_MARK(2);
+        if constexpr (PPFS_BS_PRIO == 1 || PPFS_BS_PRIO == 2 || PPFS_BS_PRIO == 4)
+            __builtin_amdgcn_s_setprio(2);
         const uint64_t gblk = t * TBW + Ln.blk;
         const uint32_t st = bs_correct<T2>(
             lds, gfp, s12p, xpm, row, Ln.c, s, true, raw, gblk, wb, nblocks * 255u PPFS_BS_TR_ARGS);
         if (status && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
             status[gblk] = (uint8_t)st;
         wave_fence(); // corrections patched into the image rows
+        if constexpr (PPFS_BS_PRIO == 1)
+            __builtin_amdgcn_s_setprio(0);
         PPFS_BS_MARK(6);
         // PPFS_BS_DEC_IDMA (NBUF = 1): the next tile's DMA windows go out between the emission's
         // rounds as soon as no later round reads them, so the DMA flies while the wave emits
@@ -633,6 +658,8 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
             }
         }
         PPFS_BS_MARK(7);
+        if constexpr (PPFS_BS_PRIO == 2)
+            __builtin_amdgcn_s_setprio(0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (nx < nfull && !idma) {
             if constexpr (NBUF == 0)

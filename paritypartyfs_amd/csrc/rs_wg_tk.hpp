@@ -384,6 +384,9 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
 // (taken at the top of iteration j - 1, read at the top of iteration j for the DMA one tile ahead).
 // Counter sets: the decode halves of the stream's pair (api.cpp ctr_for).
 // ------------------------------------------------------------------------------------
+#ifndef PPFS_TK_PRIO
+#define PPFS_TK_PRIO 0 // decode ablation: wave 0 at s_setprio 2 through the corrections
+#endif
 template <int T2, int WPC = 3, int NTST = 1>
 __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
     uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables, int write_back,
@@ -456,9 +459,13 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         barrier_lds(); // B: remainders complete
         PPFS_TK_MARK(3);
         if (wave == 0) {
+            if constexpr (PPFS_TK_PRIO)
+                __builtin_amdgcn_s_setprio(2); // the workgroup's other waves wait at barrier C for it
             const uint32_t st = phase_correct<T2>(lds, buf, par, row, true, raw, q0 * TB + row, wb, nblocks * 255u);
             if (status && PPFS_DBG_OK(status + q0 * TB + row, 1, status, nblocks))
                 status[q0 * TB + row] = (uint8_t)st;
+            if constexpr (PPFS_TK_PRIO)
+                __builtin_amdgcn_s_setprio(0);
         }
         barrier_lds(); // C: corrections patched into the LDS rows
         PPFS_TK_MARK(4);
