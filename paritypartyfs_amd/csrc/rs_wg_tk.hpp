@@ -183,6 +183,12 @@ template <int T2> __device__ __forceinline__ uint32_t sched_enc_src(uint32_t p)
     return (uint32_t)PAD + (255u - T2) * b + off - (uint32_t)T2;
 }
 
+// Every wave at s_setprio 2 from barrier B to its next remainder phase (emission, corrections, DMA
+// issue): with 2-3 workgroups per CU in different phases, the output side issues ahead of another
+// workgroup's remainder steps.  Round 5: step 4,508-4,509 vs 4,476-4,497 GiB/s (r5t); 0 = off.
+#ifndef PPFS_TK_EPRIO
+#define PPFS_TK_EPRIO 1
+#endif
 template <int T2, int WPC = 2, int NTST = 1>
 __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t* __restrict__ data,
     uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables, uint32_t* __restrict__ ctr,
@@ -290,9 +296,13 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
         PPFS_TK_MARK(1);
         if (wave == 0)
             *(uint64_t*)(lds + D::OFF_PAR + (pc ^ 1u) * 512u + 8u * lane) = 0;
+        if constexpr (PPFS_TK_EPRIO)
+            __builtin_amdgcn_s_setprio(0);
         phase_remainder<T2, K, D::NMAP, D::OFF_SLX, T5>(lds, buf, par, wave, row);
         PPFS_TK_MARK(2);
         barrier_lds(); // B: parity slots complete
+        if constexpr (PPFS_TK_EPRIO)
+            __builtin_amdgcn_s_setprio(2);
         PPFS_TK_MARK(3);
         if (tk_lane && iter)
             s_tk[(iter + 3u) & 3u] = (uint32_t)tk_tile(tk + 3u * g.gx, g, nfull); // the tile of iteration iter + 3
@@ -454,9 +464,13 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         PPFS_TK_MARK(1);
         if (wave == 0)
             *(uint64_t*)(lds + D::OFF_PAR + (pc ^ 1u) * 512u + 8u * lane) = 0;
+        if constexpr (PPFS_TK_EPRIO)
+            __builtin_amdgcn_s_setprio(0);
         phase_remainder<T2, 255, D::NMAP, D::OFF_SLX>(lds, buf, par, wave, row);
         PPFS_TK_MARK(2);
         barrier_lds(); // B: remainders complete
+        if constexpr (PPFS_TK_EPRIO)
+            __builtin_amdgcn_s_setprio(2);
         PPFS_TK_MARK(3);
         if (wave == 0) {
             if constexpr (PPFS_TK_PRIO)
