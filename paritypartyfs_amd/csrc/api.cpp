@@ -1023,7 +1023,7 @@ extern "C" int ppfs_ecc_create(const ppfs_ecc_params* params, int device, ppfs_e
         return fail(PPFS_ECC_EHIP, "hipSetDevice", e);
     }
     trace_step("create: device set");
-    if (c->rs_fast && c->rs_t2 <= 8) {
+    if (c->rs_fast && (c->rs_t2 <= 8 || c->rs_t2 == 32)) { // the ticket kernels (rs_wg_tk.hpp, rs_bs.hpp)
         const size_t cb = sizeof(uint32_t) * ppfs_ecc_ctx::kTkSlots * 2 * ppfs_ecc_ctx::kTkSetWords;
         e = mem_alloc(c, (void**)&c->d_ctr, cb);
         trace_step("create: counters allocated");
@@ -1418,7 +1418,7 @@ extern "C" const char* ppfs_ecc_stream_kernel_name(ppfs_ecc_ctx* c, void* stream
 {
     if (!c)
         return "";
-    if (c->d_ctr) { // 2t <= 8: ticket kernels while the stream has (or can get) a counter set
+    if (c->d_ctr && c->rs_t2 <= 8) { // 2t <= 8: ticket kernels while the stream has (or can get) a counter set
         const hipStream_t s = (hipStream_t)stream;
         const bool evok = ev_slot(c, s, false) >= 0 || c->ev_n < ppfs_ecc_ctx::kEvSlots;
         if (!evok || tk_slot(c, s, false) < 0)

@@ -24,6 +24,7 @@
 #include <stdint.h>
 
 #include "rs_pair.hpp"
+#include "rs_wg_tk.hpp" // tk_geom / tk_clear: the per-XCD ticket counters
 
 namespace ppfs {
 namespace bs {
@@ -41,7 +42,7 @@ using wg::st_nt;
 // g_bs_trace (prologue, DMA wait, c mod g, S1/S2 + logs, XP row + confirmation, fix / general path,
 // status, emission, image-free wait + next DMA, iterations, end), read by ppfs_bs_trace_read.
 #ifdef PPFS_TK_TRACE
-constexpr int BS_TRACE_N = 11;
+constexpr int BS_TRACE_N = 13; // + the wave's start / end on the 100 MHz s_memrealtime clock
 __device__ uint64_t g_bs_trace[4096 * BS_TRACE_N];
 #define PPFS_BS_MARK(i)                                                                                                \
     do {                                                                                                               \
@@ -416,13 +417,65 @@ template <int NW, int NBUF, bool DEC, int TLDS = 0> struct BsLds {
     static_assert(OFF_IMG % 16 == 0 && IMGW % 16 == 0, "aligned images");
 };
 
+// Tile walk of one wave (round 5).  Static (ctr null, or graph capture): tiles w, w + S, w + 2 S, ...
+// (S = the grid's waves).  With a counter set (api.cpp ctr_for) the waves of an XCD take tiles by
+// ticket, as rs_wg_tk.hpp's workgroups do: local ticket j is tile j nx + xc; a wave's first two tiles
+// are static (its rank r among the XCD's G waves, then r + G), later ones come from the XCD's counter
+// (one ticket per iteration, for the iteration after next, so its latency hides behind a whole
+// tile).  On the static walk the waves of one CU finished up to ~14 us apart (median spread; the
+// decode's span 134 us, median wave end 122 us: tools/bs_trace.py realtime, r5w), the tickets let the
+// fast ones take more.  A wave's tiles increase: it stops at its first tile past the batch, and the
+// one wave that draws tile nfull takes the partial tile.
+struct BsWalk {
+    uint64_t t, nx; // this iteration's tile, the next one
+    uint64_t S, base;
+    uint32_t* my; // this XCD's counter, or null: static
+    uint32_t nxc, xc;
+    __device__ __forceinline__ BsWalk(uint32_t* ctr, uint32_t* ctr_clear, uint32_t wave, uint32_t lane, uint32_t nw)
+    {
+        S = (uint64_t)gridDim.x * nw;
+        my = nullptr;
+        nxc = xc = 0;
+        base = 0;
+        if (ctr && ctr_clear) {
+            const wg::TkGeom g = wg::tk_geom();
+            const uint64_t G = (uint64_t)g.gx * nw, r = (uint64_t)g.rank * nw + wave;
+            my = ctr + 32u * g.xc;
+            nxc = g.nx;
+            xc = g.xc;
+            base = 2 * G;
+            t = r * nxc + xc;
+            nx = (r + G) * nxc + xc;
+            if (blockIdx.x == 0 && wave == 0 && lane == 0)
+                wg::tk_clear(ctr_clear);
+        } else {
+            t = (uint64_t)blockIdx.x * nw + wave;
+            nx = t + S;
+        }
+    }
+    // lane 0: the ticket of the iteration after next (other lanes: 0)
+    __device__ __forceinline__ uint32_t take(uint32_t lane) const
+    {
+        uint32_t tk = 0;
+        if (my && lane == 0)
+            tk = atomicInc(my, 0xFFFFFFFFu);
+        return tk;
+    }
+    __device__ __forceinline__ void advance(uint32_t tk)
+    {
+        t = nx;
+        nx = my ? (base + (uint64_t)__builtin_amdgcn_readfirstlane(tk)) * nxc + xc : nx + S;
+    }
+};
+
 // Encode: 2^k payloads -> codewords.  Workgroup b's wave w takes wave tiles b NW + w + j S
 // (S = grid NW).  NBUF = 1: a wave DMAs its next tile once its emission has read the image;
 // NBUF = 2: the next tile is DMA'd at the top of the iteration into the other buffer; NBUF = 0:
 // register prefetch (load_wave / put_wave).
 template <int T2, int NW, int NBUF, int NTST = 1>
 __global__ __launch_bounds__(64 * NW, 1) void rs_bs_encode_kernel(const uint8_t* __restrict__ data,
-    uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables)
+    uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables, uint32_t* __restrict__ ctr,
+    uint32_t* __restrict__ ctr_clear)
 {
     static_assert(T2 == 32, "byte-slice path: 2t = 32 (image pieces need 16 | 2t, state byte q = coefficient q)");
     static_assert(NBUF >= 0 && NBUF <= 2, "NBUF");
@@ -438,8 +491,9 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_encode_kernel(const uint8_t*
     const uint32_t img0 = D::OFF_IMG + wave * (uint32_t)((NBUF > 0 ? NBUF : 1) * IMGW);
     const uint32_t base0 = __builtin_amdgcn_readfirstlane(lds_addr(lds + img0));
     const uint64_t nfull = nblocks / TBW, ntiles = (nblocks + TBW - 1) / TBW;
-    const uint64_t S = (uint64_t)gridDim.x * NW;
-    uint64_t t = (uint64_t)blockIdx.x * NW + wave;
+    // tickets only for the shipped single-image form (NBUF = 2 counts its vmcnt exactly)
+    BsWalk wk(NBUF == 1 ? ctr : nullptr, ctr_clear, wave, lane, NW);
+    uint64_t t = wk.t;
     auto src_off = [](uint32_t i) { return pair::img_src<T2>(i); };
     const uint8_t* const dextent = data;
     [[maybe_unused]] u32x4 pf[KP];
@@ -453,8 +507,9 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_encode_kernel(const uint8_t*
     }
     uint32_t cur = 0;
     bool first = true;
-    for (; t < nfull; t += S) {
-        const uint64_t nx = t + S;
+    uint32_t tk_next = 0;
+    for (; t < nfull; wk.advance(tk_next), t = wk.t) {
+        const uint64_t nx = wk.nx;
         const uint32_t img = img0 + cur * IMGW;
         if constexpr (NBUF == 2) {
             // the other buffer's emission reads finished in the previous iteration (its stores
@@ -473,6 +528,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_encode_kernel(const uint8_t*
             }
         } else if constexpr (NBUF == 1) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            tk_next = wk.take(lane); // after the wait: the next top's vmcnt(0) finds it long done
         } else {
             if (nx < nfull)
                 load_wave(pf, data + nx * (TBW * K), lane, src_off, dextent, nblocks * K);
@@ -543,7 +599,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_encode_kernel(const uint8_t*
 template <int T2, int NW, int NBUF = 1, int NTST = 1, int TLDS = 0>
 __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __restrict__ raw,
     uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables,
-    int write_back)
+    int write_back, uint32_t* __restrict__ ctr, uint32_t* __restrict__ ctr_clear)
 {
     static_assert(T2 == 32, "byte-slice path: 2t = 32");
     using L = RsPairLayout<T2>;
@@ -567,6 +623,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
     __syncthreads();
 #ifdef PPFS_TK_TRACE
     uint64_t tr_[BS_TRACE_N] = {};
+    tr_[11] = __builtin_amdgcn_s_memrealtime();
     uint64_t tlast_ = clock64();
     const uint64_t t0_ = tlast_;
 #endif
@@ -579,8 +636,8 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
     const uint32_t row = img + 255u * Ln.blk;
     const uint8_t* const xpm = D::XP_IN ? lds + D::OFF_XP : tables + L::OFF_XPM;
     const uint64_t nfull = nblocks / TBW, ntiles = (nblocks + TBW - 1) / TBW;
-    const uint64_t S = (uint64_t)gridDim.x * NW;
-    uint64_t t = (uint64_t)blockIdx.x * NW + wave;
+    BsWalk wk(ctr, ctr_clear, wave, lane, NW);
+    uint64_t t = wk.t;
     auto src_off = [](uint32_t i) { return (int)(16u * i); };
     [[maybe_unused]] u32x4 pf[KP];
     if (t < nfull) {
@@ -595,13 +652,16 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
     if constexpr (PPFS_BS_PRIO == 3) // static priority for the second half of the waves (guide: s_setprio)
         if (wave >= NW / 2)
             __builtin_amdgcn_s_setprio(1);
-    for (; t < nfull; t += S) {
-        const uint64_t nx = t + S;
+    uint32_t tk_next = 0;
+    for (; t < nfull; wk.advance(tk_next), t = wk.t) {
+        const uint64_t nx = wk.nx;
         if constexpr (NBUF == 0) {
+            tk_next = wk.take(lane); // needed at the iteration's end: a whole tile covers it
             if (nx < nfull)
                 load_wave(pf, raw + nx * (TBW * 255), lane, src_off, raw, nblocks * 255u);
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            tk_next = wk.take(lane);
         }
         PPFS_BS_MARK(1);
         if constexpr (PPFS_BS_PRIO == 4)
@@ -706,6 +766,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
     }
 #ifdef PPFS_TK_TRACE
     tr_[10] = clock64() - t0_;
+    tr_[12] = __builtin_amdgcn_s_memrealtime();
     const uint32_t gw = blockIdx.x * NW + wave;
     if (lane == 0 && gw < 4096)
         for (int i = 0; i < BS_TRACE_N; ++i)

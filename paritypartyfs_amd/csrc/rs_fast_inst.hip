@@ -70,6 +70,9 @@ constexpr int ENC_WPC_STATIC = fit_wpc(wg::lds_bytes<PPFS_T2, false, ENC_NBUF>()
 #ifndef PPFS_BS_ENC_NBUF
 #define PPFS_BS_ENC_NBUF 1 // single LDS image, the next tile's DMA after the emission; 0 = register prefetch
 #endif
+#ifndef PPFS_BS_TICKETS
+#define PPFS_BS_TICKETS 1 // round 5: waves take their tiles by per-XCD ticket (rs_bs.hpp BsWalk); 0 = static walk
+#endif
 constexpr int BS_ENC_NW = 12, BS_DEC_NW = PPFS_BS_DEC_NW, BS_DEC_TLDS = PPFS_BS_DEC_TLDS, BS_DEC_NBUF = PPFS_BS_DEC_NBUF;
 #else
 // 8 < 2t <= 16: rs_fast.hpp lane-per-block kernels; 2t = 16 encodes with the solo image kernel
@@ -99,7 +102,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
             dim3(256), 0, s, d, r, nb, tab);
 #elif PPFS_T2 == 32
     PPFS_LAUNCH((bs::rs_bs_encode_kernel<PPFS_T2, BS_ENC_NW, PPFS_BS_ENC_NBUF>), dim3(rs_tile_grid(nb, 1, bs::TBW * BS_ENC_NW)),
-        dim3(64 * BS_ENC_NW), 0, s, d, r, nb, tab);
+        dim3(64 * BS_ENC_NW), 0, s, d, r, nb, tab, PPFS_BS_TICKETS ? ctr : nullptr, ctr_clear);
 #else
     if constexpr (SOLO_IMG)
         PPFS_LAUNCH((pair::rs_solo_encode_img_kernel<PPFS_T2, SOLO_WPC, SOLO_NW>),
@@ -135,7 +138,8 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
             dim3(256), 0, s, r, d, st, nb, tab, wb);
 #elif PPFS_T2 == 32
     PPFS_LAUNCH((bs::rs_bs_decode_kernel<PPFS_T2, BS_DEC_NW, BS_DEC_NBUF, 1, BS_DEC_TLDS>),
-        dim3(rs_tile_grid(nb, 1, bs::TBW * BS_DEC_NW)), dim3(64 * BS_DEC_NW), 0, s, r, d, st, nb, tab, wb);
+        dim3(rs_tile_grid(nb, 1, bs::TBW * BS_DEC_NW)), dim3(64 * BS_DEC_NW), 0, s, r, d, st, nb, tab, wb,
+        PPFS_BS_TICKETS ? ctr : nullptr, ctr_clear);
 #else
     PPFS_LAUNCH(rs255_decode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, r, d, st, nb, tab, wb);
 #endif

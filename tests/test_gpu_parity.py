@@ -177,13 +177,14 @@ def test_rs_ragged_tiles(oracle, bs, t):
         assert np.array_equal(host(raw_d), o_fixed), nb
 
 
-def test_rs_ticket_sets_after_a_small_launch(oracle):
+@pytest.mark.parametrize("bs,t", [(512, 3), (4096, 16)], ids=["t3", "t16"])
+def test_rs_ticket_sets_after_a_small_launch(oracle, bs, t):
     """One engine, one stream: a large batch (8 XCD ticket counters), then batches of fewer than 8
     tiles (a grid of < 8 workgroups counts on fewer counters and used to zero only those of the
     set the large launch left dirty), then large again -- encode and decode, each vs the oracle.  A
     stale counter would start the second large launch's tickets past tiles nobody then encodes
-    (rs_wg_tk.hpp tk_clear)."""
-    bs, t = 512, 3
+    (rs_wg_tk.hpp tk_clear).  t = 16: the byte-slice kernels' per-wave tickets (round 5,
+    rs_bs.hpp BsWalk) on the same counter sets."""
     n, k, _ = oracle.rs_sizes(bs, t)
     eng = EccEngine(ECC_REED_SOLOMON, bs, t)
     for step, nb in enumerate([3 * 768 * 64 + 11, 448, 100, 7, 3 * 768 * 64 + 11, 1 << 16, 130, 1 << 16]):

@@ -292,7 +292,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
 #elif PPFS_T2 > 16
     if constexpr (PAIR_BS)
         hipLaunchKernelGGL((bs::rs_bs_encode_kernel<PPFS_T2, PPFS_BS_ENC_NW, PPFS_BS_ENC_NBUF>),
-            dim3(rs_tile_grid(nb, 1, bs::TBW * PPFS_BS_ENC_NW)), dim3(64 * PPFS_BS_ENC_NW), 0, s, d, r, nb, tab);
+            dim3(rs_tile_grid(nb, 1, bs::TBW * PPFS_BS_ENC_NW)), dim3(64 * PPFS_BS_ENC_NW), 0, s, d, r, nb, tab, nullptr, nullptr);
     else if constexpr (PAIR_IMG)
         hipLaunchKernelGGL((pair::rs_pair_encode_img_kernel<PPFS_T2, PPFS_PAIR_IMG_WPC, PPFS_PAIR_IMG_NW>),
             dim3(rs_tile_grid(nb, PAIR_ENC_WPC, 32 * PPFS_PAIR_IMG_NW)), dim3(64 * PPFS_PAIR_IMG_NW), 0, s, d, r, nb, tab);
@@ -350,7 +350,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
 #elif PPFS_T2 > 16
     if constexpr (PAIR_BS)
         hipLaunchKernelGGL((bs::rs_bs_decode_kernel<PPFS_T2, PPFS_BS_NW, PPFS_BS_DEC_NBUF, PPFS_BS_DEC_NTST>), dim3(rs_tile_grid(nb, 1, bs::TBW * PPFS_BS_NW)),
-            dim3(64 * PPFS_BS_NW), 0, s, r, d, st, nb, tab, wb);
+            dim3(64 * PPFS_BS_NW), 0, s, r, d, st, nb, tab, wb, nullptr, nullptr);
     else
     hipLaunchKernelGGL((pair::rs_pair_decode_kernel<PPFS_T2, PPFS_PAIR_DEC>),
         dim3(rs_tile_grid(nb, PPFS_PAIR_DEC_FULL ? (1 << 24) : PAIR_DEC_WPC)),

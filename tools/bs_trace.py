@@ -20,7 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 PHASES = ["prologue", "dma_wait", "cmodg", "s12_logs", "xp_confirm", "fix", "status", "emission", "free_dma"]
-N = 11
+N = 13
 
 
 def main():
@@ -67,13 +67,27 @@ def main():
     buf = np.zeros(4096 * N, np.uint64)
     assert fn(buf.ctypes.data, buf.nbytes) == 0
     tr = buf.reshape(4096, N)
-    tr = tr[tr[:, 10] > 0].astype(np.float64)
+    gw = np.nonzero(tr[:, 10] > 0)[0]  # wave index blockIdx * NW + wave (NW = 8)
+    tr = tr[tr[:, 10] > 0]
+    t0, t1 = tr[:, 11].astype(np.int64), tr[:, 12].astype(np.int64)  # 100 MHz realtime, per wave
+    base = t0.min()
+    xcd = (gw // 8) % 8  # workgroups go round-robin over the 8 XCDs
+    per_xcd = {int(x): [round(float(np.percentile(t1[xcd == x] - base, q)) / 100.0, 1) for q in (0, 50, 100)]
+               for x in range(8)}
+    cu = gw // 8
+    per_cu_spread = np.array([(t1[cu == c].max() - t1[cu == c].min()) / 100.0 for c in np.unique(cu)])
+    tail = {"span_us": round((t1.max() - base) / 100.0, 2), "start_spread_us": round((t0.max() - base) / 100.0, 2),
+            "end_us": {q: round(float(np.percentile(t1 - base, q)) / 100.0, 2) for q in (0, 10, 50, 90, 100)},
+            "end_us_by_xcd_min_med_max": per_xcd,
+            "within_cu_end_spread_us_median": round(float(np.median(per_cu_spread)), 2)}
+    tr = tr.astype(np.float64)
     tot = tr[:, 10].mean()
     iters = tr[:, 9].sum()
     res = {"blocks": nb, "mode": "clean" if a.clean else "1-error", "waves": len(tr), "total_cycles": round(tot),
            "tiles_per_wave": round(tr[:, 9].mean(), 2),
            "share": {p: round(tr[:, i].mean() / tot, 3) for i, p in enumerate(PHASES)},
-           "per_tile": {p: round(tr[:, i].sum() / max(1.0, iters)) for i, p in enumerate(PHASES) if i > 0}}
+           "per_tile": {p: round(tr[:, i].sum() / max(1.0, iters)) for i, p in enumerate(PHASES) if i > 0},
+           "realtime": tail}
     print(json.dumps(res), flush=True)
 
 
