@@ -98,10 +98,17 @@ __device__ __forceinline__ void dma_tables_w0(uint8_t* dst, const uint8_t* __res
 struct TkGeom {
     uint32_t nx, xc, gx, rank;
 };
+// PPFS_TK_NX (ablation): counters per launch; 1 = one chip-wide counter -- its atomics serialize at
+// ~80 per us and both t = 3 kernels ran 2x slower, 2 counters +18 % (r5za).  Round 5 also measured
+// cross-XCD stealing (a workgroup whose counter runs dry draws the next XCD's): no gain, the slow
+// XCD's lag sits in its workgroups' already-drawn lookahead tiles (r5zb-r5zd).
+#ifndef PPFS_TK_NX
+#define PPFS_TK_NX 8
+#endif
 __device__ __forceinline__ TkGeom tk_geom()
 {
     TkGeom g;
-    g.nx = gridDim.x < 8u ? gridDim.x : 8u;
+    g.nx = gridDim.x < (uint32_t)PPFS_TK_NX ? gridDim.x : (uint32_t)PPFS_TK_NX;
     g.xc = blockIdx.x % g.nx;
     g.gx = (gridDim.x - g.xc + g.nx - 1u) / g.nx;
     g.rank = blockIdx.x / g.nx;
@@ -127,7 +134,8 @@ __device__ __forceinline__ void tk_clear(uint32_t* __restrict__ ctr_clear)
 // and 1 of every encode workgroup sum s_memtime cycles per loop phase into g_tk_trace, read back by
 // ppfs_tk_trace_read_t<2t> (tools/tk_trace.py).  Normal builds: nothing.
 #ifdef PPFS_TK_TRACE
-constexpr int TK_TRACE_N = 10; // prologue, issue, remainder, barrier B, emission, vm wait, barrier A, epilogue, iterations, end
+constexpr int TK_TRACE_N = 12; // prologue, issue, remainder, barrier B, emission, vm wait, barrier A, epilogue, iterations, end,
+// the workgroup's start and end on the 100 MHz s_memrealtime clock
 __device__ uint64_t g_tk_trace[4096 * 2 * TK_TRACE_N];
 // decode: prologue, issue, remainder, barrier B, correction (+ barrier C), emission, vm wait, barrier A,
 // iterations, end
@@ -222,6 +230,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
     uint32_t* const my_ctr = ctr + 32u * g.xc; // 128-byte lines
 #ifdef PPFS_TK_TRACE
     uint64_t tr_[TK_TRACE_N] = {};
+    tr_[10] = __builtin_amdgcn_s_memrealtime();
     uint64_t tlast_ = clock64();
     const uint64_t t0_ = tlast_;
 #endif
@@ -381,6 +390,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
     PPFS_TK_MARK(7);
     tr_[8] = iter;
     tr_[9] = clock64() - t0_;
+    tr_[11] = __builtin_amdgcn_s_memrealtime();
     if (wave < 2 && lane == 0 && blockIdx.x < 4096)
         for (int i = 0; i < TK_TRACE_N; ++i)
             g_tk_trace[(blockIdx.x * 2 + wave) * TK_TRACE_N + i] = tr_[i];
@@ -423,6 +433,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
     uint32_t* const my_ctr = ctr + 32u * g.xc;
 #ifdef PPFS_TK_TRACE
     uint64_t tr_[TK_TRACE_N] = {};
+    tr_[10] = __builtin_amdgcn_s_memrealtime();
     uint64_t tlast_ = clock64();
     const uint64_t t0_ = tlast_;
 #endif
@@ -544,6 +555,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     tr_[8] = iter;
     tr_[9] = clock64() - t0_;
+    tr_[11] = __builtin_amdgcn_s_memrealtime();
     if (wave < 2 && lane == 0 && blockIdx.x < 4096)
         for (int i = 0; i < TK_TRACE_N; ++i)
             g_tk_trace_dec[(blockIdx.x * 2 + wave) * TK_TRACE_N + i] = tr_[i];

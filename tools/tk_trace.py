@@ -21,7 +21,7 @@ sys.path.insert(0, ROOT)
 
 PHASES = ["prologue", "issue", "remainder", "barrier_B", "emission", "vm_wait", "barrier_A", "epilogue"]
 PHASES_DEC = ["prologue", "issue", "remainder", "barrier_B", "correction", "emission", "vm_wait", "barrier_A"]
-N = 10
+N = 12
 
 
 def main():
@@ -84,6 +84,14 @@ def main():
                          "share": {p: round(t[:, i].mean() / tot, 3) for i, p in enumerate(phases)},
                          "per_iter": {p: round(t[:, i].sum() / max(1.0, t[:, 8].sum())) for i, p in enumerate(phases)
                                       if i > 0}}
+        # workgroup ends on the realtime clock (wave 0's stamp): the tail
+        t0, t1 = buf.reshape(4096, 2, N)[:grid, 0, 10].astype(np.int64), buf.reshape(4096, 2, N)[:grid, 0, 11].astype(np.int64)
+        base = t0.min()
+        xcd = np.arange(grid) % 8
+        out["realtime"] = {"span_us": round((t1.max() - base) / 100.0, 2),
+                           "end_us": {q: round(float(np.percentile(t1 - base, q)) / 100.0, 2) for q in (0, 10, 50, 90, 100)},
+                           "end_us_by_xcd_min_med_max": {int(x): [round(float(np.percentile(t1[xcd == x] - base, q)) / 100.0, 1)
+                                                             for q in (0, 50, 100)] for x in range(8)}}
         res[key] = out
 
     read("ppfs_tk_trace_read_t6", 2, PHASES, "encode")
