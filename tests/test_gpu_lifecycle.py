@@ -129,30 +129,33 @@ def test_destroy_waits_for_work_on_every_caller_stream(oracle):
         assert np.array_equal(o.cpu().numpy(), cw)
 
 
-def _capture(eng, data, cw, out, st, nb):
+def _capture(eng, data, cw, out, st, nb, static=STATIC):
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
-        assert eng.stream_kernel_name() == STATIC  # no ticket set inside a capture
+        assert eng.stream_kernel_name() == static  # no ticket set inside a capture
         eng.encode(data, cw, nblocks=nb)
         eng.decode(cw, out, st, write_back=True, nblocks=nb)
     return g
 
 
-def test_graph_replays_on_two_streams_at_once(oracle):
+@pytest.mark.parametrize("bs,t,kname,static", [(512, 3, "rs255-wg-tk-lds", STATIC),
+                                               (4096, 16, "rs255-bs-byte-lds", "rs255-bs-byte-lds")], ids=["t3", "t16"])
+def test_graph_replays_on_two_streams_at_once(oracle, bs, t, kname, static):
     """Two graphs of encode + decode (each its own buffers) replayed concurrently on two streams,
     and one replayed beside eager launches on its capture's stream: bit-exact every time.  With the
     capture stream's ticket set baked into the graphs, the concurrent replays would share counters
-    and skip or repeat tiles."""
+    and skip or repeat tiles.  t = 16: the byte-slice kernels' per-wave tickets (round 5) take the
+    static walk inside a capture the same way (the kernel name does not change for them)."""
     nb = (1 << 18) + 5
-    n, k, data, cw = _rs_batch(oracle, nb, 34)
-    eng = EccEngine(ECC_REED_SOLOMON, 512, 3)
-    assert eng.kernel_name == "rs255-wg-tk-lds"
+    n, k, data, cw = _rs_batch(oracle, nb, 34, bs, t)
+    eng = EccEngine(ECC_REED_SOLOMON, bs, t)
+    assert eng.kernel_name == kname
     d = torch.from_numpy(data).cuda()
     bufs = [(torch.zeros(nb * n, dtype=torch.uint8, device="cuda"), torch.zeros(nb * k, dtype=torch.uint8, device="cuda"),
              torch.zeros(nb, dtype=torch.uint8, device="cuda")) for _ in range(3)]
     eng.encode(d, bufs[0][0], nblocks=nb)  # eager first: loads the kernels
     torch.cuda.synchronize()
-    graphs = [_capture(eng, d, c, o, s, nb) for c, o, s in bufs[:2]]
+    graphs = [_capture(eng, d, c, o, s, nb, static) for c, o, s in bufs[:2]]
     sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
     want_cw = torch.from_numpy(cw).cuda()
     for _ in range(3):
@@ -170,7 +173,7 @@ def test_graph_replays_on_two_streams_at_once(oracle):
             assert torch.equal(c, want_cw)
             assert torch.equal(o, d)
             assert int(s.max()) == 0
-    assert eng.stream_kernel_name() == "rs255-wg-tk-lds"  # outside a capture: ticket kernels again
+    assert eng.stream_kernel_name() == kname  # outside a capture: ticket kernels again
     del graphs
     eng.close()
 
