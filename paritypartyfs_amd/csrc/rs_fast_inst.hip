@@ -53,6 +53,9 @@ static uint32_t rs_tile_grid(uint64_t nb, int wpc, int tb = 64)
 // The static-walk encode fits as many workgroups as its LDS allows (at most 4); the ticket encode
 // runs 2 per CU (its LDS carries the ticket slots).
 constexpr int fit_wpc(int bytes, int most) { return 163840 / bytes < most ? 163840 / bytes : most; }
+#ifndef PPFS_TK_NTST
+#define PPFS_TK_NTST 1 // ticket kernels' output stores: 1 non-temporal, 0 plain (ablation)
+#endif
 constexpr int ENC_NBUF = 3, ENC_WPC = 2, DEC_NBUF = 2, DEC_WPC = 3;
 constexpr int ENC_WPC_STATIC = fit_wpc(wg::lds_bytes<PPFS_T2, false, ENC_NBUF>(), 4);
 #elif PPFS_T2 == 32
@@ -95,7 +98,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
 {
 #if PPFS_T2 <= 8
     if (ctr && ctr_clear)
-        PPFS_LAUNCH((wg::rs_wg_encode_tk_kernel<PPFS_T2, ENC_WPC, 1>), dim3(rs_tile_grid(nb, ENC_WPC)), dim3(256), 0, s,
+        PPFS_LAUNCH((wg::rs_wg_encode_tk_kernel<PPFS_T2, ENC_WPC, PPFS_TK_NTST>), dim3(rs_tile_grid(nb, ENC_WPC)), dim3(256), 0, s,
             d, r, nb, tab, ctr, ctr_clear);
     else
         PPFS_LAUNCH((wg::rs_wg_encode_kernel<PPFS_T2, ENC_NBUF, ENC_WPC_STATIC, 3, 1, false>), dim3(rs_tile_grid(nb, ENC_WPC_STATIC)),
@@ -131,7 +134,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
 {
 #if PPFS_T2 <= 8
     if (ctr && ctr_clear)
-        PPFS_LAUNCH((wg::rs_wg_decode_tk_kernel<PPFS_T2, DEC_WPC, 1>), dim3(rs_tile_grid(nb, DEC_WPC)), dim3(256), 0, s,
+        PPFS_LAUNCH((wg::rs_wg_decode_tk_kernel<PPFS_T2, DEC_WPC, PPFS_TK_NTST>), dim3(rs_tile_grid(nb, DEC_WPC)), dim3(256), 0, s,
             r, d, st, nb, tab, wb, ctr, ctr_clear);
     else
         PPFS_LAUNCH((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC, 7, 1>), dim3(rs_tile_grid(nb, DEC_WPC)),

@@ -424,9 +424,21 @@ template <int T2> __device__ __forceinline__ uint4 dec_piece(const uint8_t* lds,
     return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+// PPFS_ST_POLICY (ablation): the cache policy of the NT = 1 output stores -- 1: non-temporal
+// (the builtin), 2: nt sc1, 3: sc0 sc1 (system scope), 4: nt sc0 sc1 (inline asm; the explicit
+// vmcnt counts in the kernels count these stores the same way)
+#ifndef PPFS_ST_POLICY
+#define PPFS_ST_POLICY 1
+#endif
 template <int NT = 1> __device__ __forceinline__ void st_nt(uint8_t* dst, uint4 v)
 {
-    if constexpr (NT) {
+    if constexpr (NT && PPFS_ST_POLICY == 2) {
+        asm volatile("global_store_dwordx4 %0, %1, off nt sc1" ::"v"(dst), "v"(u32x4 { v.x, v.y, v.z, v.w }) : "memory");
+    } else if constexpr (NT && PPFS_ST_POLICY == 3) {
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(u32x4 { v.x, v.y, v.z, v.w }) : "memory");
+    } else if constexpr (NT && PPFS_ST_POLICY == 4) {
+        asm volatile("global_store_dwordx4 %0, %1, off nt sc0 sc1" ::"v"(dst), "v"(u32x4 { v.x, v.y, v.z, v.w }) : "memory");
+    } else if constexpr (NT) {
         const u32x4 u = { v.x, v.y, v.z, v.w };
         __builtin_nontemporal_store(u, (u32x4*)dst);
     } else {
