@@ -24,6 +24,7 @@
 #include <string>
 #include <thread>
 #include <unistd.h>
+#include <immintrin.h>
 #include <vector>
 
 #include "../../include/ppfs_ecc.h"
@@ -1477,6 +1478,78 @@ int copy_threads()
     return n;
 }
 
+// Streaming copy of one staging piece (round 5, PPFS_ECC_COPY_NT=0: plain memcpy): 64-byte
+// non-temporal stores skip the read-for-ownership of every destination line, so the copy moves
+// its bytes once instead of twice -- the destinations (the page-locked staging the DMA reads, or
+// a multi-MB caller buffer) do not fit in the caches anyway.  AVX-512 or AVX2 by the CPU, memcpy
+// for the unaligned head and the tail; an sfence makes the stores visible before the job's
+// completion is published.
+__attribute__((target("avx512f"))) void nt_copy512(uint8_t* d, const uint8_t* s, size_t n)
+{
+    size_t i = 0;
+    for (; i + 256 <= n; i += 256) {
+        const __m512i a = _mm512_loadu_si512((const void*)(s + i)), b = _mm512_loadu_si512((const void*)(s + i + 64));
+        const __m512i c = _mm512_loadu_si512((const void*)(s + i + 128)), e = _mm512_loadu_si512((const void*)(s + i + 192));
+        _mm512_stream_si512((__m512i*)(d + i), a);
+        _mm512_stream_si512((__m512i*)(d + i + 64), b);
+        _mm512_stream_si512((__m512i*)(d + i + 128), c);
+        _mm512_stream_si512((__m512i*)(d + i + 192), e);
+    }
+    for (; i + 64 <= n; i += 64)
+        _mm512_stream_si512((__m512i*)(d + i), _mm512_loadu_si512((const void*)(s + i)));
+    if (i < n)
+        std::memcpy(d + i, s + i, n - i);
+}
+__attribute__((target("avx2"))) void nt_copy256(uint8_t* d, const uint8_t* s, size_t n)
+{
+    size_t i = 0;
+    for (; i + 128 <= n; i += 128) {
+        const __m256i a = _mm256_loadu_si256((const __m256i*)(s + i)), b = _mm256_loadu_si256((const __m256i*)(s + i + 32));
+        const __m256i c = _mm256_loadu_si256((const __m256i*)(s + i + 64)), e = _mm256_loadu_si256((const __m256i*)(s + i + 96));
+        _mm256_stream_si256((__m256i*)(d + i), a);
+        _mm256_stream_si256((__m256i*)(d + i + 32), b);
+        _mm256_stream_si256((__m256i*)(d + i + 64), c);
+        _mm256_stream_si256((__m256i*)(d + i + 96), e);
+    }
+    if (i < n)
+        std::memcpy(d + i, s + i, n - i);
+}
+void piece_copy(void* dst, const void* src, size_t n)
+{
+    static const int mode = [] { // 2 AVX-512, 1 AVX2, 0 memcpy
+        const char* e = std::getenv("PPFS_ECC_COPY_NT");
+        if (e && *e == '0')
+            return 0;
+        // the CPU's flags from /proc/cpuinfo (this TU is also parsed for the GPU, where the
+        // compiler's CPU-feature builtins do not exist)
+        bool a512 = false, a2 = false;
+        if (FILE* f = std::fopen("/proc/cpuinfo", "r")) {
+            char line[8192];
+            while (std::fgets(line, sizeof(line), f))
+                if (std::strncmp(line, "flags", 5) == 0) {
+                    a512 = std::strstr(line, " avx512f") != nullptr;
+                    a2 = std::strstr(line, " avx2") != nullptr;
+                    break;
+                }
+            std::fclose(f);
+        }
+        return a512 ? 2 : (a2 ? 1 : 0);
+    }();
+    uint8_t* d = (uint8_t*)dst;
+    const uint8_t* s = (const uint8_t*)src;
+    if (mode == 0 || n < 4096) {
+        std::memcpy(d, s, n);
+        return;
+    }
+    const size_t head = (64 - ((uintptr_t)d & 63)) & 63; // stores 64-byte aligned
+    std::memcpy(d, s, head);
+    if (mode == 2)
+        nt_copy512(d + head, s + head, n - head);
+    else
+        nt_copy256(d + head, s + head, n - head);
+    _mm_sfence();
+}
+
 struct CopySeg {
     void* dst;
     const void* src;
@@ -1550,7 +1623,7 @@ private:
                 ++s;
             const size_t off = (p - j.first[s]) * kPiece;
             const size_t len = std::min(kPiece, j.seg[s].n - off);
-            std::memcpy((uint8_t*)j.seg[s].dst + off, (const uint8_t*)j.seg[s].src + off, len);
+            piece_copy((uint8_t*)j.seg[s].dst + off, (const uint8_t*)j.seg[s].src + off, len);
         }
         if (done && j.finished.fetch_add(done) + done == j.total) {
             std::lock_guard<std::mutex> g(m_);
