@@ -404,10 +404,10 @@ __device__ __forceinline__ void put_parity(uint8_t* lds, uint32_t img, const BsL
 // NW x NBUF wave images | 64 B slack (the rows' last-word reads and the decode emission's second
 // window run past the last image).  TLDS (decode): 0 = GF block and S12 table in LDS, 1 = the GF
 // block only (S12 read from the global table blob), 2 = neither (both global) -- LDS for more waves;
-// 3 = GF, S12 and the XPM rows (x^p mod g, 255 x 32 B) in LDS.
+// 3 = GF, S12 and the XPM rows (x^p mod g, 255 x 32 B) in LDS; 4 = GF and XPM in LDS, S12 global.
 template <int NW, int NBUF, bool DEC, int TLDS = 0> struct BsLds {
     static constexpr bool GF_IN = DEC && TLDS != 1 && TLDS != 2, S12_IN = DEC && (TLDS == 0 || TLDS == 3);
-    static constexpr bool XP_IN = DEC && TLDS == 3;
+    static constexpr bool XP_IN = DEC && (TLDS == 3 || TLDS == 4);
     static constexpr int OFF_GF = TAB_BYTES;
     static constexpr int OFF_S12 = OFF_GF + (GF_IN ? GF_BYTES : 0);
     static constexpr int OFF_XP = OFF_S12 + (S12_IN ? 32 * 256 * 2 : 0);
