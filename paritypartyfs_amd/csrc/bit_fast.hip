@@ -83,6 +83,29 @@ __device__ __forceinline__ uint4 gld16c(const uint8_t* p, const uint8_t* base, u
     return PPFS_DBG_OK(p, 16, base, extent) ? gld16(p) : make_uint4(0, 0, 0, 0);
 }
 
+// Payload loads of the parity encode: non-temporal (round 5, r5nt A/Bs on cfg4, 3 interleaved
+// rounds: 1,394-1,401 vs 1,484-1,491 us in the configs leg).  The Hamming encode gains as much
+// (1,422-1,425 vs 1,465-1,470 us) but the 1-error decode timed right after it then runs 1,642-1,658
+// vs 1,579-1,589 us, so it keeps plain loads; the CRC encode is slower with them (1,636-1,640 vs
+// 1,606-1,608 us), and so is every decode / check (Hamming +3 %, parity +4 %, CRC +3 %).
+#ifndef PPFS_BF_PAR_ENC_NTLD
+#define PPFS_BF_PAR_ENC_NTLD 1
+#endif
+#ifndef PPFS_BF_HAM_ENC_NTLD
+#define PPFS_BF_HAM_ENC_NTLD 0
+#endif
+template <bool NT> __device__ __forceinline__ uint4 gld16p(const uint8_t* p, const uint8_t* base, uint64_t extent)
+{
+    if constexpr (NT) {
+        if (!PPFS_DBG_OK(p, 16, base, extent))
+            return make_uint4(0, 0, 0, 0);
+        const bf_u32x4 v = __builtin_nontemporal_load((const bf_u32x4*)p);
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return gld16c(p, base, extent);
+    }
+}
+
 constexpr int WAVES = 4;
 // Grid and prefetch.  The kernels launch one wave per block over the whole batch (a full grid,
 // not a persistent one): the dispatcher then walks workgroups in address order, so the blocks in
@@ -152,7 +175,7 @@ template <int NP> struct HamEncStage {
     uint4 v[NPL];
 };
 
-template <int NP>
+template <int NP, bool NTL = false>
 __device__ __forceinline__ void ham_stage_load(HamEncStage<NP>& s, const uint8_t* __restrict__ data, uint64_t blk,
     const HamFast& a, uint32_t lane)
 {
@@ -165,7 +188,7 @@ __device__ __forceinline__ void ham_stage_load(HamEncStage<NP>& s, const uint8_t
         uint4 v = make_uint4(0, 0, 0, 0);
         if (p < npc) {
             if (g + 16 <= a.data_bytes) {
-                v = gld16c(data + g, data, a.data_bytes);
+                v = gld16p<NTL>(data + g, data, a.data_bytes);
             } else { // the batch's last bytes: one flat predicated load per byte (no nested
                      // divergence, which spilled the exec masks of 16 levels into SGPRs)
                 const uint32_t nb = g < a.data_bytes ? (uint32_t)(a.data_bytes - g) : 0u;
@@ -208,29 +231,29 @@ __device__ __forceinline__ void store_piece_part(uint8_t* dst, const uint32_t (&
     }
 }
 
-template <int NP>
-__global__ __launch_bounds__(256) void ham_fast_encode_kernel(const uint8_t* __restrict__ data, uint8_t* __restrict__ raw,
+template <int NP, int WV>
+__global__ __launch_bounds__(64 * WV) void ham_fast_encode_kernel(const uint8_t* __restrict__ data, uint8_t* __restrict__ raw,
     const uint8_t* __restrict__ skip, uint64_t nblocks_all, HamFast a)
 {
     constexpr int BUF = (NP + 1) * 1024 + 32; // NP + 1 staged pieces per lane + read slack
-    __shared__ __attribute__((aligned(16))) uint8_t lds[WAVES * BUF];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[WV * BUF];
     const uint32_t lane = lane_id(), wave = wave_id();
     uint8_t* buf = lds + wave * BUF;
     const uint32_t nwords = a.bs / 4, lastw = nwords - 1;
-    const uint64_t wg0 = (uint64_t)blockIdx.x * (WAVES * BF_BPW);
-    const uint64_t nblocks = nblocks_all < wg0 + WAVES * BF_BPW ? nblocks_all : wg0 + WAVES * BF_BPW;
-    const uint64_t stride = WAVES;
+    const uint64_t wg0 = (uint64_t)blockIdx.x * (WV * BF_BPW);
+    const uint64_t nblocks = nblocks_all < wg0 + WV * BF_BPW ? nblocks_all : wg0 + WV * BF_BPW;
+    const uint64_t stride = WV;
     uint64_t blk = wg0 + wave;
     HamEncStage<NP> st;
     if (blk < nblocks)
-        ham_stage_load<NP>(st, data, blk, a, lane);
+        ham_stage_load<NP, PPFS_BF_HAM_ENC_NTLD>(st, data, blk, a, lane);
     for (; blk < nblocks; blk += stride) {
         ham_stage_write<NP>(buf, st, lane);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         const uint64_t nx = blk + stride;
         if (BF_PREFETCH && nx < nblocks)
-            ham_stage_load<NP>(st, data, nx, a, lane); // lands while this block is computed
+            ham_stage_load<NP, PPFS_BF_HAM_ENC_NTLD>(st, data, nx, a, lane); // lands while this block is computed
         const uint32_t m = (uint32_t)((blk * a.ds) & 15u); // payload byte 0 sits at LDS byte m
         uint8_t* rb = raw + blk * a.bs;
         const bool skipped = skip && PPFS_DBG_OK(skip + blk, 1, skip, nblocks_all) && skip[blk] == 5;
@@ -314,7 +337,7 @@ __global__ __launch_bounds__(256) void ham_fast_encode_kernel(const uint8_t* __r
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); // LDS reads done before the rewrite
         __builtin_amdgcn_wave_barrier();
         if (!BF_PREFETCH && nx < nblocks)
-            ham_stage_load<NP>(st, data, nx, a, lane);
+            ham_stage_load<NP, PPFS_BF_HAM_ENC_NTLD>(st, data, nx, a, lane);
     }
 }
 
@@ -396,18 +419,18 @@ __device__ __forceinline__ void ham_mid_piece(const uint8_t* img, uint32_t b0, u
     }
 }
 
-template <int NP>
-__global__ __launch_bounds__(256) void ham_fast_decode_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
+template <int NP, int WV>
+__global__ __launch_bounds__(64 * WV) void ham_fast_decode_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
     uint8_t* __restrict__ status, uint64_t nblocks_all, int write_back, HamFast a)
 {
     constexpr int BUF = NP * 1024 + 16; // raw image + zero slack
-    __shared__ __attribute__((aligned(16))) uint8_t lds[WAVES * BUF];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[WV * BUF];
     const uint32_t lane = lane_id(), wave = wave_id();
     uint8_t* img = lds + wave * BUF;
     const uint32_t lastw = a.bs / 4 - 1;
-    const uint64_t wg0 = (uint64_t)blockIdx.x * (WAVES * BF_BPW);
-    const uint64_t nblocks = nblocks_all < wg0 + WAVES * BF_BPW ? nblocks_all : wg0 + WAVES * BF_BPW;
-    const uint64_t stride = WAVES;
+    const uint64_t wg0 = (uint64_t)blockIdx.x * (WV * BF_BPW);
+    const uint64_t nblocks = nblocks_all < wg0 + WV * BF_BPW ? nblocks_all : wg0 + WV * BF_BPW;
+    const uint64_t stride = WV;
     uint64_t blk = wg0 + wave;
     uint4 R[NP];
     if (blk < nblocks) {
@@ -606,24 +629,24 @@ struct ParFast {
     uint64_t data_bytes;
 };
 
-template <int NP>
-__global__ __launch_bounds__(256) void parity_fast_encode_kernel(const uint8_t* __restrict__ data,
+template <int NP, int WV>
+__global__ __launch_bounds__(64 * WV) void parity_fast_encode_kernel(const uint8_t* __restrict__ data,
     uint8_t* __restrict__ raw, const uint8_t* __restrict__ skip, uint64_t nblocks_all, ParFast a)
 {
     const uint32_t lane = lane_id(), wave = wave_id();
     const uint32_t ds = a.bs - 1;
     const HamFast ha { a.bs, ds, 0, a.data_bytes };
-    const uint64_t wg0 = (uint64_t)blockIdx.x * (WAVES * BF_BPW);
-    const uint64_t nblocks = nblocks_all < wg0 + WAVES * BF_BPW ? nblocks_all : wg0 + WAVES * BF_BPW;
-    const uint64_t stride = WAVES;
+    const uint64_t wg0 = (uint64_t)blockIdx.x * (WV * BF_BPW);
+    const uint64_t nblocks = nblocks_all < wg0 + WV * BF_BPW ? nblocks_all : wg0 + WV * BF_BPW;
+    const uint64_t stride = WV;
     uint64_t blk = wg0 + wave;
     HamEncStage<NP> cur, nxt;
     if (blk < nblocks)
-        ham_stage_load<NP>(cur, data, blk, ha, lane);
+        ham_stage_load<NP, PPFS_BF_PAR_ENC_NTLD>(cur, data, blk, ha, lane);
     for (; blk < nblocks; blk += stride) {
         const uint64_t nx = blk + stride;
         if (BF_PREFETCH && nx < nblocks)
-            ham_stage_load<NP>(nxt, data, nx, ha, lane);
+            ham_stage_load<NP, PPFS_BF_PAR_ENC_NTLD>(nxt, data, nx, ha, lane);
         const uint32_t m = (uint32_t)((blk * ds) & 15u);
         uint8_t* rb = raw + blk * a.bs;
         const uint32_t old_last = (lane == 63 && PPFS_DBG_OK(rb + a.bs - 1, 1, raw, nblocks_all * a.bs)) ? rb[a.bs - 1] : 0u;
@@ -653,19 +676,19 @@ __global__ __launch_bounds__(256) void parity_fast_encode_kernel(const uint8_t* 
         if (BF_PREFETCH)
             cur = nxt;
         else if (nx < nblocks)
-            ham_stage_load<NP>(cur, data, nx, ha, lane);
+            ham_stage_load<NP, PPFS_BF_PAR_ENC_NTLD>(cur, data, nx, ha, lane);
     }
 }
 
-template <int NP>
-__global__ __launch_bounds__(256) void parity_fast_check_kernel(const uint8_t* __restrict__ raw,
+template <int NP, int WV>
+__global__ __launch_bounds__(64 * WV) void parity_fast_check_kernel(const uint8_t* __restrict__ raw,
     uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks_all, ParFast a)
 {
     const uint32_t lane = lane_id(), wave = wave_id();
     const uint32_t ds = a.bs - 1;
-    const uint64_t wg0 = (uint64_t)blockIdx.x * (WAVES * BF_BPW);
-    const uint64_t nblocks = nblocks_all < wg0 + WAVES * BF_BPW ? nblocks_all : wg0 + WAVES * BF_BPW;
-    const uint64_t stride = WAVES;
+    const uint64_t wg0 = (uint64_t)blockIdx.x * (WV * BF_BPW);
+    const uint64_t nblocks = nblocks_all < wg0 + WV * BF_BPW ? nblocks_all : wg0 + WV * BF_BPW;
+    const uint64_t stride = WV;
     uint64_t blk = wg0 + wave;
     uint4 R[NP], N[NP];
     if (blk < nblocks)
@@ -1111,14 +1134,38 @@ __global__ __launch_bounds__(256) PPFS_CRC_ATTR void crc_fast_check_kernel(const
 
 using namespace ppfs;
 
-// Full grid: one wave per block, 4 blocks per 256-thread workgroup (see BF_PREFETCH above), capped
-// far above any batch a context stages (the kernels' loops then walk the rest).
-template <typename K> static uint32_t bf_grid(K, uint64_t nb)
+// Full grid: one wave per block, WV blocks per workgroup of WV waves (see BF_PREFETCH above); the
+// entry points refuse batches whose grid would pass 2^30 workgroups.
+template <typename K> static uint32_t bf_grid(K, uint64_t nb, int wv = bf::WAVES)
 {
-    const uint64_t want = (nb + bf::WAVES - 1) / bf::WAVES;
+    const uint64_t want = (nb + (uint64_t)wv - 1) / (uint64_t)wv;
     const uint64_t cap = 1ull << 30;
     return (uint32_t)(want < cap ? (want ? want : 1) : cap);
 }
+
+// Waves per workgroup of the Hamming and parity kernels (each wave owns its blocks and its LDS
+// buffer: no workgroup barrier).  Round 5: a wave-per-4-KiB-block copy with no coding work
+// (tools/stream_ceiling.hip, r5ce_*) moves 6.5-6.6 TB/s in one-wave workgroups at 6-8 waves per
+// CU against 5.9-6.2 TB/s in 4-wave workgroups at any cap -- fewer bytes in flight, and a freed
+// wave slot refills at once.  Measured on the kernels (configs leg, r5wv_* / r5wv2_*, two rounds):
+// parity encode in one-wave workgroups at 12 waves per CU 1.323-1.325 vs 1.393-1.398 ms (10: 1.338,
+// 14: 1.346-1.351, two-wave at 12: 1.346-1.349); parity check at 10 waves 1.462-1.463 vs 1.516-1.521
+// (8: 1.60, 12: 1.471-1.477); Hamming encode one-wave, uncapped (16 waves by registers) 1.418-1.423
+// vs 1.466-1.468 (two-wave 1.443-1.448, one-wave at 12: 1.494-1.497).  The Hamming decode keeps
+// 4-wave workgroups at 16 waves per CU: one-wave at 20 / 24 / 32 waves 1.545-1.561 / 1.611 vs
+// 1.523-1.527 ms clean, at 6 / 8 waves 3.10 / 2.41 ms (its per-block chain needs the waves).
+#ifndef PPFS_BF_HAM_ENC_WV
+#define PPFS_BF_HAM_ENC_WV 1
+#endif
+#ifndef PPFS_BF_HAM_DEC_WV
+#define PPFS_BF_HAM_DEC_WV 4
+#endif
+#ifndef PPFS_BF_PAR_ENC_WV
+#define PPFS_BF_PAR_ENC_WV 1
+#endif
+#ifndef PPFS_BF_PAR_CHK_WV
+#define PPFS_BF_PAR_CHK_WV 1
+#endif
 
 // Workgroups per CU of the streaming kernels (PPFS_BF_*_WG), enforced by dynamic LDS (0 = as many as
 // registers and static LDS allow).  One 4 KiB block per wave is in flight per wave.  Round 4 (cfg4,
@@ -1129,17 +1176,18 @@ static constexpr uint32_t bf_occ_lds(int wg, uint32_t static_lds)
 {
     return wg <= 0 ? 0u : (163840u / (uint32_t)(wg + 1) + 256u > static_lds ? 163840u / (uint32_t)(wg + 1) + 256u - static_lds : 0u);
 }
-#ifndef PPFS_BF_PAR_ENC_WG
-#define PPFS_BF_PAR_ENC_WG 3
+// Hamming / parity: the cap in waves per CU (0 = none), i.e. WV-wave workgroups per CU x WV
+#ifndef PPFS_BF_PAR_ENC_WPC
+#define PPFS_BF_PAR_ENC_WPC 12
 #endif
-#ifndef PPFS_BF_HAM_DEC_WG
-#define PPFS_BF_HAM_DEC_WG 4
+#ifndef PPFS_BF_HAM_DEC_WPC
+#define PPFS_BF_HAM_DEC_WPC 16
 #endif
-#ifndef PPFS_BF_HAM_ENC_WG
-#define PPFS_BF_HAM_ENC_WG 0
+#ifndef PPFS_BF_HAM_ENC_WPC
+#define PPFS_BF_HAM_ENC_WPC 0
 #endif
-#ifndef PPFS_BF_PAR_CHK_WG
-#define PPFS_BF_PAR_CHK_WG 3
+#ifndef PPFS_BF_PAR_CHK_WPC
+#define PPFS_BF_PAR_CHK_WPC 10
 #endif
 #ifndef PPFS_BF_CRC_CHK_WG
 #define PPFS_BF_CRC_CHK_WG 0
@@ -1147,16 +1195,25 @@ static constexpr uint32_t bf_occ_lds(int wg, uint32_t static_lds)
 #ifndef PPFS_BF_CRC_ENC_WG
 #define PPFS_BF_CRC_ENC_WG 0
 #endif
-template <int NP> static constexpr uint32_t par_enc_dyn_lds() { return bf_occ_lds(PPFS_BF_PAR_ENC_WG, 0); }
+static constexpr int bf_wg_cap(int wpc, int wv) { return wpc <= 0 ? 0 : (wpc / wv > 0 ? wpc / wv : 1); }
+template <int NP> static constexpr uint32_t par_enc_dyn_lds()
+{
+    return bf_occ_lds(bf_wg_cap(PPFS_BF_PAR_ENC_WPC, PPFS_BF_PAR_ENC_WV), 0);
+}
 template <int NP> static constexpr uint32_t ham_dec_dyn_lds()
 {
-    return bf_occ_lds(PPFS_BF_HAM_DEC_WG, bf::WAVES * (NP * 1024 + 16)); // ham_fast_decode_kernel's lds[]
+    constexpr int wv = PPFS_BF_HAM_DEC_WV;
+    return bf_occ_lds(bf_wg_cap(PPFS_BF_HAM_DEC_WPC, wv), wv * (NP * 1024 + 16)); // ham_fast_decode_kernel's lds[]
 }
 template <int NP> static constexpr uint32_t ham_enc_dyn_lds()
 {
-    return bf_occ_lds(PPFS_BF_HAM_ENC_WG, bf::WAVES * ((NP + 1) * 1024 + 32)); // ham_fast_encode_kernel's lds[]
+    constexpr int wv = PPFS_BF_HAM_ENC_WV;
+    return bf_occ_lds(bf_wg_cap(PPFS_BF_HAM_ENC_WPC, wv), wv * ((NP + 1) * 1024 + 32)); // ham_fast_encode_kernel's lds[]
 }
-template <int NP> static constexpr uint32_t par_chk_dyn_lds() { return bf_occ_lds(PPFS_BF_PAR_CHK_WG, 0); }
+template <int NP> static constexpr uint32_t par_chk_dyn_lds()
+{
+    return bf_occ_lds(bf_wg_cap(PPFS_BF_PAR_CHK_WPC, PPFS_BF_PAR_CHK_WV), 0);
+}
 template <int NP> static constexpr uint32_t crc_chk_dyn_lds() { return bf_occ_lds(PPFS_BF_CRC_CHK_WG, bf::CF_SIX_OFF); }
 template <int NP> static constexpr uint32_t crc_enc_dyn_lds() { return bf_occ_lds(PPFS_BF_CRC_ENC_WG, bf::CE::BYTES); }
 template <int NP> static constexpr uint32_t no_dyn_lds() { return 0; }
@@ -1176,14 +1233,27 @@ extern "C" int ppfs_bitfast_supported(uint32_t bs) { return bs == 1024 || bs == 
         break;                                                                                                         \
     }
 #define PPFS_NP_DISPATCH(bs, KERNEL, nb, ...) PPFS_NP_DISPATCH_SH(bs, KERNEL, nb, no_dyn_lds, __VA_ARGS__)
+// the Hamming / parity kernels: WV waves per workgroup
+#define PPFS_NP_DISPATCH_WV(bs, KERNEL, WV, nb, SH, ...)                                                               \
+    switch (bs) {                                                                                                      \
+    case 1024:                                                                                                         \
+        PPFS_LAUNCH((KERNEL<1, WV>), dim3(bf_grid(KERNEL<1, WV>, nb, WV)), dim3(64 * WV), SH<1>(), __VA_ARGS__);       \
+        break;                                                                                                         \
+    case 2048:                                                                                                         \
+        PPFS_LAUNCH((KERNEL<2, WV>), dim3(bf_grid(KERNEL<2, WV>, nb, WV)), dim3(64 * WV), SH<2>(), __VA_ARGS__);       \
+        break;                                                                                                         \
+    default:                                                                                                           \
+        PPFS_LAUNCH((KERNEL<4, WV>), dim3(bf_grid(KERNEL<4, WV>, nb, WV)), dim3(64 * WV), SH<4>(), __VA_ARGS__);       \
+        break;                                                                                                         \
+    }
 
 extern "C" hipError_t ppfs_ham_fast_encode(const uint8_t* d, uint8_t* r, const uint8_t* skip, uint64_t nb, uint32_t bs,
     uint32_t ds, uint32_t L, hipStream_t s)
 {
     const bf::HamFast a { bs, ds, L, nb * (uint64_t)ds };
-    if ((nb + 4ull * bf::BF_BPW - 1) / (4ull * bf::BF_BPW) > (1ull << 30))
+    if ((nb + (uint64_t)PPFS_BF_HAM_ENC_WV * bf::BF_BPW - 1) / ((uint64_t)PPFS_BF_HAM_ENC_WV * bf::BF_BPW) > (1ull << 30))
         return hipErrorInvalidValue;
-    PPFS_NP_DISPATCH_SH(bs, bf::ham_fast_encode_kernel, (nb + bf::BF_BPW - 1) / bf::BF_BPW, ham_enc_dyn_lds, s, d, r,
+    PPFS_NP_DISPATCH_WV(bs, bf::ham_fast_encode_kernel, PPFS_BF_HAM_ENC_WV, (nb + bf::BF_BPW - 1) / bf::BF_BPW, ham_enc_dyn_lds, s, d, r,
         skip, nb, a)
     return hipGetLastError();
 }
@@ -1192,11 +1262,11 @@ extern "C" hipError_t ppfs_ham_fast_decode(uint8_t* r, uint8_t* d, uint8_t* st, 
     uint32_t ds, uint32_t L, hipStream_t s)
 {
     const bf::HamFast a { bs, ds, L, nb * (uint64_t)ds };
-    if ((nb + 4ull * bf::BF_BPW - 1) / (4ull * bf::BF_BPW) > (1ull << 30))
+    if ((nb + (uint64_t)PPFS_BF_HAM_DEC_WV * bf::BF_BPW - 1) / ((uint64_t)PPFS_BF_HAM_DEC_WV * bf::BF_BPW) > (1ull << 30))
         return hipErrorInvalidValue;
     if (L < 32u * (bs / 4u - 1u) || L >= 8u * bs) // the kernel masks the last word only (true for 1-4 KiB)
         return hipErrorInvalidValue;
-    PPFS_NP_DISPATCH_SH(bs, bf::ham_fast_decode_kernel, (nb + bf::BF_BPW - 1) / bf::BF_BPW,
+    PPFS_NP_DISPATCH_WV(bs, bf::ham_fast_decode_kernel, PPFS_BF_HAM_DEC_WV, (nb + bf::BF_BPW - 1) / bf::BF_BPW,
         ham_dec_dyn_lds, s, r, d, st, nb, wb, a)
     return hipGetLastError();
 }
@@ -1240,9 +1310,9 @@ extern "C" hipError_t ppfs_parity_fast_encode(const uint8_t* d, uint8_t* r, cons
     uint32_t bs, hipStream_t s)
 {
     const bf::ParFast a { bs, nb * (uint64_t)(bs - 1) };
-    if ((nb + 4ull * bf::BF_BPW - 1) / (4ull * bf::BF_BPW) > (1ull << 30))
+    if ((nb + (uint64_t)PPFS_BF_PAR_ENC_WV * bf::BF_BPW - 1) / ((uint64_t)PPFS_BF_PAR_ENC_WV * bf::BF_BPW) > (1ull << 30))
         return hipErrorInvalidValue;
-    PPFS_NP_DISPATCH_SH(bs, bf::parity_fast_encode_kernel, (nb + bf::BF_BPW - 1) / bf::BF_BPW,
+    PPFS_NP_DISPATCH_WV(bs, bf::parity_fast_encode_kernel, PPFS_BF_PAR_ENC_WV, (nb + bf::BF_BPW - 1) / bf::BF_BPW,
         par_enc_dyn_lds, s, d, r, skip, nb, a)
     return hipGetLastError();
 }
@@ -1251,9 +1321,9 @@ extern "C" hipError_t ppfs_parity_fast_check(const uint8_t* r, uint8_t* d, uint8
     hipStream_t s)
 {
     const bf::ParFast a { bs, nb * (uint64_t)(bs - 1) };
-    if ((nb + 4ull * bf::BF_BPW - 1) / (4ull * bf::BF_BPW) > (1ull << 30))
+    if ((nb + (uint64_t)PPFS_BF_PAR_CHK_WV * bf::BF_BPW - 1) / ((uint64_t)PPFS_BF_PAR_CHK_WV * bf::BF_BPW) > (1ull << 30))
         return hipErrorInvalidValue;
-    PPFS_NP_DISPATCH_SH(bs, bf::parity_fast_check_kernel, (nb + bf::BF_BPW - 1) / bf::BF_BPW, par_chk_dyn_lds, s, r, d,
+    PPFS_NP_DISPATCH_WV(bs, bf::parity_fast_check_kernel, PPFS_BF_PAR_CHK_WV, (nb + bf::BF_BPW - 1) / bf::BF_BPW, par_chk_dyn_lds, s, r, d,
         st, nb, a)
     return hipGetLastError();
 }
