@@ -789,10 +789,10 @@ template <int NPLACE> struct CrcLds {
     static constexpr int BYTES = EIGHT + CF_NEIGHT * CF_EIGHT;
     static_assert(SIX % 16 == 0 && EIGHT % 16 == 0 && CF_EIGHT_OFF % 16 == 0, "16-byte staging");
     // copy the image's parts from the blob (placement maps from blob map `place0`)
-    __device__ static void stage(uint8_t* tbl, const uint8_t* __restrict__ tables, int place0)
+    __device__ static void stage(uint8_t* tbl, const uint8_t* __restrict__ tables, int place0, uint32_t nthreads)
     {
         auto part = [&](int dst, int src, int bytes) {
-            for (uint32_t p = threadIdx.x; p < (uint32_t)bytes / 16; p += 256)
+            for (uint32_t p = threadIdx.x; p < (uint32_t)bytes / 16; p += nthreads)
                 *(uint4*)(tbl + dst + 16 * p) = *(const uint4*)(tables + src + 16 * p);
         };
         part(PLACE, place0 * CF_MAP, NPLACE * CF_MAP);
@@ -803,12 +803,15 @@ template <int NPLACE> struct CrcLds {
 };
 using CE = CrcLds<16>;
 // Blocks per wave of the CRC kernels: a workgroup stages its maps once and then walks CRC_BPW
-// consecutive 4-block groups (one contiguous range, so the full grid keeps its address order); with
-// one group per workgroup the map staging read as much L2 as the blocks themselves.  Encode 8 (39 KiB
-// of maps), check 4 (22 KiB; round 4, r4zf: 4 -1.8 % against 8, 2 the same as 4; the encode at 4
-// +0.6 %, at 2 +1.7 %).
+// consecutive WV-block groups (one contiguous range, so the full grid keeps its address order); with
+// one group per workgroup the map staging read as much L2 as the blocks themselves.  Round 5 (r5crc*,
+// configs leg, 2 rounds each): the encode in 6-wave workgroups x 4 blocks per wave (24 waves per CU,
+// the 39 KiB map image allows 4 workgroups) 1.537-1.546 vs 1.583-1.593 ms for round 4's 4 x 8
+// (12 x 2: 1.545-1.549, 8 x 4: 1.551-1.556, 5 x 4: 1.567-1.573, 4 x 4: 1.570-1.593, 6 x 8: 1.627);
+// the check on its 14 KiB image in 2-wave workgroups x 4: 1.586-1.605 vs 1.603-1.628 ms for 4 x 4
+// (2 x 2: 1.70, 2 x 1: 1.89, 1-wave workgroups: 1.77-2.12 -- the image then caps a CU at 11 waves).
 #ifndef PPFS_CRC_BPW
-#define PPFS_CRC_BPW 8
+#define PPFS_CRC_BPW 4
 #endif
 #ifndef PPFS_CRC_CHK_BPW
 #define PPFS_CRC_CHK_BPW 4
@@ -973,20 +976,26 @@ __device__ __forceinline__ uint32_t crc_lane_sum(const uint8_t* tbl, uint32_t ac
 #endif
 #define PPFS_CRC_ENC_ATTR __attribute__((amdgpu_waves_per_eu(PPFS_CRC_ENC_WPE)))
 
-template <int NP>
-__global__ __launch_bounds__(256) PPFS_CRC_ENC_ATTR void crc_fast_encode_kernel(const uint8_t* __restrict__ data,
+template <int NP, int WV, int BPW>
+__global__ __launch_bounds__(64 * WV) PPFS_CRC_ENC_ATTR void crc_fast_encode_kernel(const uint8_t* __restrict__ data,
     uint8_t* __restrict__ raw, const uint8_t* __restrict__ skip, uint64_t nblocks_all, CrcFast a,
     const uint8_t* __restrict__ tables)
 {
     __shared__ __attribute__((aligned(16))) uint8_t tbl[CE::BYTES];
-    CE::stage(tbl, tables, CF_FENC);
-    __syncthreads();
-    const uint32_t lane = lane_id(), wave = wave_id();
+    CE::stage(tbl, tables, CF_FENC, 64 * WV);
+    if constexpr (WV > 1) {
+        __syncthreads();
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    const uint32_t lane = lane_id(), wave = WV > 1 ? wave_id() : 0u;
     const HamFast ha { a.bs, a.ds, 0, a.data_bytes };
     const bool n32 = a.n == 32;
-    const uint64_t wg0 = (uint64_t)blockIdx.x * (WAVES * CRC_BPW);
-    const uint64_t nblocks = nblocks_all < wg0 + WAVES * CRC_BPW ? nblocks_all : wg0 + WAVES * CRC_BPW;
-    const uint64_t stride = WAVES;
+    const uint64_t wg0 = (uint64_t)blockIdx.x * (WV * BPW);
+    const uint64_t nblocks = nblocks_all < wg0 + WV * BPW ? nblocks_all : wg0 + WV * BPW;
+    const uint64_t stride = WV;
     uint64_t blk = wg0 + wave;
     HamEncStage<NP> cur, nxt;
     if (blk < nblocks)
@@ -1042,21 +1051,34 @@ __global__ __launch_bounds__(256) PPFS_CRC_ENC_ATTR void crc_fast_encode_kernel(
     }
 }
 
-template <int NP>
-__global__ __launch_bounds__(256) PPFS_CRC_ATTR void crc_fast_check_kernel(const uint8_t* __restrict__ raw,
+// The check's LDS image (round 5): only the maps it reads -- M0..M3, K, the lane tree L..L+5
+// (blob maps 0-10), FCHK (blob map 27, here map 11) and the lane maps: 14 KiB where it used to
+// stage the blob's first 22.5 KiB (the encode's 16 placement maps included).
+constexpr int CK_FCHK = 11, CK_LANE_OFF = 12 * CF_MAP, CK_BYTES = CK_LANE_OFF + CF_LANES * CF_MAP;
+template <int NP, int WV, int BPW>
+__global__ __launch_bounds__(64 * WV) PPFS_CRC_ATTR void crc_fast_check_kernel(const uint8_t* __restrict__ raw,
     uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks_all, CrcFast a,
     const uint8_t* __restrict__ tables)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t tbl[CF_SIX_OFF];
-    for (uint32_t p = threadIdx.x; p < CF_SIX_OFF / 16; p += 256)
-        *(uint4*)(tbl + 16 * p) = *(const uint4*)(tables + 16 * p);
-    __syncthreads();
-    const uint32_t lane = lane_id(), wave = wave_id();
+    __shared__ __attribute__((aligned(16))) uint8_t tbl[CK_BYTES];
+    for (uint32_t p = threadIdx.x; p < CK_BYTES / 16; p += 64 * WV) {
+        const uint32_t o = 16 * p; // image byte o <- blob byte: maps 0-10 in place, then FCHK, then the lane maps
+        const uint32_t src = o < CK_FCHK * CF_MAP ? o : (o < CK_LANE_OFF ? CF_FCHK * CF_MAP + (o - CK_FCHK * CF_MAP) : CF_LANE_OFF + (o - CK_LANE_OFF));
+        *(uint4*)(tbl + o) = *(const uint4*)(tables + src);
+    }
+    if constexpr (WV > 1) {
+        __syncthreads();
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    const uint32_t lane = lane_id(), wave = WV > 1 ? wave_id() : 0u;
     const bool n32 = a.n == 32;
     const uint32_t ds = a.ds;
-    const uint64_t wg0 = (uint64_t)blockIdx.x * (WAVES * CRC_CHK_BPW);
-    const uint64_t nblocks = nblocks_all < wg0 + WAVES * CRC_CHK_BPW ? nblocks_all : wg0 + WAVES * CRC_CHK_BPW;
-    const uint64_t stride = WAVES;
+    const uint64_t wg0 = (uint64_t)blockIdx.x * (WV * BPW);
+    const uint64_t nblocks = nblocks_all < wg0 + WV * BPW ? nblocks_all : wg0 + WV * BPW;
+    const uint64_t stride = WV;
     uint64_t blk = wg0 + wave;
     uint4 R[NP], N[NP];
     if (blk < nblocks)
@@ -1078,8 +1100,8 @@ __global__ __launch_bounds__(256) PPFS_CRC_ATTR void crc_fast_check_kernel(const
             const uint32_t pv = crc_piece(tbl, R[k], 0u, hi_c, n32);
             acc = k == 0 ? pv : (cmap(tbl + CF_K * CF_MAP, acc) ^ pv);
         }
-        const uint32_t Vs = crc_lane_sum<CF_LANE_OFF, -1>(tbl, acc, lane);
-        const uint32_t V = cmap(tbl + CF_FCHK * CF_MAP, Vs);
+        const uint32_t Vs = crc_lane_sum<CK_LANE_OFF, -1>(tbl, acc, lane);
+        const uint32_t V = cmap(tbl + CK_FCHK * CF_MAP, Vs);
         const uint32_t st = (V << 1) & a.mask;
         // stored field: n bits MSB first from byte ds (in the last raw piece, lane 63)
         const uint4 last = make_uint4(__builtin_amdgcn_readlane(R[NP - 1].x, 63), __builtin_amdgcn_readlane(R[NP - 1].y, 63),
@@ -1189,12 +1211,6 @@ static constexpr uint32_t bf_occ_lds(int wg, uint32_t static_lds)
 #ifndef PPFS_BF_PAR_CHK_WPC
 #define PPFS_BF_PAR_CHK_WPC 10
 #endif
-#ifndef PPFS_BF_CRC_CHK_WG
-#define PPFS_BF_CRC_CHK_WG 0
-#endif
-#ifndef PPFS_BF_CRC_ENC_WG
-#define PPFS_BF_CRC_ENC_WG 0
-#endif
 static constexpr int bf_wg_cap(int wpc, int wv) { return wpc <= 0 ? 0 : (wpc / wv > 0 ? wpc / wv : 1); }
 template <int NP> static constexpr uint32_t par_enc_dyn_lds()
 {
@@ -1214,8 +1230,30 @@ template <int NP> static constexpr uint32_t par_chk_dyn_lds()
 {
     return bf_occ_lds(bf_wg_cap(PPFS_BF_PAR_CHK_WPC, PPFS_BF_PAR_CHK_WV), 0);
 }
-template <int NP> static constexpr uint32_t crc_chk_dyn_lds() { return bf_occ_lds(PPFS_BF_CRC_CHK_WG, bf::CF_SIX_OFF); }
-template <int NP> static constexpr uint32_t crc_enc_dyn_lds() { return bf_occ_lds(PPFS_BF_CRC_ENC_WG, bf::CE::BYTES); }
+// CRC check: PPFS_BF_CRC_CHK_WV waves per workgroup, PPFS_CRC_CHK_BPW blocks per wave, at most
+// PPFS_BF_CRC_CHK_WPC waves per CU (0: as registers allow)
+#ifndef PPFS_BF_CRC_CHK_WV
+#define PPFS_BF_CRC_CHK_WV 2
+#endif
+#ifndef PPFS_BF_CRC_CHK_WPC
+#define PPFS_BF_CRC_CHK_WPC 0
+#endif
+template <int NP> static constexpr uint32_t crc_chk_dyn_lds()
+{
+    return bf_occ_lds(bf_wg_cap(PPFS_BF_CRC_CHK_WPC, PPFS_BF_CRC_CHK_WV), bf::CK_BYTES);
+}
+// CRC encode: PPFS_BF_CRC_ENC_WV waves per workgroup, PPFS_CRC_BPW blocks per wave, at most
+// PPFS_BF_CRC_ENC_WPC waves per CU (0: as LDS and registers allow)
+#ifndef PPFS_BF_CRC_ENC_WV
+#define PPFS_BF_CRC_ENC_WV 6
+#endif
+#ifndef PPFS_BF_CRC_ENC_WPC
+#define PPFS_BF_CRC_ENC_WPC 0
+#endif
+template <int NP> static constexpr uint32_t crc_enc_dyn_lds()
+{
+    return bf_occ_lds(bf_wg_cap(PPFS_BF_CRC_ENC_WPC, PPFS_BF_CRC_ENC_WV), bf::CE::BYTES);
+}
 template <int NP> static constexpr uint32_t no_dyn_lds() { return 0; }
 
 extern "C" int ppfs_bitfast_supported(uint32_t bs) { return bs == 1024 || bs == 2048 || bs == 4096; }
@@ -1288,10 +1326,25 @@ extern "C" hipError_t ppfs_crc_fast_encode(const uint8_t* d, uint8_t* r, const u
     uint32_t ds, uint32_t n, uint64_t mask, const uint8_t* tab, hipStream_t s)
 {
     const bf::CrcFast a { bs, ds, n, bs - ds, (uint32_t)mask, nb * (uint64_t)ds };
-    if ((nb + 4ull * bf::CRC_BPW - 1) / (4ull * bf::CRC_BPW) > (1ull << 30))
+    constexpr uint64_t per_wg = (uint64_t)PPFS_BF_CRC_ENC_WV * bf::CRC_BPW;
+    if ((nb + per_wg - 1) / per_wg > (1ull << 30))
         return hipErrorInvalidValue;
-    PPFS_NP_DISPATCH_SH(bs, bf::crc_fast_encode_kernel, (nb + bf::CRC_BPW - 1) / bf::CRC_BPW, crc_enc_dyn_lds, s, d, r,
-        skip, nb, a, tab)
+    constexpr int wv = PPFS_BF_CRC_ENC_WV, bpw = bf::CRC_BPW;
+    const uint64_t nw = (nb + bpw - 1) / bpw; // waves
+    switch (bs) {
+    case 1024:
+        PPFS_LAUNCH((bf::crc_fast_encode_kernel<1, wv, bpw>), dim3(bf_grid(0, nw, wv)), dim3(64 * wv), crc_enc_dyn_lds<1>(), s, d,
+            r, skip, nb, a, tab);
+        break;
+    case 2048:
+        PPFS_LAUNCH((bf::crc_fast_encode_kernel<2, wv, bpw>), dim3(bf_grid(0, nw, wv)), dim3(64 * wv), crc_enc_dyn_lds<2>(), s, d,
+            r, skip, nb, a, tab);
+        break;
+    default:
+        PPFS_LAUNCH((bf::crc_fast_encode_kernel<4, wv, bpw>), dim3(bf_grid(0, nw, wv)), dim3(64 * wv), crc_enc_dyn_lds<4>(), s, d,
+            r, skip, nb, a, tab);
+        break;
+    }
     return hipGetLastError();
 }
 
@@ -1299,10 +1352,25 @@ extern "C" hipError_t ppfs_crc_fast_check(const uint8_t* r, uint8_t* d, uint8_t*
     uint32_t ds, uint32_t n, uint64_t mask, const uint8_t* tab, hipStream_t s)
 {
     const bf::CrcFast a { bs, ds, n, bs - ds, (uint32_t)mask, nb * (uint64_t)ds };
-    if ((nb + 4ull * bf::CRC_CHK_BPW - 1) / (4ull * bf::CRC_CHK_BPW) > (1ull << 30))
+    constexpr uint64_t per_wg = (uint64_t)PPFS_BF_CRC_CHK_WV * bf::CRC_CHK_BPW;
+    if ((nb + per_wg - 1) / per_wg > (1ull << 30))
         return hipErrorInvalidValue;
-    PPFS_NP_DISPATCH_SH(bs, bf::crc_fast_check_kernel, (nb + bf::CRC_CHK_BPW - 1) / bf::CRC_CHK_BPW, crc_chk_dyn_lds, s, r, d,
-        st, nb, a, tab)
+    constexpr int wv = PPFS_BF_CRC_CHK_WV, bpw = bf::CRC_CHK_BPW;
+    const uint64_t nw = (nb + bpw - 1) / bpw; // waves
+    switch (bs) {
+    case 1024:
+        PPFS_LAUNCH((bf::crc_fast_check_kernel<1, wv, bpw>), dim3(bf_grid(0, nw, wv)), dim3(64 * wv), crc_chk_dyn_lds<1>(), s, r,
+            d, st, nb, a, tab);
+        break;
+    case 2048:
+        PPFS_LAUNCH((bf::crc_fast_check_kernel<2, wv, bpw>), dim3(bf_grid(0, nw, wv)), dim3(64 * wv), crc_chk_dyn_lds<2>(), s, r,
+            d, st, nb, a, tab);
+        break;
+    default:
+        PPFS_LAUNCH((bf::crc_fast_check_kernel<4, wv, bpw>), dim3(bf_grid(0, nw, wv)), dim3(64 * wv), crc_chk_dyn_lds<4>(), s, r,
+            d, st, nb, a, tab);
+        break;
+    }
     return hipGetLastError();
 }
 

@@ -168,6 +168,47 @@ __global__ __launch_bounds__(256) void cp_flatn(const u32x4* __restrict__ in, u3
         __builtin_nontemporal_store(v[k], out + i0 + 256 * k);
 }
 
+// copy, persistent waves drawing BPT-block tiles from per-XCD ticket counters (the t <= 4 RS
+// kernels' walk): XCD xc = blockIdx.x mod 8 walks tiles j * 8 + xc; a wave's first tile is static,
+// then one atomic per tile (taken a tile ahead); block 0 zeroes the other counter set for the next launch
+template <int BPT>
+__global__ __launch_bounds__(1024) void cp_ticket(const u32x4* __restrict__ in, u32x4* __restrict__ out, uint32_t nblk,
+    uint32_t* __restrict__ ctr, uint32_t* __restrict__ ctr_clear)
+{
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const uint32_t nx = gridDim.x < 8u ? gridDim.x : 8u, xc = blockIdx.x % nx, rank = blockIdx.x / nx;
+    const uint32_t gx = (gridDim.x - xc + nx - 1u) / nx;
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (uint32_t x = 0; x < 8u; ++x)
+            __hip_atomic_store(ctr_clear + 32u * x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t* const my = ctr + 32u * xc;
+    const uint64_t G = (uint64_t)gx * nw;
+    uint64_t j = (uint64_t)rank * nw + wave;
+    const uint64_t ntiles = (nblk + BPT - 1) / BPT;
+    for (;;) {
+        const uint64_t tile = j * nx + xc;
+        if (tile >= ntiles)
+            break;
+        uint32_t tk = 0;
+        if (lane == 0)
+            tk = atomicAdd(my, 1u);
+#pragma unroll
+        for (int b = 0; b < BPT; ++b) {
+            const uint64_t blk = tile * BPT + b;
+            if (blk < nblk) {
+                u32x4 v[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    v[k] = ld<true>(in + blk * 256 + 64 * k + lane);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    __builtin_nontemporal_store(v[k], out + blk * 256 + 64 * k + lane);
+            }
+        }
+        j = G + (uint64_t)__builtin_amdgcn_readfirstlane(tk);
+    }
+}
+
 template <typename F> static double time_ms(F launch, int reps)
 {
     hipEvent_t a, b;
@@ -275,6 +316,31 @@ int main(int argc, char** argv)
         report(nm, time_ms([&] { ro_wave<true, 1, 1, true><<<nblk, 64, lds>>>(in, st, nblk); }, reps), rds);
         snprintf(nm, sizeof nm, "ro_wave nt=0 bpw=1 wgw=1 waves/CU=%d", wpc);
         report(nm, time_ms([&] { ro_wave<false, 1, 1, true><<<nblk, 64, lds>>>(in, st, nblk); }, reps), rds);
+    }
+    {
+        uint32_t* ctr = nullptr;
+        CK(hipMalloc(&ctr, 2 * 8 * 32 * 4));
+        CK(hipMemset(ctr, 0, 2 * 8 * 32 * 4));
+        int it = 0;
+        struct Shape { int threads, wg_per_cu; };
+        for (Shape sh : { Shape { 1024, 1 }, Shape { 512, 2 }, Shape { 256, 4 }, Shape { 64, 16 }, Shape { 768, 1 }, Shape { 512, 1 },
+                 Shape { 256, 3 }, Shape { 64, 12 }, Shape { 64, 8 } }) {
+            for (int bpt : { 1, 4 }) {
+                char nm[96];
+                snprintf(nm, sizeof nm, "cp_ticket threads=%d wg/CU=%d bpt=%d", sh.threads, sh.wg_per_cu, bpt);
+                const uint32_t grid = (uint32_t)(cus * sh.wg_per_cu);
+                report(nm, time_ms([&] {
+                    uint32_t* c0 = ctr + 256 * (it & 1);
+                    uint32_t* c1 = ctr + 256 * ((it + 1) & 1);
+                    ++it;
+                    if (bpt == 1)
+                        cp_ticket<1><<<grid, sh.threads>>>(in, out, nblk, c0, c1);
+                    else
+                        cp_ticket<4><<<grid, sh.threads>>>(in, out, nblk, c0, c1);
+                }, reps), cp);
+            }
+        }
+        CK(hipFree(ctr));
     }
     for (int g : { 4, 8, 16 }) {
         char nm[64];
