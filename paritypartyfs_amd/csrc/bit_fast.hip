@@ -1054,7 +1054,16 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ENC_ATTR void crc_fast_encode_ker
 // The check's LDS image (round 5): only the maps it reads -- M0..M3, K, the lane tree L..L+5
 // (blob maps 0-10), FCHK (blob map 27, here map 11) and the lane maps: 14 KiB where it used to
 // stage the blob's first 22.5 KiB (the encode's 16 placement maps included).
-constexpr int CK_FCHK = 11, CK_LANE_OFF = 12 * CF_MAP, CK_BYTES = CK_LANE_OFF + CF_LANES * CF_MAP;
+// PPFS_CRC_CHK_EIGHT (A/B): the piece and Horner maps as the encode's 8-bit tables instead (4 lookups
+// per map, not 8), image = lane maps | 6-bit tree maps | FCHK | 8-bit maps, 31 KiB
+#ifndef PPFS_CRC_CHK_EIGHT
+#define PPFS_CRC_CHK_EIGHT 0
+#endif
+constexpr int CK_FCHK = 11, CK_LANE_OFF = 12 * CF_MAP, CK_NIB_BYTES = CK_LANE_OFF + CF_LANES * CF_MAP;
+constexpr int CK8_SIX = CF_LANES * CF_MAP, CK8_FCHK = CK8_SIX + CF_NSIX * CF_MAP6, CK8_EIGHT = CK8_FCHK + CF_MAP;
+constexpr int CK8_BYTES = CK8_EIGHT + CF_NEIGHT * CF_EIGHT;
+constexpr int CK_BYTES = PPFS_CRC_CHK_EIGHT ? CK8_BYTES : CK_NIB_BYTES;
+static_assert(CK8_SIX % 16 == 0 && CK8_FCHK % 16 == 0 && CK8_EIGHT % 16 == 0, "16-byte staging");
 template <int NP, int WV, int BPW>
 __global__ __launch_bounds__(64 * WV) PPFS_CRC_ATTR void crc_fast_check_kernel(const uint8_t* __restrict__ raw,
     uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks_all, CrcFast a,
@@ -1062,8 +1071,13 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ATTR void crc_fast_check_kernel(c
 {
     __shared__ __attribute__((aligned(16))) uint8_t tbl[CK_BYTES];
     for (uint32_t p = threadIdx.x; p < CK_BYTES / 16; p += 64 * WV) {
-        const uint32_t o = 16 * p; // image byte o <- blob byte: maps 0-10 in place, then FCHK, then the lane maps
-        const uint32_t src = o < CK_FCHK * CF_MAP ? o : (o < CK_LANE_OFF ? CF_FCHK * CF_MAP + (o - CK_FCHK * CF_MAP) : CF_LANE_OFF + (o - CK_LANE_OFF));
+        const uint32_t o = 16 * p;
+        uint32_t src;
+        if constexpr (PPFS_CRC_CHK_EIGHT) // lane maps, 6-bit maps, FCHK, 8-bit maps
+            src = o < CK8_SIX ? CF_LANE_OFF + o
+                : (o < CK8_FCHK ? CF_SIX_OFF + (o - CK8_SIX) : (o < CK8_EIGHT ? CF_FCHK * CF_MAP + (o - CK8_FCHK) : CF_EIGHT_OFF + (o - CK8_EIGHT)));
+        else // maps 0-10 in place, then FCHK, then the lane maps
+            src = o < CK_FCHK * CF_MAP ? o : (o < CK_LANE_OFF ? CF_FCHK * CF_MAP + (o - CK_FCHK * CF_MAP) : CF_LANE_OFF + (o - CK_LANE_OFF));
         *(uint4*)(tbl + o) = *(const uint4*)(tables + src);
     }
     if constexpr (WV > 1) {
@@ -1097,11 +1111,19 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ATTR void crc_fast_check_kernel(c
             const int32_t q16 = 16 * (64 * k + (int32_t)lane);
             const int32_t hi = (int32_t)ds - q16;
             const uint32_t hi_c = hi < 0 ? 0u : (hi > 16 ? 16u : (uint32_t)hi);
-            const uint32_t pv = crc_piece(tbl, R[k], 0u, hi_c, n32);
-            acc = k == 0 ? pv : (cmap(tbl + CF_K * CF_MAP, acc) ^ pv);
+            if constexpr (PPFS_CRC_CHK_EIGHT) {
+                const uint32_t pv = crc_piece8(tbl + CK8_EIGHT, R[k], 0u, hi_c, n32);
+                acc = k == 0 ? pv : (cmap8(tbl + CK8_EIGHT + 4 * CF_EIGHT, acc) ^ pv);
+            } else {
+                const uint32_t pv = crc_piece(tbl, R[k], 0u, hi_c, n32);
+                acc = k == 0 ? pv : (cmap(tbl + CF_K * CF_MAP, acc) ^ pv);
+            }
         }
-        const uint32_t Vs = crc_lane_sum<CK_LANE_OFF, -1>(tbl, acc, lane);
-        const uint32_t V = cmap(tbl + CK_FCHK * CF_MAP, Vs);
+        uint32_t V;
+        if constexpr (PPFS_CRC_CHK_EIGHT)
+            V = cmap(tbl + CK8_FCHK, crc_lane_sum<0, CK8_SIX>(tbl, acc, lane));
+        else
+            V = cmap(tbl + CK_FCHK * CF_MAP, crc_lane_sum<CK_LANE_OFF, -1>(tbl, acc, lane));
         const uint32_t st = (V << 1) & a.mask;
         // stored field: n bits MSB first from byte ds (in the last raw piece, lane 63)
         const uint4 last = make_uint4(__builtin_amdgcn_readlane(R[NP - 1].x, 63), __builtin_amdgcn_readlane(R[NP - 1].y, 63),
