@@ -126,6 +126,12 @@ constexpr int BF_BPW = PPFS_BF_BPW;
 
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 
+#define PPFS_BF_PRAGMA(x) _Pragma(#x)
+#define PPFS_BF_UNROLL(n) PPFS_BF_PRAGMA(unroll n)
+#ifndef PPFS_HAM_DEC_EMIT_UNROLL
+#define PPFS_HAM_DEC_EMIT_UNROLL 1
+#endif
+
 // XOR over the 64 lanes of a wave, returned wave-uniform: a DPP butterfly inside each row of 16
 // lanes, then row broadcasts 15 and 31 (lane 63 ends with the total).
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v)
@@ -549,8 +555,9 @@ __global__ __launch_bounds__(64 * WV) void ham_fast_decode_kernel(uint8_t* __res
                 }
                 store(lane, b0, o);
             }
-            // pieces k >= 1: no head path; one rolled loop keeps the live state to one piece
-#pragma unroll 1
+            // pieces k >= 1: no head path; PPFS_HAM_DEC_EMIT_UNROLL pieces' window reads in flight
+            // (1: one rolled loop keeps the live state to one piece)
+            PPFS_BF_UNROLL(PPFS_HAM_DEC_EMIT_UNROLL)
             for (int k = 1; k <= NP; ++k) {
                 const uint32_t p = 64u * k + lane;
                 if (p >= npc)
