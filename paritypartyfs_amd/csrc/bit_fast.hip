@@ -131,6 +131,12 @@ __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32
 #ifndef PPFS_HAM_DEC_EMIT_UNROLL
 #define PPFS_HAM_DEC_EMIT_UNROLL 1
 #endif
+// Hamming decode: the LDS image stores issued before the syndrome reduction (1, round 5), so they
+// complete under its DPP chain, or after it, only for blocks with a payload output (0).  Configs leg,
+// 3 interleaved rounds (r5hei): clean 1.512-1.523 vs 1.531 ms, 1-error 1.582-1.590 vs 1.588-1.602 ms.
+#ifndef PPFS_HAM_DEC_EARLY_IMG
+#define PPFS_HAM_DEC_EARLY_IMG 1
+#endif
 
 // XOR over the 64 lanes of a wave, returned wave-uniform: a DPP butterfly inside each row of 16
 // lanes, then row broadcasts 15 and 31 (lane 63 ends with the total).
@@ -466,6 +472,13 @@ __global__ __launch_bounds__(64 * WV) void ham_fast_decode_kernel(uint8_t* __res
         // the lane's word w = 256 k + 4 lane + u contributes 4 lane if odd, plus 256 k + u, whose bits
         // are the parities of the words with that bit of k or u set.  Only the block's last word (lane
         // 63, piece NP - 1, u = 3) holds bits past L, which are not part of the code.
+        if (PPFS_HAM_DEC_EARLY_IMG && data) {
+#pragma unroll
+            for (int k = 0; k < NP; ++k)
+                *(uint4*)(img + 16u * (64u * k + lane)) = make_uint4(X[k][0], X[k][1], X[k][2], X[k][3]);
+            if (lane < 4)
+                *(uint32_t*)(img + NP * 1024 + 4 * lane) = 0;
+        }
         uint32_t xk[NP][4];
 #pragma unroll
         for (int k = 0; k < NP; ++k)
@@ -503,11 +516,13 @@ __global__ __launch_bounds__(64 * WV) void ham_fast_decode_kernel(uint8_t* __res
         if (status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
             status[blk] = (uint8_t)st;
         if (data && st != 5) {
+            if (!PPFS_HAM_DEC_EARLY_IMG) {
 #pragma unroll
-            for (int k = 0; k < NP; ++k)
-                *(uint4*)(img + 16u * (64u * k + lane)) = make_uint4(X[k][0], X[k][1], X[k][2], X[k][3]);
-            if (lane < 4)
-                *(uint32_t*)(img + NP * 1024 + 4 * lane) = 0;
+                for (int k = 0; k < NP; ++k)
+                    *(uint4*)(img + 16u * (64u * k + lane)) = make_uint4(X[k][0], X[k][1], X[k][2], X[k][3]);
+                if (lane < 4)
+                    *(uint32_t*)(img + NP * 1024 + 4 * lane) = 0;
+            }
             // the correction, after the image stores of the same wave (LDS ops of a wave run in order)
             if (owner) {
                 __hip_atomic_fetch_xor((uint32_t*)(img + ((S >> 5) << 2)), 0x80u << (8 * ((S >> 3) & 3u)) >> (S & 7u),
@@ -824,6 +839,23 @@ using CE = CrcLds<16>;
 #define PPFS_CRC_CHK_BPW 4
 #endif
 constexpr int CRC_BPW = PPFS_CRC_BPW, CRC_CHK_BPW = PPFS_CRC_CHK_BPW;
+// Register prefetch of a wave's next block in the CRC kernels (A/B knobs; default: BF_PREFETCH)
+#ifndef PPFS_CRC_ENC_PF
+#define PPFS_CRC_ENC_PF PPFS_BF_PREFETCH
+#endif
+#ifndef PPFS_CRC_CHK_PF
+#define PPFS_CRC_CHK_PF PPFS_BF_PREFETCH
+#endif
+constexpr bool CRC_ENC_PF = PPFS_CRC_ENC_PF, CRC_CHK_PF = PPFS_CRC_CHK_PF;
+// Output stores issued before the CRC computation (A/B knobs): the encode stores every raw piece
+// but the block's last one (lane 63, which carries the CRC field) first, the check its payload
+// output first, so the stores drain under the lookups instead of behind them
+#ifndef PPFS_CRC_ENC_EARLY_ST
+#define PPFS_CRC_ENC_EARLY_ST 0
+#endif
+#ifndef PPFS_CRC_CHK_EARLY_ST
+#define PPFS_CRC_CHK_EARLY_ST 0
+#endif
 
 // (x >> 8k) & 0x3C (a nibble * 4, the entry's byte offset): one v_and_b32_sdwa for k > 0
 __device__ __forceinline__ uint32_t sel3c(uint32_t x, int k)
@@ -1009,11 +1041,24 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ENC_ATTR void crc_fast_encode_ker
         ham_stage_load<NP>(cur, data, blk, ha, lane);
     for (; blk < nblocks; blk += stride) {
         const uint64_t nx = blk + stride;
-        if (BF_PREFETCH && nx < nblocks)
+        if (CRC_ENC_PF && nx < nblocks)
             ham_stage_load<NP>(nxt, data, nx, ha, lane);
         const uint32_t m = (uint32_t)((blk * a.ds) & 15u); // payload byte 0 = superset byte m
         uint8_t* rb = raw + blk * a.bs;
         // superset piece q = 64 k + lane holds superset bytes [16 q, +16); payload = [m, m + ds)
+        const bool store_blk = !(skip && PPFS_DBG_OK(skip + blk, 1, skip, nblocks_all) && skip[blk] == 5);
+        if (PPFS_CRC_ENC_EARLY_ST && store_blk) {
+            // every raw piece but the block's last (lane 63, piece NP - 1: the CRC field)
+#pragma unroll
+            for (int k = 0; k < NP; ++k) {
+                if (k == NP - 1 && lane == 63)
+                    continue;
+                const uint4 nb = next_piece(cur.v[k], cur.v[k + 1]);
+                const uint4 o = shift_pieces(cur.v[k], nb, m);
+                if (PPFS_DBG_OK(rb + 16u * (64u * k + lane), 16, raw, nblocks_all * a.bs))
+                    gst16_raw(rb + 16u * (64u * k + lane), o);
+            }
+        }
         uint32_t acc = 0;
 #pragma unroll
         for (int k = 0; k <= NP; ++k) {
@@ -1027,14 +1072,16 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ENC_ATTR void crc_fast_encode_ker
         const uint32_t Vs = crc_lane_sum<CE::LANE, CE::SIX>(tbl, acc, lane);
         const uint32_t V = cmap(tbl + CE::PLACE + m * CF_MAP, Vs);
         const uint32_t st = (V << 1) & a.mask;
-        if (!(skip && PPFS_DBG_OK(skip + blk, 1, skip, nblocks_all) && skip[blk] == 5)) {
+        if (store_blk) {
             // raw bytes [ds, ds + nbc): the n CRC bits MSB first (a partial last byte keeps its old
             // low bits); all in the row's last raw piece (lane 63, k = NP - 1)
             uint32_t old_last = 0;
             if (lane == 63 && (a.n & 7u) && PPFS_DBG_OK(rb + a.ds + a.nbc - 1, 1, raw, nblocks_all * a.bs))
                 old_last = rb[a.ds + a.nbc - 1];
 #pragma unroll
-            for (int k = 0; k < NP; ++k) {
+            for (int k = PPFS_CRC_ENC_EARLY_ST ? NP - 1 : 0; k < NP; ++k) {
+                if (PPFS_CRC_ENC_EARLY_ST && lane != 63)
+                    break;
                 const uint4 nb = next_piece(cur.v[k], cur.v[k + 1]);
                 uint4 o = shift_pieces(cur.v[k], nb, m);
                 if (k == NP - 1 && lane == 63) {
@@ -1051,7 +1098,7 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ENC_ATTR void crc_fast_encode_ker
                     gst16_raw(rb + 16u * (64u * k + lane), o);
             }
         }
-        if (BF_PREFETCH)
+        if (CRC_ENC_PF)
             cur = nxt;
         else if (nx < nblocks)
             ham_stage_load<NP>(cur, data, nx, ha, lane);
@@ -1108,10 +1155,37 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ATTR void crc_fast_check_kernel(c
             R[k] = gld16c(raw + blk * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
     for (; blk < nblocks; blk += stride) {
         const uint64_t nx = blk + stride;
-        if (BF_PREFETCH && nx < nblocks)
+        if (CRC_CHK_PF && nx < nblocks)
 #pragma unroll
             for (int k = 0; k < NP; ++k)
                 N[k] = gld16c(raw + nx * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
+        auto emit = [&]() {
+            if (data) {
+                const uint64_t start = blk * ds, a0 = start & ~15ull;
+                const uint32_t m = (uint32_t)(start - a0);
+#pragma unroll
+                for (int k = 0; k <= NP; ++k) {
+                    const uint32_t p = 64u * k + lane;
+                    const uint4 own = k < NP ? R[k] : make_uint4(0, 0, 0, 0);
+                    const uint4 prev = k == 0 ? prev_piece<true>(own, own) : prev_piece<false>(own, R[k > 0 ? k - 1 : 0]);
+                    const uint4 oo = m == 0 ? own : shift_pieces(prev, own, (16u - m) & 15u);
+                    const int32_t b0 = (int32_t)(16 * p) - (int32_t)m;
+                    uint8_t* dst = data + a0 + 16ull * p;
+                    if (b0 >= 0 && b0 + 16 <= (int32_t)ds) {
+                        if (PPFS_DBG_OK(dst, 16, data, nblocks_all * ds))
+                            gst16(dst, oo);
+                    } else if (b0 < (int32_t)ds && b0 + 16 > 0
+                        && PPFS_DBG_OK(dst + (b0 < 0 ? -b0 : 0), (b0 + 16 > (int32_t)ds ? (int32_t)ds - b0 : 16) - (b0 < 0 ? -b0 : 0),
+                            data, nblocks_all * ds)) {
+                        const uint32_t w[4] = { oo.x, oo.y, oo.z, oo.w };
+                        store_piece_part(dst, w, b0 < 0 ? (uint32_t)(-b0) : 0u,
+                            b0 + 16 > (int32_t)ds ? (uint32_t)((int32_t)ds - b0) : 16u);
+                    }
+                }
+            }
+        };
+        if (PPFS_CRC_CHK_EARLY_ST)
+            emit();
         uint32_t acc = 0;
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
@@ -1145,30 +1219,9 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ATTR void crc_fast_check_kernel(c
         const uint32_t field = (uint32_t)(f >> (8 * a.nbc - a.n));
         if (status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
             status[blk] = (st == field) ? 0 : 5;
-        if (data) {
-            const uint64_t start = blk * ds, a0 = start & ~15ull;
-            const uint32_t m = (uint32_t)(start - a0);
-#pragma unroll
-            for (int k = 0; k <= NP; ++k) {
-                const uint32_t p = 64u * k + lane;
-                const uint4 own = k < NP ? R[k] : make_uint4(0, 0, 0, 0);
-                const uint4 prev = k == 0 ? prev_piece<true>(own, own) : prev_piece<false>(own, R[k > 0 ? k - 1 : 0]);
-                const uint4 oo = m == 0 ? own : shift_pieces(prev, own, (16u - m) & 15u);
-                const int32_t b0 = (int32_t)(16 * p) - (int32_t)m;
-                uint8_t* dst = data + a0 + 16ull * p;
-                if (b0 >= 0 && b0 + 16 <= (int32_t)ds) {
-                    if (PPFS_DBG_OK(dst, 16, data, nblocks_all * ds))
-                        gst16(dst, oo);
-                } else if (b0 < (int32_t)ds && b0 + 16 > 0
-                    && PPFS_DBG_OK(dst + (b0 < 0 ? -b0 : 0), (b0 + 16 > (int32_t)ds ? (int32_t)ds - b0 : 16) - (b0 < 0 ? -b0 : 0),
-                        data, nblocks_all * ds)) {
-                    const uint32_t w[4] = { oo.x, oo.y, oo.z, oo.w };
-                    store_piece_part(dst, w, b0 < 0 ? (uint32_t)(-b0) : 0u,
-                        b0 + 16 > (int32_t)ds ? (uint32_t)((int32_t)ds - b0) : 16u);
-                }
-            }
-        }
-        if (BF_PREFETCH) {
+        if (!PPFS_CRC_CHK_EARLY_ST)
+            emit();
+        if (CRC_CHK_PF) {
 #pragma unroll
             for (int k = 0; k < NP; ++k)
                 R[k] = N[k];
