@@ -506,7 +506,7 @@ def main(argv=None):
     red_dev = red_dev or dev
     # Every launch of the run goes to one created stream, not the legacy null stream (which orders
     # each launch against the other blocking streams): 0-1.7 % per step across two boxes
-    # (tools/overlap_probe.py; running consecutive steps on two streams gained nothing either).
+    # (tools/probes/overlap_probe.py; running consecutive steps on two streams gained nothing either).
     torch.cuda.set_stream(torch.cuda.Stream(dev))
 
     from paritypartyfs_amd import ECC_REED_SOLOMON, EccEngine, device_copy, pinned

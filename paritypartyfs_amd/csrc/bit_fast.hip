@@ -702,6 +702,10 @@ __global__ __launch_bounds__(64 * WV) void parity_fast_encode_kernel(const uint8
     }
 }
 
+// Parity check: the payload output stored before the parity reduction (A/B knob)
+#ifndef PPFS_PAR_CHK_EARLY_ST
+#define PPFS_PAR_CHK_EARLY_ST 0
+#endif
 template <int NP, int WV>
 __global__ __launch_bounds__(64 * WV) void parity_fast_check_kernel(const uint8_t* __restrict__ raw,
     uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks_all, ParFast a)
@@ -723,6 +727,37 @@ __global__ __launch_bounds__(64 * WV) void parity_fast_check_kernel(const uint8_
 #pragma unroll
             for (int k = 0; k < NP; ++k)
                 N[k] = gld16c(raw + nx * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
+        auto emit = [&]() {
+            if (data) {
+                // payload byte x = raw byte x; output pieces on the payload's global 16-byte grid:
+                // piece p holds raw bytes [16 p - m, +16) = tail of raw piece p-1 + head of raw piece p
+                const uint64_t start = blk * ds, a0 = start & ~15ull;
+                const uint32_t m = (uint32_t)(start - a0);
+#pragma unroll
+                for (int k = 0; k <= NP; ++k) {
+                    const uint32_t p = 64u * k + lane;
+                    const uint4 own = k < NP ? R[k] : make_uint4(0, 0, 0, 0);
+                    const uint4 prev = k == 0 ? prev_piece<true>(own, own) : prev_piece<false>(own, R[k > 0 ? k - 1 : 0]);
+                    // bytes [16 - m, 16) of prev then [0, 16 - m) of own
+                    const uint4 o = shift_pieces(prev, own, (16u - m) & 15u);
+                    const uint4 oo = m == 0 ? own : o;
+                    const int32_t b0 = (int32_t)(16 * p) - (int32_t)m;
+                    uint8_t* dst = data + a0 + 16ull * p;
+                    if (b0 >= 0 && b0 + 16 <= (int32_t)ds) {
+                        if (PPFS_DBG_OK(dst, 16, data, nblocks_all * ds))
+                            gst16(dst, oo);
+                    } else if (b0 < (int32_t)ds && b0 + 16 > 0
+                        && PPFS_DBG_OK(dst + (b0 < 0 ? -b0 : 0), (b0 + 16 > (int32_t)ds ? (int32_t)ds - b0 : 16) - (b0 < 0 ? -b0 : 0),
+                            data, nblocks_all * ds)) {
+                        const uint32_t w[4] = { oo.x, oo.y, oo.z, oo.w };
+                        store_piece_part(dst, w, b0 < 0 ? (uint32_t)(-b0) : 0u,
+                            b0 + 16 > (int32_t)ds ? (uint32_t)((int32_t)ds - b0) : 16u);
+                    }
+                }
+            }
+        };
+        if (PPFS_PAR_CHK_EARLY_ST)
+            emit();
         uint32_t ones = 0;
 #pragma unroll
         for (int k = 0; k < NP; ++k)
@@ -731,33 +766,8 @@ __global__ __launch_bounds__(64 * WV) void parity_fast_check_kernel(const uint8_
         const uint32_t odd = wave_xor(ones & 1u);
         if (status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
             status[blk] = odd ? 5 : 0;
-        if (data) {
-            // payload byte x = raw byte x; output pieces on the payload's global 16-byte grid:
-            // piece p holds raw bytes [16 p - m, +16) = tail of raw piece p-1 + head of raw piece p
-            const uint64_t start = blk * ds, a0 = start & ~15ull;
-            const uint32_t m = (uint32_t)(start - a0);
-#pragma unroll
-            for (int k = 0; k <= NP; ++k) {
-                const uint32_t p = 64u * k + lane;
-                const uint4 own = k < NP ? R[k] : make_uint4(0, 0, 0, 0);
-                const uint4 prev = k == 0 ? prev_piece<true>(own, own) : prev_piece<false>(own, R[k > 0 ? k - 1 : 0]);
-                // bytes [16 - m, 16) of prev then [0, 16 - m) of own
-                const uint4 o = shift_pieces(prev, own, (16u - m) & 15u);
-                const uint4 oo = m == 0 ? own : o;
-                const int32_t b0 = (int32_t)(16 * p) - (int32_t)m;
-                uint8_t* dst = data + a0 + 16ull * p;
-                if (b0 >= 0 && b0 + 16 <= (int32_t)ds) {
-                    if (PPFS_DBG_OK(dst, 16, data, nblocks_all * ds))
-                        gst16(dst, oo);
-                } else if (b0 < (int32_t)ds && b0 + 16 > 0
-                    && PPFS_DBG_OK(dst + (b0 < 0 ? -b0 : 0), (b0 + 16 > (int32_t)ds ? (int32_t)ds - b0 : 16) - (b0 < 0 ? -b0 : 0),
-                        data, nblocks_all * ds)) {
-                    const uint32_t w[4] = { oo.x, oo.y, oo.z, oo.w };
-                    store_piece_part(dst, w, b0 < 0 ? (uint32_t)(-b0) : 0u,
-                        b0 + 16 > (int32_t)ds ? (uint32_t)((int32_t)ds - b0) : 16u);
-                }
-            }
-        }
+        if (!PPFS_PAR_CHK_EARLY_ST)
+            emit();
         if (BF_PREFETCH) {
 #pragma unroll
             for (int k = 0; k < NP; ++k)
@@ -1249,7 +1259,7 @@ template <typename K> static uint32_t bf_grid(K, uint64_t nb, int wv = bf::WAVES
 
 // Waves per workgroup of the Hamming and parity kernels (each wave owns its blocks and its LDS
 // buffer: no workgroup barrier).  Round 5: a wave-per-4-KiB-block copy with no coding work
-// (tools/stream_ceiling.hip, r5ce_*) moves 6.5-6.6 TB/s in one-wave workgroups at 6-8 waves per
+// (tools/probes/stream_ceiling.hip, r5ce_*) moves 6.5-6.6 TB/s in one-wave workgroups at 6-8 waves per
 // CU against 5.9-6.2 TB/s in 4-wave workgroups at any cap -- fewer bytes in flight, and a freed
 // wave slot refills at once.  Measured on the kernels (configs leg, r5wv_* / r5wv2_*, two rounds):
 // parity encode in one-wave workgroups at 12 waves per CU 1.323-1.325 vs 1.393-1.398 ms (10: 1.338,

@@ -49,7 +49,7 @@ template <int T2, int NSEG_ = 0> struct RsCfg {
     static constexpr int W = T2 <= 8 ? 2 : (T2 <= 16 ? 4 : 8); // remainder words (top aligned)
     // independent remainder chains per lane (segments of 256/NSEG bytes), combined with
     // x^64 / x^128 map tables: more LDS reads in flight per wave
-    // measured on MI355X (tools/rs_ablate.hip): one chain per lane is fastest at 2 waves/SIMD
+    // measured on MI355X (tools/probes/rs_ablate.hip): one chain per lane is fastest at 2 waves/SIMD
     static constexpr int NSEG = NSEG_ ? NSEG_ : 1;
     static constexpr int SEGL = 256 / NSEG;
     static constexpr int SLICE_BYTES = W <= 4 ? 4096 : 8192;    // 16 nibble tables x 16 x 16 B (x2)

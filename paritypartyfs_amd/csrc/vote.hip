@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* __restr
 // ---- device copy at the HBM ceiling (measurement reference for bench.py's roofline) ----
 // One thread per 16 bytes over a full grid (workgroups dispatched in address order: one
 // contiguous window of HBM in flight), plain 16-byte loads and stores; ragged ends by bytes.
-// The same shape reached 6.26 TB/s on 8.6 GB (tools/stream_ablate4.hip).
+// The same shape reached 6.26 TB/s on 8.6 GB (tools/probes/stream_ablate4.hip).
 namespace ppfs {
 __global__ __launch_bounds__(256) void copy16_kernel(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
     uint64_t n16, uint64_t head, uint64_t bytes)
@@ -178,7 +178,7 @@ extern "C" hipError_t ppfs_inject_launch(uint8_t* raw, uint64_t stride, uint64_t
 // Completion flag of the small-batch launch path (api.cpp wait_flag): queued after a call's
 // kernels on the same stream, it makes their outputs visible system-wide and stores `v` (release)
 // into host-coherent memory, where the host spins on it.  Cheaper than hipStreamSynchronize's
-// completion signal (measured 6.4 vs 10.3 us for one empty kernel, tools/latency_probe.cpp).
+// completion signal (measured 6.4 vs 10.3 us for one empty kernel, tools/probes/latency_probe.cpp).
 namespace ppfs {
 __global__ __launch_bounds__(64) void flag_kernel(uint32_t* flag, uint32_t v)
 {

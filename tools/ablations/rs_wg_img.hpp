@@ -11,7 +11,7 @@ namespace wg {
 // The tile is DMA'd straight into the OUTPUT layout: codeword j of the tile at LDS IMG + 255 j,
 // payload at IMG + 255 j + 2t.  Output piece i (16 bytes at image offset 16 i) takes its payload
 // bytes from tile payload offset 16 i - 2t (b + 1), b = the block of the piece's last byte; the
-// LDS-DMA reads that source at any byte alignment (checked on gfx950: tools/dma_align_test.hip).
+// LDS-DMA reads that source at any byte alignment (checked on gfx950: tools/probes/dma_align_test.hip).
 // Two kinds of pieces cannot be one contiguous source and are assembled in registers instead:
 // piece 0 (block 0's parity, then its payload from offset 0) and the pieces in which block b's
 // 2t parity bytes sit between the tail of block b-1's payload and the head of block b's.  After the

@@ -7,7 +7,7 @@ P=paritypartyfs_amd/_lib/libppfs_ecc.so
 for r in 1 2; do
   for lib in $L/libppfs_ecc_4stream.so $P; do
     for ft in "" "--from-torch"; do
-      PPFS_ECC_LIB=$lib timeout -k 10 300 python tools/host_path_probe.py --modes pinned,pageable --reps 3 $ft > gpurun_out/r5h_tmp.jsonl 2>gpurun_out/r5h_probe.err || { tail -5 gpurun_out/r5h_probe.err; exit 1; }
+      PPFS_ECC_LIB=$lib timeout -k 10 300 python tools/probes/host_path_probe.py --modes pinned,pageable --reps 3 $ft > gpurun_out/r5h_tmp.jsonl 2>gpurun_out/r5h_probe.err || { tail -5 gpurun_out/r5h_probe.err; exit 1; }
       python3 -c "import json,sys; [print(json.dumps({'lib': sys.argv[1], 'torch': sys.argv[2] != '', 'round': int(sys.argv[3]), **json.loads(l)})) for l in open(sys.argv[4])]" $(basename $lib) "$ft" $r gpurun_out/r5h_tmp.jsonl >> gpurun_out/r5h_host_ab.jsonl
     done
   done

@@ -8,7 +8,7 @@ for r in 1 2; do
   for v in "spawn 4" "pool 4" "pool 8" "pool 12" "pool 16"; do
     set -- $v
     lib=$P; [ $1 = spawn ] && lib=$L/libppfs_ecc_spawn.so
-    PPFS_ECC_COPY_THREADS=$2 PPFS_ECC_LIB=$lib timeout -k 10 300 python tools/host_path_probe.py --modes pageable --reps 3 --from-torch > gpurun_out/r5i_tmp.jsonl 2>gpurun_out/r5i_probe.err || { tail -5 gpurun_out/r5i_probe.err; exit 1; }
+    PPFS_ECC_COPY_THREADS=$2 PPFS_ECC_LIB=$lib timeout -k 10 300 python tools/probes/host_path_probe.py --modes pageable --reps 3 --from-torch > gpurun_out/r5i_tmp.jsonl 2>gpurun_out/r5i_probe.err || { tail -5 gpurun_out/r5i_probe.err; exit 1; }
     python3 -c "import json,sys; [print(json.dumps({'variant': sys.argv[1], 'threads': int(sys.argv[2]), 'round': int(sys.argv[3]), **json.loads(l)})) for l in open(sys.argv[4])]" $1 $2 $r gpurun_out/r5i_tmp.jsonl >> gpurun_out/r5i_pageable_ab.jsonl
   done
 done

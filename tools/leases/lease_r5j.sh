@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 cat gpurun_out/r5j_cpu.txt
 for r in 1 2; do
   for n in 6 8 10 12 14; do
-    PPFS_ECC_COPY_THREADS=$n timeout -k 10 300 python tools/host_path_probe.py --modes pageable --reps 3 --from-torch > gpurun_out/r5j_tmp.jsonl 2>gpurun_out/r5j_probe.err || { tail -5 gpurun_out/r5j_probe.err; exit 1; }
+    PPFS_ECC_COPY_THREADS=$n timeout -k 10 300 python tools/probes/host_path_probe.py --modes pageable --reps 3 --from-torch > gpurun_out/r5j_tmp.jsonl 2>gpurun_out/r5j_probe.err || { tail -5 gpurun_out/r5j_probe.err; exit 1; }
     python3 -c "import json,sys; [print(json.dumps({'threads': int(sys.argv[1]), 'round': int(sys.argv[2]), **json.loads(l)})) for l in open(sys.argv[3])]" $n $r gpurun_out/r5j_tmp.jsonl >> gpurun_out/r5j_pageable_threads.jsonl
   done
 done

@@ -6,7 +6,7 @@ L=paritypartyfs_amd/_lib/lease
 P=paritypartyfs_amd/_lib/libppfs_ecc.so
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_gpu_block_device.py -k "ham" > gpurun_out/r5n_pytest.log 2>&1; rc=$?; tail -2 gpurun_out/r5n_pytest.log; [ $rc -eq 0 ] || exit $rc
 for lib in $L/libppfs_ecc_base.so $P; do
-  PPFS_ECC_LIB=$lib timeout -k 10 300 python tools/wb_probe.py --only hamming > gpurun_out/r5n_tmp.jsonl 2>gpurun_out/r5n_probe.err || { tail -5 gpurun_out/r5n_probe.err; exit 1; }
+  PPFS_ECC_LIB=$lib timeout -k 10 300 python tools/probes/wb_probe.py --only hamming > gpurun_out/r5n_tmp.jsonl 2>gpurun_out/r5n_probe.err || { tail -5 gpurun_out/r5n_probe.err; exit 1; }
   echo "$(basename $lib) $(cat gpurun_out/r5n_tmp.jsonl)" | tee -a gpurun_out/r5n_wb_probe.txt
 done
 for r in 1 2; do

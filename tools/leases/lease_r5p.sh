@@ -7,7 +7,7 @@ for f in /sys/bus/pci/devices/*; do v=$(cat $f/vendor 2>/dev/null); c=$(cat $f/c
 timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_parity.py -k "host" > gpurun_out/r5p_pytest.log 2>&1; rc=$?; tail -2 gpurun_out/r5p_pytest.log; [ $rc -eq 0 ] || exit $rc
 for r in 1 2; do
   for numa in 0 1; do
-    PPFS_ECC_COPY_NUMA=$numa timeout -k 10 300 python tools/host_path_probe.py --modes pageable --reps 3 --from-torch > gpurun_out/r5p_tmp.jsonl 2>gpurun_out/r5p_probe.err || { tail -5 gpurun_out/r5p_probe.err; exit 1; }
+    PPFS_ECC_COPY_NUMA=$numa timeout -k 10 300 python tools/probes/host_path_probe.py --modes pageable --reps 3 --from-torch > gpurun_out/r5p_tmp.jsonl 2>gpurun_out/r5p_probe.err || { tail -5 gpurun_out/r5p_probe.err; exit 1; }
     python3 -c "import json,sys; [print(json.dumps({'numa': int(sys.argv[1]), 'round': int(sys.argv[2]), **json.loads(l)})) for l in open(sys.argv[3])]" $numa $r gpurun_out/r5p_tmp.jsonl >> gpurun_out/r5p_numa_ab.jsonl
   done
 done

@@ -10,7 +10,7 @@ per (operation, memory kind).
 --devices 0,0,...: run encode / decode through an EccGroup (ppfs_ecc_group_*: contiguous shards,
 one host thread per listed device; the scrub rows are single-context).
 
-usage: python3 tools/bench_host.py [--blocks N] [--reps R] [--devices D0,D1,...]
+usage: python3 tools/probes/bench_host.py [--blocks N] [--reps R] [--devices D0,D1,...]
 """
 import argparse
 import json
@@ -20,7 +20,7 @@ import time
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():

@@ -1,7 +1,7 @@
 // dma_align_test.hip -- does global_load_lds_dwordx4 (LDS-DMA) accept a global source address that
 // is not 16- / 4-byte aligned on gfx950?  One workgroup: 64 lanes each DMA 16 bytes from
 // src + misalign + 16 * lane into LDS, then copy LDS out; the host compares against the source.
-// Build: hipcc --offload-arch=gfx950 -O2 tools/dma_align_test.hip -o tools/dma_align_test.bin
+// Build: hipcc --offload-arch=gfx950 -O2 tools/probes/dma_align_test.hip -o tools/dma_align_test.bin
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

@@ -2,7 +2,7 @@
 2^20 blocks of one config, pageable and page-locked caller buffers, each call timed `--reps` times
 (bench.py's host_inclusive leg times one call of each).  Prints one JSON line per (mode, op) with
 every rep's GiB/s (algorithmic bytes: data + codeword per block).  Diagnostic, not shipped:
-    python tools/host_path_probe.py [--block-size 512 --t 3 --reps 5 --modes pinned,pageable]
+    python tools/probes/host_path_probe.py [--block-size 512 --t 3 --reps 5 --modes pinned,pageable]
 """
 import argparse
 import json
@@ -12,7 +12,7 @@ import time
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 from paritypartyfs_amd import ECC_REED_SOLOMON, EccEngine, pinned  # noqa: E402
 

@@ -6,7 +6,7 @@ injection runs beside batch k-1's decode.  Prints one JSON line per form (ms per
   pipe  S1: encode(X_k), decode(X_{k-1});  S2: inject(X_k) after encode(X_k); the decode of X_k
         waits for its injection (fence-free HIP events for the cross-stream waits)
 
-usage: python tools/inject_overlap_probe.py [--steps 40] [--block-size 512 --t 3]
+usage: python tools/probes/inject_overlap_probe.py [--steps 40] [--block-size 512 --t 3]
 """
 import argparse
 import ctypes
@@ -15,7 +15,7 @@ import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 

@@ -2,7 +2,7 @@
 """Standalone kernel timings of one engine build (PPFS_ECC_LIB), without output checks, for
 ablation builds whose outputs are wrong on purpose (rs_wg.hpp MODE bits, tools/build_alt.sh).
 
-usage: PPFS_ECC_LIB=... python tools/kernel_ablate.py [--block-size 512 --t 3] [--tag name]
+usage: PPFS_ECC_LIB=... python tools/probes/kernel_ablate.py [--block-size 512 --t 3] [--tag name]
 Prints one JSON line: median ms of L back-to-back launches, hot (same buffers) and cold (4 rotating
 buffer sets), for encode and clean decode (status + write-back on).
 """
@@ -14,7 +14,7 @@ import time
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 

@@ -1,6 +1,6 @@
 // latency_probe.cpp -- where does a per-block readBlock / writeBlock spend its time?
-// Build: hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/latency_probe.cpp -I include
-//            -L paritypartyfs_amd/_lib -lppfs_ecc -Wl,-rpath,$PWD/paritypartyfs_amd/_lib -o tools/latency_probe.bin
+// Build: hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/probes/latency_probe.cpp -I include
+//            -L paritypartyfs_amd/_lib -lppfs_ecc -Wl,-rpath,$PWD/paritypartyfs_amd/_lib -o tools/probes/latency_probe.bin
 // Prints one JSON line per probe: median / p10 / p90 microseconds over N calls.
 #include <hip/hip_runtime.h>
 

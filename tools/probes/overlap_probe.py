@@ -3,7 +3,7 @@
 throughput of the encode + inject + decode step?  Prints one JSON line: ms per step with one stream
 (the bench's form) and with the steps alternating over two streams, both verified.
 
-usage: python tools/overlap_probe.py [--steps 40] [--blocks 1048576]
+usage: python tools/probes/overlap_probe.py [--steps 40] [--blocks 1048576]
 """
 import argparse
 import json
@@ -11,7 +11,7 @@ import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
 

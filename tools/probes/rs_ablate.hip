@@ -1,7 +1,7 @@
 // rs_ablate.hip -- diagnostic build (not shipped): RS(255,249) encode/decode variants timed in
 // one process on random data (interleaved rounds, median).  Variant knobs: NSEG (independent
 // remainder chains per lane) and PF (prefetch next tile into VGPRs during compute).
-// hipcc --offload-arch=gfx950 -O3 -std=c++17 -I paritypartyfs_amd/csrc tools/rs_ablate.hip -o tools/rs_ablate.bin
+// hipcc --offload-arch=gfx950 -O3 -std=c++17 -I paritypartyfs_amd/csrc tools/probes/rs_ablate.hip -o tools/rs_ablate.bin
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

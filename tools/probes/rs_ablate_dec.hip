@@ -2,7 +2,7 @@
 // in one process on real codewords carrying one byte error each (the bench workload); every
 // variant's payload output is checked against the original data.
 // hipcc --offload-arch=gfx950 -O3 -std=c++17 -I paritypartyfs_amd/csrc -I include \
-//     tools/rs_ablate_dec.hip -o tools/rs_ablate_dec.bin
+//     tools/probes/rs_ablate_dec.hip -o tools/rs_ablate_dec.bin
 #include "../paritypartyfs_amd/csrc/api.cpp" // host table builders (same TU: anonymous namespace)
 #include "rs_fast.hpp"
 

@@ -3,7 +3,7 @@
 // (and, variant 2, 255 payload bytes the kernel reads and 249 it writes back), one lane of the
 // resident workgroup polls for it, the workgroup answers with a system-scope release store.
 // The kernel exits on a stop flag, after 200 ms without a request, or after 2 s in any case.
-// Build: hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/server_probe.cpp -o tools/server_probe.bin
+// Build: hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/probes/server_probe.cpp -o tools/server_probe.bin
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -4,7 +4,7 @@
 // wave-tile) without any coding work:
 //   copy_flat      grid-stride 16 B/lane copy of the same total bytes (reference ceiling)
 //   tile_regs<D,L> persistent wave-tiles through VGPRs, prefetch depth D (1 or 2), L = LDS round trip
-// hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/stream_ablate.hip -o tools/stream_ablate.bin
+// hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probes/stream_ablate.hip -o tools/stream_ablate.bin
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -6,7 +6,7 @@
 //                    CH = 16 KiB every wave streams its own contiguous 16 KiB (the RS tile walk) and
 //                    at CH = 1 KiB concurrent waves cover one contiguous region (flat-copy-like).
 //                    PERS = persistent grid (2 WG/CU) vs one iteration per wave.
-// hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/stream_ablate2.hip -o tools/stream_ablate2.bin
+// hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probes/stream_ablate2.hip -o tools/stream_ablate2.bin
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -7,7 +7,7 @@
 //   ro_wave_st<...>      the same plus one status byte per block (the CRC check's output)
 //   ro_flat<NT>          grid-stride 4 x 16 B per thread, 8 workgroups of 256 per CU
 //   cp_wave<NTL,NTS>     copy: a wave per block, 4 x 16 B in, 4 x 16 B out (the encode's shape)
-// hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/stream_ceiling.hip -o tools/stream_ceiling.bin
+// hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probes/stream_ceiling.hip -o tools/stream_ceiling.bin
 // usage: stream_ceiling [blocks=1048576] [reps=20]   (one JSON line per variant)
 #include <hip/hip_runtime.h>
 

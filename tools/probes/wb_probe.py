@@ -7,7 +7,7 @@ median kernel time of the decode (dispatch-packet events, tools/bench_configs.ti
   err          encode, injection                         -> decode (write-back)   [bench_configs]
   err_nowb     encode, injection                         -> decode (no write-back)
   err_flush    encode, injection, 1 GiB unrelated copy   -> decode (write-back)
-Diagnostic, not shipped:  python tools/wb_probe.py [--only hamming|rs3|rs16]
+Diagnostic, not shipped:  python tools/probes/wb_probe.py [--only hamming|rs3|rs16]
 """
 import argparse
 import json
@@ -16,7 +16,7 @@ import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 
 def main():
