@@ -1061,11 +1061,10 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ENC_ATTR void crc_fast_encode_ker
             // every raw piece but the block's last (lane 63, piece NP - 1: the CRC field)
 #pragma unroll
             for (int k = 0; k < NP; ++k) {
-                if (k == NP - 1 && lane == 63)
-                    continue;
+                // every lane shifts (the neighbour pieces are whole-wave DPP moves); lane 63 skips the store
                 const uint4 nb = next_piece(cur.v[k], cur.v[k + 1]);
                 const uint4 o = shift_pieces(cur.v[k], nb, m);
-                if (PPFS_DBG_OK(rb + 16u * (64u * k + lane), 16, raw, nblocks_all * a.bs))
+                if (!(k == NP - 1 && lane == 63) && PPFS_DBG_OK(rb + 16u * (64u * k + lane), 16, raw, nblocks_all * a.bs))
                     gst16_raw(rb + 16u * (64u * k + lane), o);
             }
         }
@@ -1090,8 +1089,6 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ENC_ATTR void crc_fast_encode_ker
                 old_last = rb[a.ds + a.nbc - 1];
 #pragma unroll
             for (int k = PPFS_CRC_ENC_EARLY_ST ? NP - 1 : 0; k < NP; ++k) {
-                if (PPFS_CRC_ENC_EARLY_ST && lane != 63)
-                    break;
                 const uint4 nb = next_piece(cur.v[k], cur.v[k + 1]);
                 uint4 o = shift_pieces(cur.v[k], nb, m);
                 if (k == NP - 1 && lane == 63) {
@@ -1104,7 +1101,7 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ENC_ATTR void crc_fast_encode_ker
                     const uint32_t keep = rbits ? ((1u << (8u - rbits)) - 1u) << 24 : 0u; // old low bits
                     o.w = (o.w & ~fmask) | field | ((old_last << 24) & keep);
                 }
-                if (PPFS_DBG_OK(rb + 16u * (64u * k + lane), 16, raw, nblocks_all * a.bs))
+                if ((!PPFS_CRC_ENC_EARLY_ST || lane == 63) && PPFS_DBG_OK(rb + 16u * (64u * k + lane), 16, raw, nblocks_all * a.bs))
                     gst16_raw(rb + 16u * (64u * k + lane), o);
             }
         }
