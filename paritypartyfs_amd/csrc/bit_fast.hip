@@ -134,6 +134,11 @@ __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32
 // Hamming decode: the LDS image stores issued before the syndrome reduction (1, round 5), so they
 // complete under its DPP chain, or after it, only for blocks with a payload output (0).  Configs leg,
 // 3 interleaved rounds (r5hei): clean 1.512-1.523 vs 1.531 ms, 1-error 1.582-1.590 vs 1.588-1.602 ms.
+// Status bytes and corrected-byte write-backs of the Hamming decode and the CRC / parity checks
+// stored after the payload emission (1) instead of before it (0, A/B knob)
+#ifndef PPFS_BF_LATE_ST
+#define PPFS_BF_LATE_ST 0
+#endif
 #ifndef PPFS_HAM_DEC_EARLY_IMG
 #define PPFS_HAM_DEC_EARLY_IMG 1
 #endif
@@ -513,7 +518,7 @@ __global__ __launch_bounds__(64 * WV) void ham_fast_decode_kernel(uint8_t* __res
         const bool owner = par && ((S >> 7) & 63u) == lane;
         if (!data && owner && write_back && PPFS_DBG_OK(rb + (S >> 3), 1, raw, nblocks_all * a.bs))
             rb[S >> 3] = (uint8_t)(rb[S >> 3] ^ (0x80u >> (S & 7u)));
-        if (status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
+        if (!PPFS_BF_LATE_ST && status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
             status[blk] = (uint8_t)st;
         if (data && st != 5) {
             if (!PPFS_HAM_DEC_EARLY_IMG) {
@@ -527,7 +532,7 @@ __global__ __launch_bounds__(64 * WV) void ham_fast_decode_kernel(uint8_t* __res
             if (owner) {
                 __hip_atomic_fetch_xor((uint32_t*)(img + ((S >> 5) << 2)), 0x80u << (8 * ((S >> 3) & 3u)) >> (S & 7u),
                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (write_back && PPFS_DBG_OK(rb + (S >> 3), 1, raw, nblocks_all * a.bs))
+                if (!PPFS_BF_LATE_ST && write_back && PPFS_DBG_OK(rb + (S >> 3), 1, raw, nblocks_all * a.bs))
                     rb[S >> 3] = img[S >> 3]; // the corrected byte (same lane: after its flip)
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -582,7 +587,11 @@ __global__ __launch_bounds__(64 * WV) void ham_fast_decode_kernel(uint8_t* __res
                 ham_mid_piece(img, (uint32_t)b0, o);
                 store(p, b0, o);
             }
+            if (PPFS_BF_LATE_ST && owner && write_back && PPFS_DBG_OK(rb + (S >> 3), 1, raw, nblocks_all * a.bs))
+                rb[S >> 3] = img[S >> 3];
         }
+        if (PPFS_BF_LATE_ST && status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
+            status[blk] = (uint8_t)st;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         (void)lastw;
@@ -764,10 +773,12 @@ __global__ __launch_bounds__(64 * WV) void parity_fast_check_kernel(const uint8_
             ones += __builtin_popcount(R[k].x) + __builtin_popcount(R[k].y) + __builtin_popcount(R[k].z)
                 + __builtin_popcount(R[k].w);
         const uint32_t odd = wave_xor(ones & 1u);
-        if (status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
+        if (!PPFS_BF_LATE_ST && status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
             status[blk] = odd ? 5 : 0;
         if (!PPFS_PAR_CHK_EARLY_ST)
             emit();
+        if (PPFS_BF_LATE_ST && status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
+            status[blk] = odd ? 5 : 0;
         if (BF_PREFETCH) {
 #pragma unroll
             for (int k = 0; k < NP; ++k)
@@ -1224,10 +1235,12 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ATTR void crc_fast_check_kernel(c
             f = (f << 8) | ((lw[b >> 2] >> (8 * (b & 3))) & 0xFFu);
         }
         const uint32_t field = (uint32_t)(f >> (8 * a.nbc - a.n));
-        if (status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
+        if (!PPFS_BF_LATE_ST && status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
             status[blk] = (st == field) ? 0 : 5;
         if (!PPFS_CRC_CHK_EARLY_ST)
             emit();
+        if (PPFS_BF_LATE_ST && status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
+            status[blk] = (st == field) ? 0 : 5;
         if (CRC_CHK_PF) {
 #pragma unroll
             for (int k = 0; k < NP; ++k)
