@@ -135,9 +135,11 @@ __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32
 // complete under its DPP chain, or after it, only for blocks with a payload output (0).  Configs leg,
 // 3 interleaved rounds (r5hei): clean 1.512-1.523 vs 1.531 ms, 1-error 1.582-1.590 vs 1.588-1.602 ms.
 // Status bytes and corrected-byte write-backs of the Hamming decode and the CRC / parity checks
-// stored after the payload emission (1) instead of before it (0, A/B knob)
+// stored after the payload emission (1, round 5) instead of before it (0).  Configs leg, 3
+// interleaved rounds (r5late): parity check 1.439-1.441 vs 1.467-1.469 ms, Hamming 1-error
+// 1.576-1.579 vs 1.578-1.587 ms, clean 1.500-1.511 vs 1.509-1.513, CRC check within noise.
 #ifndef PPFS_BF_LATE_ST
-#define PPFS_BF_LATE_ST 0
+#define PPFS_BF_LATE_ST 1
 #endif
 #ifndef PPFS_HAM_DEC_EARLY_IMG
 #define PPFS_HAM_DEC_EARLY_IMG 1

@@ -76,6 +76,11 @@ __device__ uint64_t g_bs_trace[4096 * BS_TRACE_N];
 #ifndef PPFS_BS_EPRIO
 #define PPFS_BS_EPRIO 1
 #endif
+// Decode: a block's status byte stored after the tile's emission (1) instead of right after its
+// correction (0, A/B knob)
+#ifndef PPFS_BS_LATE_ST
+#define PPFS_BS_LATE_ST 0
+#endif
 #ifndef PPFS_BS_EMIT_G
 #define PPFS_BS_EMIT_G 4 // decode emission: output pieces read from LDS together (4: +0.5 % cfg5 step, r3p)
 #endif
@@ -677,7 +682,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
         const uint64_t gblk = t * TBW + Ln.blk;
         const uint32_t st = bs_correct<T2>(
             lds, gfp, s12p, xpm, row, Ln.c, s, true, raw, gblk, wb, nblocks * 255u PPFS_BS_TR_ARGS);
-        if (status && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
+        if (!PPFS_BS_LATE_ST && status && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
             status[gblk] = (uint8_t)st;
         wave_fence(); // corrections patched into the image rows
         if constexpr (PPFS_BS_PRIO == 1)
@@ -717,6 +722,8 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
                 }
             }
         }
+        if (PPFS_BS_LATE_ST && status && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
+            status[gblk] = (uint8_t)st;
         PPFS_BS_MARK(7);
         if constexpr (PPFS_BS_PRIO == 2)
             __builtin_amdgcn_s_setprio(0);
