@@ -81,6 +81,11 @@ __device__ uint64_t g_bs_trace[4096 * BS_TRACE_N];
 #ifndef PPFS_BS_LATE_ST
 #define PPFS_BS_LATE_ST 0
 #endif
+// Decode: a single error's write-back to HBM deferred to after the tile's emission (1; the LDS row
+// is still patched before it) or stored at once (0, A/B knob)
+#ifndef PPFS_BS_LATE_WB
+#define PPFS_BS_LATE_WB 0
+#endif
 #ifndef PPFS_BS_EMIT_G
 #define PPFS_BS_EMIT_G 4 // decode emission: output pieces read from LDS together (4: +0.5 % cfg5 step, r3p)
 #endif
@@ -273,8 +278,9 @@ __device__ __noinline__ void bs_correct_general(uint8_t* lds, const uint8_t* gfp
 template <int T2>
 __device__ __forceinline__ uint32_t bs_correct(uint8_t* lds, const uint8_t* gfp, const uint8_t* s12p, const uint8_t* __restrict__ xp,
     uint32_t row, uint32_t c, const uint32_t (&s)[4], bool valid, uint8_t* __restrict__ raw_g, uint64_t gblk,
-    bool wb, uint64_t raw_bytes PPFS_BS_TR_PARAMS)
+    bool wb, uint64_t raw_bytes, uint32_t& dpos, uint32_t& dval PPFS_BS_TR_PARAMS)
 {
+    dpos = ~0u;
     const bool err = valid && pair::pair_or<1>(s[0] | s[1] | s[2] | s[3]) != 0u;
     if (!__builtin_amdgcn_ballot_w64(err))
         return 0u;
@@ -320,8 +326,19 @@ __device__ __forceinline__ uint32_t bs_correct(uint8_t* lds, const uint8_t* gfp,
     }
     const bool geo = err && pair::pair_or<1>(bad) == 0u;
     PPFS_BS_MARK(4);
-    if (geo && c == 0)
-        col::col_fix(lds, row, raw_g, gblk, wb, lx, gf.exp(le), raw_bytes);
+    if (geo && c == 0) {
+        if constexpr (PPFS_BS_LATE_WB) {
+            const uint32_t ev = gf.exp(le);
+            if (ev) {
+                const uint8_t fixed = (uint8_t)(lds[row + lx] ^ ev);
+                lds[row + lx] = fixed;
+                dpos = lx;
+                dval = fixed;
+            }
+        } else {
+            col::col_fix(lds, row, raw_g, gblk, wb, lx, gf.exp(le), raw_bytes);
+        }
+    }
     if (err && !geo)
         bs_correct_general<T2>(lds, gfp, row, c, s[0], s[1], s[2], s[3], raw_g, gblk, wb, raw_bytes);
     PPFS_BS_MARK(5);
@@ -680,8 +697,9 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
         if constexpr (PPFS_BS_PRIO == 1 || PPFS_BS_PRIO == 2 || PPFS_BS_PRIO == 4)
             __builtin_amdgcn_s_setprio(2);
         const uint64_t gblk = t * TBW + Ln.blk;
+        uint32_t dpos, dval = 0;
         const uint32_t st = bs_correct<T2>(
-            lds, gfp, s12p, xpm, row, Ln.c, s, true, raw, gblk, wb, nblocks * 255u PPFS_BS_TR_ARGS);
+            lds, gfp, s12p, xpm, row, Ln.c, s, true, raw, gblk, wb, nblocks * 255u, dpos, dval PPFS_BS_TR_ARGS);
         if (!PPFS_BS_LATE_ST && status && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
             status[gblk] = (uint8_t)st;
         wave_fence(); // corrections patched into the image rows
@@ -722,6 +740,8 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
                 }
             }
         }
+        if (PPFS_BS_LATE_WB && wb && dpos != ~0u && PPFS_DBG_OK(raw + gblk * 255u + dpos, 1, raw, nblocks * 255u))
+            wb_byte(raw + gblk * 255u + dpos, (uint8_t)dval);
         if (PPFS_BS_LATE_ST && status && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
             status[gblk] = (uint8_t)st;
         PPFS_BS_MARK(7);
@@ -752,8 +772,11 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
         bs_cmodg(s, lds, row, Ln);
         const bool valid = Ln.blk < nb;
         const uint64_t gblk = t * TBW + Ln.blk;
+        uint32_t dpos, dval = 0;
         const uint32_t st = bs_correct<T2>(
-            lds, gfp, s12p, xpm, row, Ln.c, s, valid, raw, gblk, wb, nblocks * 255u PPFS_BS_TR_ARGS);
+            lds, gfp, s12p, xpm, row, Ln.c, s, valid, raw, gblk, wb, nblocks * 255u, dpos, dval PPFS_BS_TR_ARGS);
+        if (PPFS_BS_LATE_WB && valid && wb && dpos != ~0u && PPFS_DBG_OK(raw + gblk * 255u + dpos, 1, raw, nblocks * 255u))
+            wb_byte(raw + gblk * 255u + dpos, (uint8_t)dval);
         if (status && valid && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
             status[gblk] = (uint8_t)st;
         wave_fence();
