@@ -81,10 +81,12 @@ __device__ uint64_t g_bs_trace[4096 * BS_TRACE_N];
 #ifndef PPFS_BS_LATE_ST
 #define PPFS_BS_LATE_ST 0
 #endif
-// Decode: a single error's write-back to HBM deferred to after the tile's emission (1; the LDS row
-// is still patched before it) or stored at once (0, A/B knob)
+// Decode: a single error's write-back to HBM deferred to after the tile's emission (1, round 5; the
+// LDS row is still patched before it) or stored at once (0).  cfg5 step, 3 interleaved rounds
+// (r5rswb): decode 123.3-125.6 vs 124.3-126.0 us.  (The status byte after the emission, PPFS_BS_LATE_ST:
+// 126.1-127.1 vs 124.5-124.8 us, r5rsl: off.)
 #ifndef PPFS_BS_LATE_WB
-#define PPFS_BS_LATE_WB 0
+#define PPFS_BS_LATE_WB 1
 #endif
 #ifndef PPFS_BS_EMIT_G
 #define PPFS_BS_EMIT_G 4 // decode emission: output pieces read from LDS together (4: +0.5 % cfg5 step, r3p)
