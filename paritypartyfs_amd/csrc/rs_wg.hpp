@@ -463,10 +463,14 @@ __device__ __forceinline__ void stage_bytes(uint8_t* dst, const uint8_t* __restr
 
 // Decode phase 2 (wave 0, lane = block): the reference correction for blocks with r' != 0.
 // fix(pos, e) patches codeword byte pos of the lane's row (LDS) and, with write-back, in HBM.
+// defer (optional): a single error's HBM write-back is returned there as pos << 8 | byte (~0u: none)
+// for the caller to store later; the LDS row is patched at once either way.
 template <int T2>
 __device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, uint32_t par, uint32_t r, bool valid,
-    uint8_t* __restrict__ raw_g, uint64_t blk, bool wb, [[maybe_unused]] uint64_t raw_bytes)
+    uint8_t* __restrict__ raw_g, uint64_t blk, bool wb, [[maybe_unused]] uint64_t raw_bytes, uint32_t* defer = nullptr)
 {
+    if (defer)
+        *defer = ~0u;
     using L = RsWgLayout<T2>;
     const uint64_t rem = *(const uint64_t*)(lds + par + 8u * r);
     const bool err = valid && rem != 0;
@@ -511,7 +515,15 @@ __device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, ui
                     rs_correct_general<T2>(S, gf, fix);
             }
         } else if (err && geo) {
-            fix(gpos, ge);
+            if (defer) {
+                if (ge != 0) {
+                    const uint8_t fixed = (uint8_t)(lds[row + gpos] ^ ge);
+                    lds[row + gpos] = fixed;
+                    *defer = gpos << 8 | fixed;
+                }
+            } else {
+                fix(gpos, ge);
+            }
         }
     }
     return err ? 1u : 0u;

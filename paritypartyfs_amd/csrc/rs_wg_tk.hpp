@@ -410,6 +410,9 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
 #ifndef PPFS_TK_LATE_ST
 #define PPFS_TK_LATE_ST 0 // decode A/B: wave 0 stores the tile's status bytes after its emission stores
 #endif
+#ifndef PPFS_TK_LATE_WB
+#define PPFS_TK_LATE_WB 0 // decode A/B: wave 0 writes a single error's byte back after its emission stores
+#endif
 template <int T2, int WPC = 3, int NTST = 1>
 __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
     uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables, int write_back,
@@ -475,7 +478,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         if (dmaw && q1 < nfull)
             dma_tile192<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, raw + q1 * (TB * 255), tid, raw,
                 nblocks * 255u);
-        uint32_t st_tile = 0;
+        uint32_t st_tile = 0, wb_late = ~0u;
         PPFS_TK_MARK(1);
         if (wave == 0)
             *(uint64_t*)(lds + D::OFF_PAR + (pc ^ 1u) * 512u + 8u * lane) = 0;
@@ -490,7 +493,8 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         if (wave == 0) {
             if constexpr (PPFS_TK_PRIO)
                 __builtin_amdgcn_s_setprio(2); // the workgroup's other waves wait at barrier C for it
-            st_tile = phase_correct<T2>(lds, buf, par, row, true, raw, q0 * TB + row, wb, nblocks * 255u);
+            st_tile = phase_correct<T2>(lds, buf, par, row, true, raw, q0 * TB + row, wb, nblocks * 255u,
+                PPFS_TK_LATE_WB && wb ? &wb_late : nullptr);
             if (!PPFS_TK_LATE_ST && status && PPFS_DBG_OK(status + q0 * TB + row, 1, status, nblocks))
                 status[q0 * TB + row] = (uint8_t)st_tile;
             if constexpr (PPFS_TK_PRIO)
@@ -508,6 +512,9 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
                     st_nt<NTST>(dst + 16u * p, o);
             }
         }
+        if (PPFS_TK_LATE_WB && wave == 0 && wb_late != ~0u
+            && PPFS_DBG_OK(raw + (q0 * TB + row) * 255u + (wb_late >> 8), 1, raw, nblocks * 255u))
+            wb_byte(raw + (q0 * TB + row) * 255u + (wb_late >> 8), (uint8_t)wb_late);
         if (PPFS_TK_LATE_ST && wave == 0 && status && PPFS_DBG_OK(status + q0 * TB + row, 1, status, nblocks))
             status[q0 * TB + row] = (uint8_t)st_tile;
         ++iter;
