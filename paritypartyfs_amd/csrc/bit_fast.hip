@@ -30,50 +30,18 @@
 namespace ppfs {
 namespace bf {
 
-#ifndef PPFS_BF_NTST
-#define PPFS_BF_NTST 0
-#endif
-#ifndef PPFS_BF_NTLD
-#define PPFS_BF_NTLD 0
-#endif
 typedef unsigned int bf_u32x4 __attribute__((ext_vector_type(4)));
-// streamed global traffic: every block is read once and written once.  Non-temporal variants
-// (build knobs) on cfg4 (bs 4096, 2^20 blocks): NT loads 0-7 % slower everywhere; NT stores 1-3 %
-// faster on encode, 4-5 % slower on decode -- the encode outputs use them (gst16_raw below),
-// everything else is plain.
-__device__ __forceinline__ uint4 gld16(const uint8_t* p)
-{
-    if constexpr (PPFS_BF_NTLD) {
-        const bf_u32x4 v = __builtin_nontemporal_load((const bf_u32x4*)p);
-        return make_uint4(v.x, v.y, v.z, v.w);
-    } else {
-        return *(const uint4*)p;
-    }
-}
-__device__ __forceinline__ void gst16(uint8_t* p, uint4 v)
-{
-    if constexpr (PPFS_BF_NTST) {
-        const bf_u32x4 u = { v.x, v.y, v.z, v.w };
-        __builtin_nontemporal_store(u, (bf_u32x4*)p);
-    } else {
-        *(uint4*)p = v;
-    }
-}
-
-// Encode outputs (whole raw blocks) use non-temporal stores: on the full grid (r1l A/B) they cut
-// Hamming encode 1.51 -> 1.46 ms and parity 1.59 -> 1.55 ms, while the same stores on the decode
-// outputs cost 4-5 %, so decode / check keep gst16's plain stores.
-#ifndef PPFS_BF_ENC_NTST
-#define PPFS_BF_ENC_NTST 1
-#endif
+// streamed global traffic: every block is read once and written once.  Non-temporal variants on
+// cfg4 (bs 4096, 2^20 blocks): NT loads 0-7 % slower except the parity encode's payload (below); NT
+// stores 1-3 % faster on encode, 4-5 % slower on decode -- the encode outputs use them (gst16_raw:
+// on the full grid, r1l, Hamming encode 1.51 -> 1.46 ms, parity 1.59 -> 1.55 ms), everything else
+// is plain.
+__device__ __forceinline__ uint4 gld16(const uint8_t* p) { return *(const uint4*)p; }
+__device__ __forceinline__ void gst16(uint8_t* p, uint4 v) { *(uint4*)p = v; }
 __device__ __forceinline__ void gst16_raw(uint8_t* p, uint4 v)
 {
-    if constexpr (PPFS_BF_ENC_NTST) {
-        const bf_u32x4 u = { v.x, v.y, v.z, v.w };
-        __builtin_nontemporal_store(u, (bf_u32x4*)p);
-    } else {
-        gst16(p, v);
-    }
+    const bf_u32x4 u = { v.x, v.y, v.z, v.w };
+    __builtin_nontemporal_store(u, (bf_u32x4*)p);
 }
 
 // PPFS_ECC_DEBUG (dbg.hpp): a load outside its buffer reads zeros (and is reported); normal
@@ -88,12 +56,7 @@ __device__ __forceinline__ uint4 gld16c(const uint8_t* p, const uint8_t* base, u
 // (1,422-1,425 vs 1,465-1,470 us) but the 1-error decode timed right after it then runs 1,642-1,658
 // vs 1,579-1,589 us, so it keeps plain loads; the CRC encode is slower with them (1,636-1,640 vs
 // 1,606-1,608 us), and so is every decode / check (Hamming +3 %, parity +4 %, CRC +3 %).
-#ifndef PPFS_BF_PAR_ENC_NTLD
-#define PPFS_BF_PAR_ENC_NTLD 1
-#endif
-#ifndef PPFS_BF_HAM_ENC_NTLD
-#define PPFS_BF_HAM_ENC_NTLD 0
-#endif
+constexpr bool PAR_ENC_NTLD = true, HAM_ENC_NTLD = false;
 template <bool NT> __device__ __forceinline__ uint4 gld16p(const uint8_t* p, const uint8_t* base, uint64_t extent)
 {
     if constexpr (NT) {
@@ -111,39 +74,20 @@ constexpr int WAVES = 4;
 // not a persistent one): the dispatcher then walks workgroups in address order, so the blocks in
 // flight form one contiguous window of HBM.  A persistent grid-stride walk spreads them over
 // gridDim x 4 KiB and ran 9-22 % slower on cfg4 (A/B in DESIGN.md section 4.3).  With one block
-// per wave the register prefetch of the next block is dead weight, so it is off by default
-// (loads at the loop end, which only runs for grids capped below the batch).
-#ifndef PPFS_BF_PREFETCH
-#define PPFS_BF_PREFETCH 0
-#endif
-constexpr bool BF_PREFETCH = PPFS_BF_PREFETCH;
-// Blocks per wave of the Hamming / parity kernels: a workgroup walks BF_BPW consecutive 4-block
-// groups (one contiguous range, so the grid keeps its address order).
-#ifndef PPFS_BF_BPW
-#define PPFS_BF_BPW 1
-#endif
-constexpr int BF_BPW = PPFS_BF_BPW;
+// per wave a register prefetch of the next block is dead weight (measured: no gain, Appendix A);
+// a wave loads its next block at the loop end, which only runs for grids capped below the batch.
+// Blocks per wave of the Hamming / parity kernels: one group of WV blocks per workgroup (more, in
+// one contiguous range: slower, r4m).
+constexpr int BF_BPW = 1;
 
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 
-#define PPFS_BF_PRAGMA(x) _Pragma(#x)
-#define PPFS_BF_UNROLL(n) PPFS_BF_PRAGMA(unroll n)
-#ifndef PPFS_HAM_DEC_EMIT_UNROLL
-#define PPFS_HAM_DEC_EMIT_UNROLL 1
-#endif
-// Hamming decode: the LDS image stores issued before the syndrome reduction (1, round 5), so they
-// complete under its DPP chain, or after it, only for blocks with a payload output (0).  Configs leg,
-// 3 interleaved rounds (r5hei): clean 1.512-1.523 vs 1.531 ms, 1-error 1.582-1.590 vs 1.588-1.602 ms.
-// Status bytes and corrected-byte write-backs of the Hamming decode and the CRC / parity checks
-// stored after the payload emission (1, round 5) instead of before it (0).  Configs leg, 3
-// interleaved rounds (r5late): parity check 1.439-1.441 vs 1.467-1.469 ms, Hamming 1-error
-// 1.576-1.579 vs 1.578-1.587 ms, clean 1.500-1.511 vs 1.509-1.513, CRC check within noise.
-#ifndef PPFS_BF_LATE_ST
-#define PPFS_BF_LATE_ST 1
-#endif
-#ifndef PPFS_HAM_DEC_EARLY_IMG
-#define PPFS_HAM_DEC_EARLY_IMG 1
-#endif
+// Hamming decode: the LDS image stores issued before the syndrome reduction (round 5), so they
+// complete under its DPP chain (after it: configs leg, 3 interleaved rounds, r5hei: clean
+// 1.512-1.523 vs 1.531 ms, 1-error 1.582-1.590 vs 1.588-1.602 ms).  Status bytes and corrected-byte
+// write-backs of the Hamming decode and the CRC / parity checks are stored after the payload
+// emission (round 5; before it: r5late, parity check 1.439-1.441 vs 1.467-1.469 ms, Hamming 1-error
+// 1.576-1.579 vs 1.578-1.587 ms, clean 1.500-1.511 vs 1.509-1.513, CRC check within noise).
 
 // XOR over the 64 lanes of a wave, returned wave-uniform: a DPP butterfly inside each row of 16
 // lanes, then row broadcasts 15 and 31 (lane 63 ends with the total).
@@ -265,14 +209,12 @@ __global__ __launch_bounds__(64 * WV) void ham_fast_encode_kernel(const uint8_t*
     uint64_t blk = wg0 + wave;
     HamEncStage<NP> st;
     if (blk < nblocks)
-        ham_stage_load<NP, PPFS_BF_HAM_ENC_NTLD>(st, data, blk, a, lane);
+        ham_stage_load<NP, HAM_ENC_NTLD>(st, data, blk, a, lane);
     for (; blk < nblocks; blk += stride) {
         ham_stage_write<NP>(buf, st, lane);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         const uint64_t nx = blk + stride;
-        if (BF_PREFETCH && nx < nblocks)
-            ham_stage_load<NP, PPFS_BF_HAM_ENC_NTLD>(st, data, nx, a, lane); // lands while this block is computed
         const uint32_t m = (uint32_t)((blk * a.ds) & 15u); // payload byte 0 sits at LDS byte m
         uint8_t* rb = raw + blk * a.bs;
         const bool skipped = skip && PPFS_DBG_OK(skip + blk, 1, skip, nblocks_all) && skip[blk] == 5;
@@ -355,8 +297,8 @@ __global__ __launch_bounds__(64 * WV) void ham_fast_encode_kernel(const uint8_t*
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); // LDS reads done before the rewrite
         __builtin_amdgcn_wave_barrier();
-        if (!BF_PREFETCH && nx < nblocks)
-            ham_stage_load<NP, PPFS_BF_HAM_ENC_NTLD>(st, data, nx, a, lane);
+        if (nx < nblocks)
+            ham_stage_load<NP, HAM_ENC_NTLD>(st, data, nx, a, lane);
     }
 }
 
@@ -467,11 +409,6 @@ __global__ __launch_bounds__(64 * WV) void ham_fast_decode_kernel(uint8_t* __res
             X[k][3] = R[k].w;
         }
         const uint64_t nx = blk + stride;
-        if (BF_PREFETCH && nx < nblocks) {
-#pragma unroll
-            for (int k = 0; k < NP; ++k)
-                R[k] = gld16c(raw + nx * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
-        }
         // Syndrome (round 4: fewer VALU).  S = XOR of the positions of the set bits = (XOR over odd-
         // parity words w of w) << 5 | qbits(XOR of all words).  Parity is byte-order free, so the
         // words stay in memory order and only the XOR of all words is byte-swapped.  The odd-parity
@@ -479,7 +416,7 @@ __global__ __launch_bounds__(64 * WV) void ham_fast_decode_kernel(uint8_t* __res
         // the lane's word w = 256 k + 4 lane + u contributes 4 lane if odd, plus 256 k + u, whose bits
         // are the parities of the words with that bit of k or u set.  Only the block's last word (lane
         // 63, piece NP - 1, u = 3) holds bits past L, which are not part of the code.
-        if (PPFS_HAM_DEC_EARLY_IMG && data) {
+        if (data) {
 #pragma unroll
             for (int k = 0; k < NP; ++k)
                 *(uint4*)(img + 16u * (64u * k + lane)) = make_uint4(X[k][0], X[k][1], X[k][2], X[k][3]);
@@ -520,22 +457,11 @@ __global__ __launch_bounds__(64 * WV) void ham_fast_decode_kernel(uint8_t* __res
         const bool owner = par && ((S >> 7) & 63u) == lane;
         if (!data && owner && write_back && PPFS_DBG_OK(rb + (S >> 3), 1, raw, nblocks_all * a.bs))
             rb[S >> 3] = (uint8_t)(rb[S >> 3] ^ (0x80u >> (S & 7u)));
-        if (!PPFS_BF_LATE_ST && status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
-            status[blk] = (uint8_t)st;
         if (data && st != 5) {
-            if (!PPFS_HAM_DEC_EARLY_IMG) {
-#pragma unroll
-                for (int k = 0; k < NP; ++k)
-                    *(uint4*)(img + 16u * (64u * k + lane)) = make_uint4(X[k][0], X[k][1], X[k][2], X[k][3]);
-                if (lane < 4)
-                    *(uint32_t*)(img + NP * 1024 + 4 * lane) = 0;
-            }
             // the correction, after the image stores of the same wave (LDS ops of a wave run in order)
             if (owner) {
                 __hip_atomic_fetch_xor((uint32_t*)(img + ((S >> 5) << 2)), 0x80u << (8 * ((S >> 3) & 3u)) >> (S & 7u),
                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (!PPFS_BF_LATE_ST && write_back && PPFS_DBG_OK(rb + (S >> 3), 1, raw, nblocks_all * a.bs))
-                    rb[S >> 3] = img[S >> 3]; // the corrected byte (same lane: after its flip)
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -577,9 +503,8 @@ __global__ __launch_bounds__(64 * WV) void ham_fast_decode_kernel(uint8_t* __res
                 }
                 store(lane, b0, o);
             }
-            // pieces k >= 1: no head path; PPFS_HAM_DEC_EMIT_UNROLL pieces' window reads in flight
-            // (1: one rolled loop keeps the live state to one piece)
-            PPFS_BF_UNROLL(PPFS_HAM_DEC_EMIT_UNROLL)
+            // pieces k >= 1: no head path; one rolled loop keeps the live state to one piece
+#pragma unroll 1
             for (int k = 1; k <= NP; ++k) {
                 const uint32_t p = 64u * k + lane;
                 if (p >= npc)
@@ -589,15 +514,16 @@ __global__ __launch_bounds__(64 * WV) void ham_fast_decode_kernel(uint8_t* __res
                 ham_mid_piece(img, (uint32_t)b0, o);
                 store(p, b0, o);
             }
-            if (PPFS_BF_LATE_ST && owner && write_back && PPFS_DBG_OK(rb + (S >> 3), 1, raw, nblocks_all * a.bs))
+            // the corrected byte (the owner lane: after its flip)
+            if (owner && write_back && PPFS_DBG_OK(rb + (S >> 3), 1, raw, nblocks_all * a.bs))
                 rb[S >> 3] = img[S >> 3];
         }
-        if (PPFS_BF_LATE_ST && status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
+        if (status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
             status[blk] = (uint8_t)st;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         (void)lastw;
-        if (!BF_PREFETCH && nx < nblocks) {
+        if (nx < nblocks) {
 #pragma unroll
             for (int k = 0; k < NP; ++k)
                 R[k] = gld16c(raw + nx * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
@@ -673,13 +599,11 @@ __global__ __launch_bounds__(64 * WV) void parity_fast_encode_kernel(const uint8
     const uint64_t nblocks = nblocks_all < wg0 + WV * BF_BPW ? nblocks_all : wg0 + WV * BF_BPW;
     const uint64_t stride = WV;
     uint64_t blk = wg0 + wave;
-    HamEncStage<NP> cur, nxt;
+    HamEncStage<NP> cur;
     if (blk < nblocks)
-        ham_stage_load<NP, PPFS_BF_PAR_ENC_NTLD>(cur, data, blk, ha, lane);
+        ham_stage_load<NP, PAR_ENC_NTLD>(cur, data, blk, ha, lane);
     for (; blk < nblocks; blk += stride) {
         const uint64_t nx = blk + stride;
-        if (BF_PREFETCH && nx < nblocks)
-            ham_stage_load<NP, PPFS_BF_PAR_ENC_NTLD>(nxt, data, nx, ha, lane);
         const uint32_t m = (uint32_t)((blk * ds) & 15u);
         uint8_t* rb = raw + blk * a.bs;
         const uint32_t old_last = (lane == 63 && PPFS_DBG_OK(rb + a.bs - 1, 1, raw, nblocks_all * a.bs)) ? rb[a.bs - 1] : 0u;
@@ -706,17 +630,13 @@ __global__ __launch_bounds__(64 * WV) void parity_fast_encode_kernel(const uint8
                     gst16_raw(rb + 16u * (64u * k + lane), o);
             }
         }
-        if (BF_PREFETCH)
-            cur = nxt;
-        else if (nx < nblocks)
-            ham_stage_load<NP, PPFS_BF_PAR_ENC_NTLD>(cur, data, nx, ha, lane);
+        if (nx < nblocks)
+            ham_stage_load<NP, PAR_ENC_NTLD>(cur, data, nx, ha, lane);
     }
 }
 
-// Parity check: the payload output stored before the parity reduction (A/B knob)
-#ifndef PPFS_PAR_CHK_EARLY_ST
-#define PPFS_PAR_CHK_EARLY_ST 0
-#endif
+// Parity check (the payload output stored before the parity reduction: 1.633-1.637 vs 1.447-1.450 ms,
+// r5est)
 template <int NP, int WV>
 __global__ __launch_bounds__(64 * WV) void parity_fast_check_kernel(const uint8_t* __restrict__ raw,
     uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks_all, ParFast a)
@@ -727,17 +647,13 @@ __global__ __launch_bounds__(64 * WV) void parity_fast_check_kernel(const uint8_
     const uint64_t nblocks = nblocks_all < wg0 + WV * BF_BPW ? nblocks_all : wg0 + WV * BF_BPW;
     const uint64_t stride = WV;
     uint64_t blk = wg0 + wave;
-    uint4 R[NP], N[NP];
+    uint4 R[NP];
     if (blk < nblocks)
 #pragma unroll
         for (int k = 0; k < NP; ++k)
             R[k] = gld16c(raw + blk * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
     for (; blk < nblocks; blk += stride) {
         const uint64_t nx = blk + stride;
-        if (BF_PREFETCH && nx < nblocks)
-#pragma unroll
-            for (int k = 0; k < NP; ++k)
-                N[k] = gld16c(raw + nx * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
         auto emit = [&]() {
             if (data) {
                 // payload byte x = raw byte x; output pieces on the payload's global 16-byte grid:
@@ -767,25 +683,16 @@ __global__ __launch_bounds__(64 * WV) void parity_fast_check_kernel(const uint8_
                 }
             }
         };
-        if (PPFS_PAR_CHK_EARLY_ST)
-            emit();
         uint32_t ones = 0;
 #pragma unroll
         for (int k = 0; k < NP; ++k)
             ones += __builtin_popcount(R[k].x) + __builtin_popcount(R[k].y) + __builtin_popcount(R[k].z)
                 + __builtin_popcount(R[k].w);
         const uint32_t odd = wave_xor(ones & 1u);
-        if (!PPFS_BF_LATE_ST && status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
+        emit();
+        if (status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
             status[blk] = odd ? 5 : 0;
-        if (!PPFS_PAR_CHK_EARLY_ST)
-            emit();
-        if (PPFS_BF_LATE_ST && status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
-            status[blk] = odd ? 5 : 0;
-        if (BF_PREFETCH) {
-#pragma unroll
-            for (int k = 0; k < NP; ++k)
-                R[k] = N[k];
-        } else if (nx < nblocks) {
+        if (nx < nblocks) {
 #pragma unroll
             for (int k = 0; k < NP; ++k)
                 R[k] = gld16c(raw + nx * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
@@ -855,30 +762,9 @@ using CE = CrcLds<16>;
 // (12 x 2: 1.545-1.549, 8 x 4: 1.551-1.556, 5 x 4: 1.567-1.573, 4 x 4: 1.570-1.593, 6 x 8: 1.627);
 // the check on its 14 KiB image in 2-wave workgroups x 4: 1.586-1.605 vs 1.603-1.628 ms for 4 x 4
 // (2 x 2: 1.70, 2 x 1: 1.89, 1-wave workgroups: 1.77-2.12 -- the image then caps a CU at 11 waves).
-#ifndef PPFS_CRC_BPW
-#define PPFS_CRC_BPW 4
-#endif
-#ifndef PPFS_CRC_CHK_BPW
-#define PPFS_CRC_CHK_BPW 4
-#endif
-constexpr int CRC_BPW = PPFS_CRC_BPW, CRC_CHK_BPW = PPFS_CRC_CHK_BPW;
-// Register prefetch of a wave's next block in the CRC kernels (A/B knobs; default: BF_PREFETCH)
-#ifndef PPFS_CRC_ENC_PF
-#define PPFS_CRC_ENC_PF PPFS_BF_PREFETCH
-#endif
-#ifndef PPFS_CRC_CHK_PF
-#define PPFS_CRC_CHK_PF PPFS_BF_PREFETCH
-#endif
-constexpr bool CRC_ENC_PF = PPFS_CRC_ENC_PF, CRC_CHK_PF = PPFS_CRC_CHK_PF;
-// Output stores issued before the CRC computation (A/B knobs): the encode stores every raw piece
-// but the block's last one (lane 63, which carries the CRC field) first, the check its payload
-// output first, so the stores drain under the lookups instead of behind them
-#ifndef PPFS_CRC_ENC_EARLY_ST
-#define PPFS_CRC_ENC_EARLY_ST 0
-#endif
-#ifndef PPFS_CRC_CHK_EARLY_ST
-#define PPFS_CRC_CHK_EARLY_ST 0
-#endif
+// (Register prefetch of a wave's next block and output stores issued before the lookups: slower,
+// DESIGN.md Appendix A, r5cpf / r5est.)
+constexpr int CRC_BPW = 4, CRC_CHK_BPW = 4;
 
 // (x >> 8k) & 0x3C (a nibble * 4, the entry's byte offset): one v_and_b32_sdwa for k > 0
 __device__ __forceinline__ uint32_t sel3c(uint32_t x, int k)
@@ -1059,28 +945,15 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ENC_ATTR void crc_fast_encode_ker
     const uint64_t nblocks = nblocks_all < wg0 + WV * BPW ? nblocks_all : wg0 + WV * BPW;
     const uint64_t stride = WV;
     uint64_t blk = wg0 + wave;
-    HamEncStage<NP> cur, nxt;
+    HamEncStage<NP> cur;
     if (blk < nblocks)
         ham_stage_load<NP>(cur, data, blk, ha, lane);
     for (; blk < nblocks; blk += stride) {
         const uint64_t nx = blk + stride;
-        if (CRC_ENC_PF && nx < nblocks)
-            ham_stage_load<NP>(nxt, data, nx, ha, lane);
         const uint32_t m = (uint32_t)((blk * a.ds) & 15u); // payload byte 0 = superset byte m
         uint8_t* rb = raw + blk * a.bs;
         // superset piece q = 64 k + lane holds superset bytes [16 q, +16); payload = [m, m + ds)
         const bool store_blk = !(skip && PPFS_DBG_OK(skip + blk, 1, skip, nblocks_all) && skip[blk] == 5);
-        if (PPFS_CRC_ENC_EARLY_ST && store_blk) {
-            // every raw piece but the block's last (lane 63, piece NP - 1: the CRC field)
-#pragma unroll
-            for (int k = 0; k < NP; ++k) {
-                // every lane shifts (the neighbour pieces are whole-wave DPP moves); lane 63 skips the store
-                const uint4 nb = next_piece(cur.v[k], cur.v[k + 1]);
-                const uint4 o = shift_pieces(cur.v[k], nb, m);
-                if (!(k == NP - 1 && lane == 63) && PPFS_DBG_OK(rb + 16u * (64u * k + lane), 16, raw, nblocks_all * a.bs))
-                    gst16_raw(rb + 16u * (64u * k + lane), o);
-            }
-        }
         uint32_t acc = 0;
 #pragma unroll
         for (int k = 0; k <= NP; ++k) {
@@ -1101,7 +974,7 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ENC_ATTR void crc_fast_encode_ker
             if (lane == 63 && (a.n & 7u) && PPFS_DBG_OK(rb + a.ds + a.nbc - 1, 1, raw, nblocks_all * a.bs))
                 old_last = rb[a.ds + a.nbc - 1];
 #pragma unroll
-            for (int k = PPFS_CRC_ENC_EARLY_ST ? NP - 1 : 0; k < NP; ++k) {
+            for (int k = 0; k < NP; ++k) {
                 const uint4 nb = next_piece(cur.v[k], cur.v[k + 1]);
                 uint4 o = shift_pieces(cur.v[k], nb, m);
                 if (k == NP - 1 && lane == 63) {
@@ -1114,30 +987,20 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ENC_ATTR void crc_fast_encode_ker
                     const uint32_t keep = rbits ? ((1u << (8u - rbits)) - 1u) << 24 : 0u; // old low bits
                     o.w = (o.w & ~fmask) | field | ((old_last << 24) & keep);
                 }
-                if ((!PPFS_CRC_ENC_EARLY_ST || lane == 63) && PPFS_DBG_OK(rb + 16u * (64u * k + lane), 16, raw, nblocks_all * a.bs))
+                if (PPFS_DBG_OK(rb + 16u * (64u * k + lane), 16, raw, nblocks_all * a.bs))
                     gst16_raw(rb + 16u * (64u * k + lane), o);
             }
         }
-        if (CRC_ENC_PF)
-            cur = nxt;
-        else if (nx < nblocks)
+        if (nx < nblocks)
             ham_stage_load<NP>(cur, data, nx, ha, lane);
     }
 }
 
 // The check's LDS image (round 5): only the maps it reads -- M0..M3, K, the lane tree L..L+5
 // (blob maps 0-10), FCHK (blob map 27, here map 11) and the lane maps: 14 KiB where it used to
-// stage the blob's first 22.5 KiB (the encode's 16 placement maps included).
-// PPFS_CRC_CHK_EIGHT (A/B): the piece and Horner maps as the encode's 8-bit tables instead (4 lookups
-// per map, not 8), image = lane maps | 6-bit tree maps | FCHK | 8-bit maps, 31 KiB
-#ifndef PPFS_CRC_CHK_EIGHT
-#define PPFS_CRC_CHK_EIGHT 0
-#endif
-constexpr int CK_FCHK = 11, CK_LANE_OFF = 12 * CF_MAP, CK_NIB_BYTES = CK_LANE_OFF + CF_LANES * CF_MAP;
-constexpr int CK8_SIX = CF_LANES * CF_MAP, CK8_FCHK = CK8_SIX + CF_NSIX * CF_MAP6, CK8_EIGHT = CK8_FCHK + CF_MAP;
-constexpr int CK8_BYTES = CK8_EIGHT + CF_NEIGHT * CF_EIGHT;
-constexpr int CK_BYTES = PPFS_CRC_CHK_EIGHT ? CK8_BYTES : CK_NIB_BYTES;
-static_assert(CK8_SIX % 16 == 0 && CK8_FCHK % 16 == 0 && CK8_EIGHT % 16 == 0, "16-byte staging");
+// stage the blob's first 22.5 KiB (the encode's 16 placement maps included).  (The encode's 8-bit
+// piece and Horner maps here instead, a 31 KiB image: same or +2 %, r4za / r4zb.)
+constexpr int CK_FCHK = 11, CK_LANE_OFF = 12 * CF_MAP, CK_BYTES = CK_LANE_OFF + CF_LANES * CF_MAP;
 template <int NP, int WV, int BPW>
 __global__ __launch_bounds__(64 * WV) PPFS_CRC_ATTR void crc_fast_check_kernel(const uint8_t* __restrict__ raw,
     uint8_t* __restrict__ data, uint8_t* __restrict__ status, uint64_t nblocks_all, CrcFast a,
@@ -1146,12 +1009,8 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ATTR void crc_fast_check_kernel(c
     __shared__ __attribute__((aligned(16))) uint8_t tbl[CK_BYTES];
     for (uint32_t p = threadIdx.x; p < CK_BYTES / 16; p += 64 * WV) {
         const uint32_t o = 16 * p;
-        uint32_t src;
-        if constexpr (PPFS_CRC_CHK_EIGHT) // lane maps, 6-bit maps, FCHK, 8-bit maps
-            src = o < CK8_SIX ? CF_LANE_OFF + o
-                : (o < CK8_FCHK ? CF_SIX_OFF + (o - CK8_SIX) : (o < CK8_EIGHT ? CF_FCHK * CF_MAP + (o - CK8_FCHK) : CF_EIGHT_OFF + (o - CK8_EIGHT)));
-        else // maps 0-10 in place, then FCHK, then the lane maps
-            src = o < CK_FCHK * CF_MAP ? o : (o < CK_LANE_OFF ? CF_FCHK * CF_MAP + (o - CK_FCHK * CF_MAP) : CF_LANE_OFF + (o - CK_LANE_OFF));
+        // maps 0-10 in place, then FCHK, then the lane maps
+        const uint32_t src = o < CK_FCHK * CF_MAP ? o : (o < CK_LANE_OFF ? CF_FCHK * CF_MAP + (o - CK_FCHK * CF_MAP) : CF_LANE_OFF + (o - CK_LANE_OFF));
         *(uint4*)(tbl + o) = *(const uint4*)(tables + src);
     }
     if constexpr (WV > 1) {
@@ -1168,17 +1027,13 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ATTR void crc_fast_check_kernel(c
     const uint64_t nblocks = nblocks_all < wg0 + WV * BPW ? nblocks_all : wg0 + WV * BPW;
     const uint64_t stride = WV;
     uint64_t blk = wg0 + wave;
-    uint4 R[NP], N[NP];
+    uint4 R[NP];
     if (blk < nblocks)
 #pragma unroll
         for (int k = 0; k < NP; ++k)
             R[k] = gld16c(raw + blk * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
     for (; blk < nblocks; blk += stride) {
         const uint64_t nx = blk + stride;
-        if (CRC_CHK_PF && nx < nblocks)
-#pragma unroll
-            for (int k = 0; k < NP; ++k)
-                N[k] = gld16c(raw + nx * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);
         auto emit = [&]() {
             if (data) {
                 const uint64_t start = blk * ds, a0 = start & ~15ull;
@@ -1204,27 +1059,16 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ATTR void crc_fast_check_kernel(c
                 }
             }
         };
-        if (PPFS_CRC_CHK_EARLY_ST)
-            emit();
         uint32_t acc = 0;
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
             const int32_t q16 = 16 * (64 * k + (int32_t)lane);
             const int32_t hi = (int32_t)ds - q16;
             const uint32_t hi_c = hi < 0 ? 0u : (hi > 16 ? 16u : (uint32_t)hi);
-            if constexpr (PPFS_CRC_CHK_EIGHT) {
-                const uint32_t pv = crc_piece8(tbl + CK8_EIGHT, R[k], 0u, hi_c, n32);
-                acc = k == 0 ? pv : (cmap8(tbl + CK8_EIGHT + 4 * CF_EIGHT, acc) ^ pv);
-            } else {
-                const uint32_t pv = crc_piece(tbl, R[k], 0u, hi_c, n32);
-                acc = k == 0 ? pv : (cmap(tbl + CF_K * CF_MAP, acc) ^ pv);
-            }
+            const uint32_t pv = crc_piece(tbl, R[k], 0u, hi_c, n32);
+            acc = k == 0 ? pv : (cmap(tbl + CF_K * CF_MAP, acc) ^ pv);
         }
-        uint32_t V;
-        if constexpr (PPFS_CRC_CHK_EIGHT)
-            V = cmap(tbl + CK8_FCHK, crc_lane_sum<0, CK8_SIX>(tbl, acc, lane));
-        else
-            V = cmap(tbl + CK_FCHK * CF_MAP, crc_lane_sum<CK_LANE_OFF, -1>(tbl, acc, lane));
+        const uint32_t V = cmap(tbl + CK_FCHK * CF_MAP, crc_lane_sum<CK_LANE_OFF, -1>(tbl, acc, lane));
         const uint32_t st = (V << 1) & a.mask;
         // stored field: n bits MSB first from byte ds (in the last raw piece, lane 63)
         const uint4 last = make_uint4(__builtin_amdgcn_readlane(R[NP - 1].x, 63), __builtin_amdgcn_readlane(R[NP - 1].y, 63),
@@ -1237,17 +1081,10 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ATTR void crc_fast_check_kernel(c
             f = (f << 8) | ((lw[b >> 2] >> (8 * (b & 3))) & 0xFFu);
         }
         const uint32_t field = (uint32_t)(f >> (8 * a.nbc - a.n));
-        if (!PPFS_BF_LATE_ST && status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
+        emit();
+        if (status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
             status[blk] = (st == field) ? 0 : 5;
-        if (!PPFS_CRC_CHK_EARLY_ST)
-            emit();
-        if (PPFS_BF_LATE_ST && status && lane == 0 && PPFS_DBG_OK(status + blk, 1, status, nblocks_all))
-            status[blk] = (st == field) ? 0 : 5;
-        if (CRC_CHK_PF) {
-#pragma unroll
-            for (int k = 0; k < NP; ++k)
-                R[k] = N[k];
-        } else if (nx < nblocks) {
+        if (nx < nblocks) {
 #pragma unroll
             for (int k = 0; k < NP; ++k)
                 R[k] = gld16c(raw + nx * a.bs + 16u * (64u * k + lane), raw, nblocks_all * a.bs);

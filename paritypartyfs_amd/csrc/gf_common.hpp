@@ -47,18 +47,9 @@ struct Gf {
     __device__ __forceinline__ uint32_t qs(uint32_t c) const { return t[GF_QS + c]; }
 };
 
-// Write-back of one corrected codeword byte to HBM (decode with write_back).  PPFS_WB_NT=1 (ablation
-// builds): a non-temporal byte store.
-#ifndef PPFS_WB_NT
-#define PPFS_WB_NT 0
-#endif
-__device__ __forceinline__ void wb_byte(uint8_t* p, uint8_t v)
-{
-    if constexpr (PPFS_WB_NT)
-        __builtin_nontemporal_store(v, p);
-    else
-        *p = v;
-}
+// Write-back of one corrected codeword byte to HBM (decode with write_back).  A plain byte store: the
+// non-temporal form measured no faster.
+__device__ __forceinline__ void wb_byte(uint8_t* p, uint8_t v) { *p = v; }
 
 // Wave-uniform values: keep the compiler honest about what is uniform.
 __device__ __forceinline__ uint32_t wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }

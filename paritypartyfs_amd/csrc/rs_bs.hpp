@@ -34,10 +34,6 @@ using wg::lds_addr;
 using wg::st_bytes;
 using wg::st_nt;
 
-#ifndef PPFS_BS_XCHG
-#define PPFS_BS_XCHG 0
-#endif
-
 // PPFS_TK_TRACE (profiling builds only): every decode wave sums s_memtime cycles per phase into
 // g_bs_trace (prologue, DMA wait, c mod g, S1/S2 + logs, XP row + confirmation, fix / general path,
 // status, emission, image-free wait + next DMA, iterations, end), read by ppfs_bs_trace_read.
@@ -58,39 +54,14 @@ __device__ uint64_t g_bs_trace[4096 * BS_TRACE_N];
 #define PPFS_BS_TR_ARGS
 #endif
 
-#ifndef PPFS_BS_LOGCHK
-#define PPFS_BS_LOGCHK 0 // decode: single-error confirmation in the log domain
-#endif
-#ifndef PPFS_BS_DEC_IDMA
-#define PPFS_BS_DEC_IDMA 0 // decode: next tile's DMA interleaved with the emission rounds
-#endif
 // Wave priorities (round 5): the waves of a CU alternate between the LDS-latency-bound chain and the
-// shorter correction / emission phases; raising a wave's priority (s_setprio 2) outside its chain lets
-// those phases issue ahead of the other waves' chain steps.  Decode: 1 = the correction, 2 = + the
-// emission (shipped: 1-error 131.9-135.3 vs 136.6-139.3 us on two boxes, r5q / r5r), 4 = everything
-// but the chain, 3 = static prio 1 for waves NW/2.. (no gain); 0 = off.  Encode: the emission and
-// the next tile's DMA (1, shipped; 0 = off).
-#ifndef PPFS_BS_PRIO
-#define PPFS_BS_PRIO 2
-#endif
-#ifndef PPFS_BS_EPRIO
-#define PPFS_BS_EPRIO 1
-#endif
-// Decode: a block's status byte stored after the tile's emission (1) instead of right after its
-// correction (0, A/B knob)
-#ifndef PPFS_BS_LATE_ST
-#define PPFS_BS_LATE_ST 0
-#endif
-// Decode: a single error's write-back to HBM deferred to after the tile's emission (1, round 5; the
-// LDS row is still patched before it) or stored at once (0).  cfg5 step, 3 interleaved rounds
-// (r5rswb): decode 123.3-125.6 vs 124.3-126.0 us.  (The status byte after the emission, PPFS_BS_LATE_ST:
-// 126.1-127.1 vs 124.5-124.8 us, r5rsl: off.)
-#ifndef PPFS_BS_LATE_WB
-#define PPFS_BS_LATE_WB 1
-#endif
-#ifndef PPFS_BS_EMIT_G
-#define PPFS_BS_EMIT_G 4 // decode emission: output pieces read from LDS together (4: +0.5 % cfg5 step, r3p)
-#endif
+// shorter correction / emission phases; a wave raises its priority (s_setprio 2) outside its chain so
+// those phases issue ahead of the other waves' chain steps: decode through the correction and the
+// emission (1-error 131.9-135.3 vs 136.6-139.3 us on two boxes, r5q / r5r), encode through the
+// emission and the next tile's DMA.  A single error's write-back to HBM goes out after the tile's
+// emission (the LDS row is patched at once; r5rswb: 123.3-125.6 vs 124.3-126.0 us); the status byte
+// right after the correction (after the emission: 126.1-127.1 vs 124.5-124.8 us, r5rsl).
+constexpr int EMIT_G = 4; // decode emission: output pieces read from LDS together (+0.5 % cfg5 step, r3p)
 
 constexpr int TBW = 32;            // blocks per wave tile
 constexpr int IMGW = TBW * 255;    // 8,160 B: one wave tile's codeword image
@@ -191,18 +162,10 @@ __device__ __forceinline__ void bs_remainder(uint32_t (&s)[4], const uint8_t* ld
             // pair: quad_perm [1,1,3,3]); state * x^8: column 1 takes column 0's upper half
             // (quad_perm [0,0,2,2]), column 0 takes zeros.  Each DPP move folds into its XOR / AND
             // (v_xor_b32_dpp, v_and_b32_dpp).
-#if PPFS_BS_XCHG
-            // ablation builds: the partner exchange of rs_pair.hpp (DPP move, select, AND)
-            const uint32_t p2 = pair::pair_xchg<1>(s[2]), p3 = pair::pair_xchg<1>(s[3]);
-            lo ^= L.c ? s[2] : p2;
-            hi ^= L.c ? s[3] : p3;
-            uint32_t n[4] = { p2 & cm, p3 & cm, s[0], s[1] };
-#else
             lo ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)s[2], 0xF5, 0xF, 0xF, true);
             hi ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)s[3], 0xF5, 0xF, 0xF, true);
             uint32_t n[4] = { (uint32_t)__builtin_amdgcn_mov_dpp((int)s[2], 0xA0, 0xF, 0xF, true) & cm,
                 (uint32_t)__builtin_amdgcn_mov_dpp((int)s[3], 0xA0, 0xF, 0xF, true) & cm, s[0], s[1] }; // state * x^8
-#endif
             bs_lookups(n, lds, L, lo, hi);
             s[0] = n[0];
             s[1] = n[1];
@@ -288,14 +251,6 @@ __device__ __forceinline__ uint32_t bs_correct(uint8_t* lds, const uint8_t* gfp,
         return 0u;
     const Gf gf { gfp };
     const uint16_t* t = (const uint16_t*)(s12p + 8192u * c); // state byte u = 16c + k
-#if PPFS_BS_LOGCHK
-    // LOG of the lane's 16 state bytes, issued beside the S12 lookups (independent of S1, S2): the
-    // confirmation below then compares logs, with no lookup after the XP row arrives
-    uint32_t lr[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k)
-        lr[k] = gf.log((s[k >> 2] >> (8 * (k & 3))) & 0xFFu);
-#endif
     uint32_t s12 = 0;
 #pragma unroll
     for (int k = 0; k < 16; ++k)
@@ -315,30 +270,19 @@ __device__ __forceinline__ uint32_t bs_correct(uint8_t* lds, const uint8_t* gfp,
     for (int k = 0; k < 16; ++k) {
         const uint32_t x = (xw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
         const uint32_t rb = (s[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-#if PPFS_BS_LOGCHK
-        // rb == e alpha^(log x) <=> (x zero and rb zero) or (rb nonzero and log rb == le + x mod 255)
-        uint32_t lsum = le + x;
-        lsum = lsum >= 255u ? lsum - 255u : lsum;
-        const bool ok = x == 0xFFu ? rb == 0u : (rb != 0u && lr[k] == lsum);
-        bad |= ok ? 0u : 1u;
-#else
         const uint32_t ev = x == 0xFFu ? 0u : gf.exp(le + x);
         bad |= ev != rb ? 1u : 0u;
-#endif
     }
     const bool geo = err && pair::pair_or<1>(bad) == 0u;
     PPFS_BS_MARK(4);
     if (geo && c == 0) {
-        if constexpr (PPFS_BS_LATE_WB) {
-            const uint32_t ev = gf.exp(le);
-            if (ev) {
-                const uint8_t fixed = (uint8_t)(lds[row + lx] ^ ev);
-                lds[row + lx] = fixed;
-                dpos = lx;
-                dval = fixed;
-            }
-        } else {
-            col::col_fix(lds, row, raw_g, gblk, wb, lx, gf.exp(le), raw_bytes);
+        // the LDS row now; the HBM write-back after the tile's emission (dpos / dval)
+        const uint32_t ev = gf.exp(le);
+        if (ev) {
+            const uint8_t fixed = (uint8_t)(lds[row + lx] ^ ev);
+            lds[row + lx] = fixed;
+            dpos = lx;
+            dval = fixed;
         }
     }
     if (err && !geo)
@@ -361,29 +305,6 @@ __device__ __forceinline__ void dma_wave(uint32_t img_base, const uint8_t* __res
             dma16(src + so, __builtin_amdgcn_readfirstlane(img_base + 1024u * (uint32_t)k));
     }
 }
-
-// One wave-instruction k of dma_wave (image pieces lane + 64 k)
-template <typename F>
-__device__ __forceinline__ void dma_wave_k(uint32_t img_base, const uint8_t* __restrict__ src, uint32_t lane, F src_off,
-    int k, [[maybe_unused]] const uint8_t* gbase, [[maybe_unused]] uint64_t extent)
-{
-    const uint32_t i = lane + 64u * (uint32_t)k;
-    const int so = src_off(i);
-    if (((k + 1) * 64 <= IMG_PIECES || i < (uint32_t)IMG_PIECES) && so >= 0 && PPFS_DBG_OK(src + so, 16, gbase, extent))
-        dma16(src + so, __builtin_amdgcn_readfirstlane(img_base + 1024u * (uint32_t)k));
-}
-
-// Decode emission of 2t = 32 (pair_dec_piece: payload piece p of the tile reads image bytes
-// [16 p + 32 (b + 1), +48), b = 16 p / 223): the lowest image byte that output round k (pieces
-// 64 k .. 64 k + 63) reads, and so the number of tile DMA instructions (1 KiB image windows) that
-// may be issued for the NEXT tile once rounds 0..k have read the image
-constexpr int bs_emit_minread(int k) { return 1024 * k + 32 * ((1024 * k) / 223 + 1); }
-constexpr int bs_dma_free_after(int k, int ko)
-{
-    return k + 1 >= ko ? KP : (bs_emit_minread(k + 1) / 1024 < KP ? bs_emit_minread(k + 1) / 1024 : KP);
-}
-static_assert(bs_dma_free_after(0, 7) == 1 && bs_dma_free_after(5, 7) == 6 && bs_dma_free_after(6, 7) == KP,
-    "one DMA window per emission round, the last two after the last round");
 
 // Register prefetch of a wave tile (NBUF = 0): piece i = lane + 64 k into pf[k] with plain
 // 16-byte loads (compiler-counted), written into the image once the previous tile's emission has
@@ -558,12 +479,10 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_encode_kernel(const uint8_t*
                 load_wave(pf, data + nx * (TBW * K), lane, src_off, dextent, nblocks * K);
         }
         first = false;
-        if constexpr (PPFS_BS_EPRIO)
-            __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(0);
         uint32_t s[4];
         bs_remainder<K>(s, lds, img + 255u * Ln.blk + (uint32_t)T2, Ln);
-        if constexpr (PPFS_BS_EPRIO)
-            __builtin_amdgcn_s_setprio(2);
+        __builtin_amdgcn_s_setprio(2);
         put_parity(lds, img, Ln, s);
         uint8_t* dst = raw + t * (TBW * 255);
 #pragma unroll
@@ -673,9 +592,6 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
         }
     }
     PPFS_BS_MARK(0);
-    if constexpr (PPFS_BS_PRIO == 3) // static priority for the second half of the waves (guide: s_setprio)
-        if (wave >= NW / 2)
-            __builtin_amdgcn_s_setprio(1);
     uint32_t tk_next = 0;
     for (; t < nfull; wk.advance(tk_next), t = wk.t) {
         const uint64_t nx = wk.nx;
@@ -688,69 +604,49 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
             tk_next = wk.take(lane);
         }
         PPFS_BS_MARK(1);
-        if constexpr (PPFS_BS_PRIO == 4)
-            __builtin_amdgcn_s_setprio(0);
         uint32_t s[4];
         bs_cmodg(s, lds, row, Ln);
 #ifdef PPFS_TK_TRACE
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
         PPFS_BS_MARK(2);
-        if constexpr (PPFS_BS_PRIO == 1 || PPFS_BS_PRIO == 2 || PPFS_BS_PRIO == 4)
-            __builtin_amdgcn_s_setprio(2);
+        __builtin_amdgcn_s_setprio(2);
         const uint64_t gblk = t * TBW + Ln.blk;
         uint32_t dpos, dval = 0;
         const uint32_t st = bs_correct<T2>(
             lds, gfp, s12p, xpm, row, Ln.c, s, true, raw, gblk, wb, nblocks * 255u, dpos, dval PPFS_BS_TR_ARGS);
-        if (!PPFS_BS_LATE_ST && status && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
+        if (status && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
             status[gblk] = (uint8_t)st;
         wave_fence(); // corrections patched into the image rows
-        if constexpr (PPFS_BS_PRIO == 1)
-            __builtin_amdgcn_s_setprio(0);
         PPFS_BS_MARK(6);
-        // PPFS_BS_DEC_IDMA (NBUF = 1): the next tile's DMA windows go out between the emission's
-        // rounds as soon as no later round reads them, so the DMA flies while the wave emits
-        const bool idma = PPFS_BS_DEC_IDMA && NBUF == 1 && want && nx < nfull;
-        int dma_done = 0;
         if (want) {
             uint8_t* dst = data + t * (TBW * K);
-            // PPFS_BS_EMIT_G pieces per group: their LDS reads in flight together, then their stores
+            // EMIT_G pieces per group: their LDS reads in flight together, then their stores
 #pragma unroll
-            for (int k0 = 0; k0 < KO; k0 += PPFS_BS_EMIT_G) {
-                uint4 v[PPFS_BS_EMIT_G];
+            for (int k0 = 0; k0 < KO; k0 += EMIT_G) {
+                uint4 v[EMIT_G];
 #pragma unroll
-                for (int g = 0; g < PPFS_BS_EMIT_G && k0 + g < KO; ++g) {
+                for (int g = 0; g < EMIT_G && k0 + g < KO; ++g) {
                     uint32_t p = lane + 64u * (uint32_t)(k0 + g);
                     asm volatile("" : "+v"(p));
                     v[g] = pair::pair_dec_piece<T2>(lds, img - pair::PAD, p);
                 }
 #pragma unroll
-                for (int g = 0; g < PPFS_BS_EMIT_G && k0 + g < KO; ++g) {
+                for (int g = 0; g < EMIT_G && k0 + g < KO; ++g) {
                     const int k = k0 + g;
                     const uint32_t p = lane + 64u * (uint32_t)k;
                     if (((k + 1) * 64 <= OUT_PIECES || p < (uint32_t)OUT_PIECES) && PPFS_DBG_OK(dst + 16u * p, 16, data, nblocks * K))
                         st_nt<NTST>(dst + 16u * p, v[g]);
                 }
                 asm volatile("" ::: "memory");
-                if (idma) { // the stores consumed the group's LDS reads
-                    const int kl = k0 + PPFS_BS_EMIT_G < KO ? k0 + PPFS_BS_EMIT_G - 1 : KO - 1;
-#pragma unroll
-                    for (int j = 0; j < KP; ++j)
-                        if (j >= dma_done && j < bs_dma_free_after(kl, KO))
-                            dma_wave_k(base, raw + nx * (TBW * 255), lane, src_off, j, raw, nblocks * 255u);
-                    dma_done = bs_dma_free_after(kl, KO);
-                }
             }
         }
-        if (PPFS_BS_LATE_WB && wb && dpos != ~0u && PPFS_DBG_OK(raw + gblk * 255u + dpos, 1, raw, nblocks * 255u))
+        if (wb && dpos != ~0u && PPFS_DBG_OK(raw + gblk * 255u + dpos, 1, raw, nblocks * 255u))
             wb_byte(raw + gblk * 255u + dpos, (uint8_t)dval);
-        if (PPFS_BS_LATE_ST && status && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
-            status[gblk] = (uint8_t)st;
         PPFS_BS_MARK(7);
-        if constexpr (PPFS_BS_PRIO == 2)
-            __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (nx < nfull && !idma) {
+        if (nx < nfull) {
             if constexpr (NBUF == 0)
                 put_wave(lds, img, pf, lane, src_off);
             else
@@ -777,7 +673,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rs_bs_decode_kernel(uint8_t* __res
         uint32_t dpos, dval = 0;
         const uint32_t st = bs_correct<T2>(
             lds, gfp, s12p, xpm, row, Ln.c, s, valid, raw, gblk, wb, nblocks * 255u, dpos, dval PPFS_BS_TR_ARGS);
-        if (PPFS_BS_LATE_WB && valid && wb && dpos != ~0u && PPFS_DBG_OK(raw + gblk * 255u + dpos, 1, raw, nblocks * 255u))
+        if (valid && wb && dpos != ~0u && PPFS_DBG_OK(raw + gblk * 255u + dpos, 1, raw, nblocks * 255u))
             wb_byte(raw + gblk * 255u + dpos, (uint8_t)dval);
         if (status && valid && Ln.c == 0 && PPFS_DBG_OK(status + gblk, 1, status, nblocks))
             status[gblk] = (uint8_t)st;

@@ -167,12 +167,6 @@ template <int W, int N> __device__ __forceinline__ void xor_into(uint32_t (&acc)
     }
 }
 
-#ifndef PPFS_SDWA_ADDR
-#define PPFS_SDWA_ADDR 1
-#endif
-#ifndef PPFS_ENC_DIRECT_EMIT
-#define PPFS_ENC_DIRECT_EMIT 1
-#endif
 // (x >> 8K) & 0xF0 in one VALU op (SDWA byte select; LLVM only forms it for K = 2, 3)
 template <int K> __device__ __forceinline__ uint32_t nib16(uint32_t x)
 {
@@ -223,21 +217,9 @@ __device__ __forceinline__ void slice8(uint32_t (&st)[W], uint32_t lo, uint32_t 
         acc[w] = FIRST ? 0u : st[w - 2];
     constexpr int NL = FIRST ? (NB < 8 ? NB : 8) : 8;
     Ent<W> e[2 * NL];
-#if PPFS_SDWA_ADDR
     // slot address of a nibble = nibble * 16: the high nibble of byte k is (x >> 8k) & 0xF0,
     // the low one (x << 4 >> 8k) & 0xF0 -- one v_and_b32_sdwa (byte select) each
     slice_lookups<W, NL, 0>(e, lo, hi, lo << 4, hi << 4, lds);
-#else
-    const uint32_t ll = (lo << 4) & 0xF0F0F0F0u, lh = lo & 0xF0F0F0F0u;
-    const uint32_t hl = (hi << 4) & 0xF0F0F0F0u, hh = hi & 0xF0F0F0F0u;
-#pragma unroll
-    for (int p = 0; p < NL; ++p) {
-        const uint32_t xl = p < 4 ? ll : hl, xh = p < 4 ? lh : hh;
-        const int sh = 8 * (p & 3);
-        e[2 * p] = tbl_ld<W>(lds, ((xl >> sh) & 0xFFu) + (2 * p) * 256);
-        e[2 * p + 1] = tbl_ld<W>(lds, ((xh >> sh) & 0xFFu) + (2 * p + 1) * 256);
-    }
-#endif
     xor_into<W, 2 * NL>(acc, e);
 #pragma unroll
     for (int w = 0; w < W; ++w)
@@ -619,7 +601,6 @@ __device__ __forceinline__ void rs_encode_lane(uint8_t* tile, const uint8_t* lds
         }
         return v;
     };
-#if PPFS_ENC_DIRECT_EMIT
     if constexpr (T2 >= 4) {
         // Direct emission: v_q = funnel(R[q+1], R[q]) by sh = 8 * ((2a - 2t) mod 4) bits holds
         // payload bytes 4q + sh/8 - a .. +3, whose output position ob + 2t + 4q + sh/8 - a is
@@ -652,7 +633,6 @@ __device__ __forceinline__ void rs_encode_lane(uint8_t* tile, const uint8_t* lds
         }
         return;
     }
-#endif
     // payload byte j at register byte a + j -> stream byte p at register byte a + p - 2t
     emit_row<NR, RS_N, -T2, 3 - T2, T2>(tile, RS_N * l, (int)a - T2, R, par);
 }
@@ -695,9 +675,6 @@ __device__ __forceinline__ void emit_payload_direct(uint8_t* tile, uint32_t l, u
     }
 }
 
-#ifndef PPFS_DEC_DIRECT_EMIT
-#define PPFS_DEC_DIRECT_EMIT 1
-#endif
 
 template <int T2, int NS, typename Pre>
 __device__ __forceinline__ void rs_decode_lane(uint8_t* tile, const uint8_t* lds, uint32_t l, bool valid,
@@ -773,12 +750,7 @@ __device__ __forceinline__ void rs_decode_lane(uint8_t* tile, const uint8_t* lds
     if (!want_data)
         return;
     wave_fence();
-#if PPFS_DEC_DIRECT_EMIT
     emit_payload_direct<T2, NR>(tile, l, a, R);
-#else
-    // payload byte j = codeword byte 2t + j at register byte a + 2t + j
-    emit_row<NR, K, T2, T2 + 3, 0>(tile, K * l, (int)a + T2, R, [](uint32_t v, int) { return v; });
-#endif
     // the row's own bytes only: ordered after this lane's emission stores
     if (fpos >= (uint32_t)T2 && fpos != 0xFFFFFFFFu)
         tile[K * l + fpos - T2] = (uint8_t)fval;
@@ -868,14 +840,10 @@ __device__ __forceinline__ void load_regs(uint4 (&L)[(NPIECE + 63) / 64], const 
 
 // conditional prefetch that defines L on both paths: a conditionally-kept L would stay live
 // (and be spilled) through the whole loop body
-#ifndef PPFS_BRANCHLESS_PF
-#define PPFS_BRANCHLESS_PF 1
-#endif
 template <int NPIECE, int NT = 0>
 __device__ __forceinline__ void load_regs_if(bool cond, uint4 (&L)[(NPIECE + 63) / 64], const uint8_t* __restrict__ src,
     uint32_t lane, const uint8_t* __restrict__ dummy = nullptr)
 {
-#if PPFS_BRANCHLESS_PF
     if (dummy) {
         // branch-free: without a next tile the loads re-read a 1 KiB L2-resident region, so the
         // loads are unconditional and the waitcnt pass can count them (a branch around them
@@ -896,7 +864,6 @@ __device__ __forceinline__ void load_regs_if(bool cond, uint4 (&L)[(NPIECE + 63)
         }
         return;
     }
-#endif
     if (cond) {
         load_regs<NPIECE, NT>(L, src, lane);
     } else {

@@ -53,30 +53,16 @@ static uint32_t rs_tile_grid(uint64_t nb, int wpc, int tb = 64)
 // The static-walk encode fits as many workgroups as its LDS allows (at most 4); the ticket encode
 // runs 2 per CU (its LDS carries the ticket slots).
 constexpr int fit_wpc(int bytes, int most) { return 163840 / bytes < most ? 163840 / bytes : most; }
-#ifndef PPFS_TK_NTST
-#define PPFS_TK_NTST 1 // ticket kernels' output stores: 1 non-temporal, 0 plain (ablation)
-#endif
+constexpr int TK_NTST = 1; // ticket kernels' output stores non-temporal (plain stores: slower)
 constexpr int ENC_NBUF = 3, ENC_WPC = 2, DEC_NBUF = 2, DEC_WPC = 3;
 constexpr int ENC_WPC_STATIC = fit_wpc(wg::lds_bytes<PPFS_T2, false, ENC_NBUF>(), 4);
 #elif PPFS_T2 == 32
 // 2t = 32 (rs_bs.hpp): one workgroup per CU, every wave on its own 32-block tiles;
-// encode 12 waves (3 per SIMD), decode 8 (LDS- and register-bound)
-#ifndef PPFS_BS_DEC_NW
-#define PPFS_BS_DEC_NW 8
-#endif
-#ifndef PPFS_BS_DEC_TLDS
-#define PPFS_BS_DEC_TLDS 3 // round 3: XP rows in LDS (with the register prefetch: 139 -> 130 us in the cfg5 step)
-#endif
-#ifndef PPFS_BS_DEC_NBUF
-#define PPFS_BS_DEC_NBUF 0 // register prefetch of the next tile (rs_bs.hpp load_wave); 1 = single LDS image
-#endif
-#ifndef PPFS_BS_ENC_NBUF
-#define PPFS_BS_ENC_NBUF 1 // single LDS image, the next tile's DMA after the emission; 0 = register prefetch
-#endif
-#ifndef PPFS_BS_TICKETS
-#define PPFS_BS_TICKETS 1 // round 5: waves take their tiles by per-XCD ticket (rs_bs.hpp BsWalk); 0 = static walk
-#endif
-constexpr int BS_ENC_NW = 12, BS_DEC_NW = PPFS_BS_DEC_NW, BS_DEC_TLDS = PPFS_BS_DEC_TLDS, BS_DEC_NBUF = PPFS_BS_DEC_NBUF;
+// encode 12 waves (3 per SIMD), decode 8 (LDS- and register-bound).  Decode: GF block, S12 table and
+// the XP rows in LDS (TLDS 3; round 3: 139 -> 130 us in the cfg5 step), register prefetch of the next
+// tile (NBUF 0); encode: one LDS image, the next tile's DMA after the emission (NBUF 1).  Both take
+// their tiles by per-XCD ticket when the launch has a counter set (rs_bs.hpp BsWalk).
+constexpr int BS_ENC_NW = 12, BS_ENC_NBUF = 1, BS_DEC_NW = 8, BS_DEC_TLDS = 3, BS_DEC_NBUF = 0;
 #else
 // 8 < 2t <= 16: rs_fast.hpp lane-per-block kernels; 2t = 16 encodes with the solo image kernel
 constexpr bool SOLO_IMG = PPFS_T2 == 16;
@@ -98,14 +84,14 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_encode_t, PPFS_T2)(const uint8_t* d,
 {
 #if PPFS_T2 <= 8
     if (ctr && ctr_clear)
-        PPFS_LAUNCH((wg::rs_wg_encode_tk_kernel<PPFS_T2, ENC_WPC, PPFS_TK_NTST>), dim3(rs_tile_grid(nb, ENC_WPC)), dim3(256), 0, s,
+        PPFS_LAUNCH((wg::rs_wg_encode_tk_kernel<PPFS_T2, ENC_WPC, TK_NTST>), dim3(rs_tile_grid(nb, ENC_WPC)), dim3(256), 0, s,
             d, r, nb, tab, ctr, ctr_clear);
     else
         PPFS_LAUNCH((wg::rs_wg_encode_kernel<PPFS_T2, ENC_NBUF, ENC_WPC_STATIC, 3, 1, false>), dim3(rs_tile_grid(nb, ENC_WPC_STATIC)),
             dim3(256), 0, s, d, r, nb, tab);
 #elif PPFS_T2 == 32
-    PPFS_LAUNCH((bs::rs_bs_encode_kernel<PPFS_T2, BS_ENC_NW, PPFS_BS_ENC_NBUF>), dim3(rs_tile_grid(nb, 1, bs::TBW * BS_ENC_NW)),
-        dim3(64 * BS_ENC_NW), 0, s, d, r, nb, tab, PPFS_BS_TICKETS ? ctr : nullptr, ctr_clear);
+    PPFS_LAUNCH((bs::rs_bs_encode_kernel<PPFS_T2, BS_ENC_NW, BS_ENC_NBUF>), dim3(rs_tile_grid(nb, 1, bs::TBW * BS_ENC_NW)),
+        dim3(64 * BS_ENC_NW), 0, s, d, r, nb, tab, ctr, ctr_clear);
 #else
     if constexpr (SOLO_IMG)
         PPFS_LAUNCH((pair::rs_solo_encode_img_kernel<PPFS_T2, SOLO_WPC, SOLO_NW>),
@@ -134,7 +120,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
 {
 #if PPFS_T2 <= 8
     if (ctr && ctr_clear)
-        PPFS_LAUNCH((wg::rs_wg_decode_tk_kernel<PPFS_T2, DEC_WPC, PPFS_TK_NTST>), dim3(rs_tile_grid(nb, DEC_WPC)), dim3(256), 0, s,
+        PPFS_LAUNCH((wg::rs_wg_decode_tk_kernel<PPFS_T2, DEC_WPC, TK_NTST>), dim3(rs_tile_grid(nb, DEC_WPC)), dim3(256), 0, s,
             r, d, st, nb, tab, wb, ctr, ctr_clear);
     else
         PPFS_LAUNCH((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC, 7, 1>), dim3(rs_tile_grid(nb, DEC_WPC)),
@@ -142,7 +128,7 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
 #elif PPFS_T2 == 32
     PPFS_LAUNCH((bs::rs_bs_decode_kernel<PPFS_T2, BS_DEC_NW, BS_DEC_NBUF, 1, BS_DEC_TLDS>),
         dim3(rs_tile_grid(nb, 1, bs::TBW * BS_DEC_NW)), dim3(64 * BS_DEC_NW), 0, s, r, d, st, nb, tab, wb,
-        PPFS_BS_TICKETS ? ctr : nullptr, ctr_clear);
+        ctr, ctr_clear);
 #else
     PPFS_LAUNCH(rs255_decode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, r, d, st, nb, tab, wb);
 #endif

@@ -53,12 +53,9 @@ __device__ __forceinline__ void barrier_lds()
 // the explicit counted vmcnt in the kernels.  (M0 write -> LDS-DMA needs one wait state.)
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm" // m0 is reserved; nothing else in these kernels uses it
-#ifndef PPFS_WG_DMA_POLICY
-#define PPFS_WG_DMA_POLICY "" // cache policy of the tile loads (ablation builds: " nt" measured slower)
-#endif
 __device__ __forceinline__ void dma16(const uint8_t* g, uint32_t lds_base)
 {
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" PPFS_WG_DMA_POLICY ::"v"(g),
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g),
                  "s"(lds_base)
                  : "memory", "m0");
 }
@@ -424,21 +421,11 @@ template <int T2> __device__ __forceinline__ uint4 dec_piece(const uint8_t* lds,
     return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
-// PPFS_ST_POLICY (ablation): the cache policy of the NT = 1 output stores -- 1: non-temporal
-// (the builtin), 2: nt sc1, 3: sc0 sc1 (system scope), 4: nt sc0 sc1 (inline asm; the explicit
-// vmcnt counts in the kernels count these stores the same way)
-#ifndef PPFS_ST_POLICY
-#define PPFS_ST_POLICY 1
-#endif
+// Output stores: NT = 1 non-temporal (the other cache policies measured no faster step, DESIGN.md
+// Appendix A, round 5 store policy), NT = 0 plain
 template <int NT = 1> __device__ __forceinline__ void st_nt(uint8_t* dst, uint4 v)
 {
-    if constexpr (NT && PPFS_ST_POLICY == 2) {
-        asm volatile("global_store_dwordx4 %0, %1, off nt sc1" ::"v"(dst), "v"(u32x4 { v.x, v.y, v.z, v.w }) : "memory");
-    } else if constexpr (NT && PPFS_ST_POLICY == 3) {
-        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(u32x4 { v.x, v.y, v.z, v.w }) : "memory");
-    } else if constexpr (NT && PPFS_ST_POLICY == 4) {
-        asm volatile("global_store_dwordx4 %0, %1, off nt sc0 sc1" ::"v"(dst), "v"(u32x4 { v.x, v.y, v.z, v.w }) : "memory");
-    } else if constexpr (NT) {
+    if constexpr (NT) {
         const u32x4 u = { v.x, v.y, v.z, v.w };
         __builtin_nontemporal_store(u, (u32x4*)dst);
     } else {
@@ -463,14 +450,10 @@ __device__ __forceinline__ void stage_bytes(uint8_t* dst, const uint8_t* __restr
 
 // Decode phase 2 (wave 0, lane = block): the reference correction for blocks with r' != 0.
 // fix(pos, e) patches codeword byte pos of the lane's row (LDS) and, with write-back, in HBM.
-// defer (optional): a single error's HBM write-back is returned there as pos << 8 | byte (~0u: none)
-// for the caller to store later; the LDS row is patched at once either way.
 template <int T2>
 __device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, uint32_t par, uint32_t r, bool valid,
-    uint8_t* __restrict__ raw_g, uint64_t blk, bool wb, [[maybe_unused]] uint64_t raw_bytes, uint32_t* defer = nullptr)
+    uint8_t* __restrict__ raw_g, uint64_t blk, bool wb, [[maybe_unused]] uint64_t raw_bytes)
 {
-    if (defer)
-        *defer = ~0u;
     using L = RsWgLayout<T2>;
     const uint64_t rem = *(const uint64_t*)(lds + par + 8u * r);
     const bool err = valid && rem != 0;
@@ -515,15 +498,7 @@ __device__ __forceinline__ uint32_t phase_correct(uint8_t* lds, uint32_t buf, ui
                     rs_correct_general<T2>(S, gf, fix);
             }
         } else if (err && geo) {
-            if (defer) {
-                if (ge != 0) {
-                    const uint8_t fixed = (uint8_t)(lds[row + gpos] ^ ge);
-                    lds[row + gpos] = fixed;
-                    *defer = gpos << 8 | fixed;
-                }
-            } else {
-                fix(gpos, ge);
-            }
+            fix(gpos, ge);
         }
     }
     return err ? 1u : 0u;

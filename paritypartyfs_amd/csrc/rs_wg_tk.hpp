@@ -98,17 +98,15 @@ __device__ __forceinline__ void dma_tables_w0(uint8_t* dst, const uint8_t* __res
 struct TkGeom {
     uint32_t nx, xc, gx, rank;
 };
-// PPFS_TK_NX (ablation): counters per launch; 1 = one chip-wide counter -- its atomics serialize at
-// ~80 per us and both t = 3 kernels ran 2x slower, 2 counters +18 % (r5za).  Round 5 also measured
-// cross-XCD stealing (a workgroup whose counter runs dry draws the next XCD's): no gain, the slow
-// XCD's lag sits in its workgroups' already-drawn lookahead tiles (r5zb-r5zd).
-#ifndef PPFS_TK_NX
-#define PPFS_TK_NX 8
-#endif
+// One counter per XCD (8).  One chip-wide counter: its atomics serialize at ~80 per us and both t = 3
+// kernels ran 2x slower, 2 counters +18 % (r5za).  Round 5 also measured cross-XCD stealing (a
+// workgroup whose counter runs dry draws the next XCD's): no gain, the slow XCD's lag sits in its
+// workgroups' already-drawn lookahead tiles (r5zb-r5zd).
+constexpr uint32_t TK_NX = 8;
 __device__ __forceinline__ TkGeom tk_geom()
 {
     TkGeom g;
-    g.nx = gridDim.x < (uint32_t)PPFS_TK_NX ? gridDim.x : (uint32_t)PPFS_TK_NX;
+    g.nx = gridDim.x < TK_NX ? gridDim.x : TK_NX;
     g.xc = blockIdx.x % g.nx;
     g.gx = (gridDim.x - g.xc + g.nx - 1u) / g.nx;
     g.rank = blockIdx.x / g.nx;
@@ -193,10 +191,7 @@ template <int T2> __device__ __forceinline__ uint32_t sched_enc_src(uint32_t p)
 
 // Every wave at s_setprio 2 from barrier B to its next remainder phase (emission, corrections, DMA
 // issue): with 2-3 workgroups per CU in different phases, the output side issues ahead of another
-// workgroup's remainder steps.  Round 5: step 4,508-4,509 vs 4,476-4,497 GiB/s (r5t); 0 = off.
-#ifndef PPFS_TK_EPRIO
-#define PPFS_TK_EPRIO 1
-#endif
+// workgroup's remainder steps.  Round 5: step 4,508-4,509 vs 4,476-4,497 GiB/s (r5t).
 template <int T2, int WPC = 2, int NTST = 1>
 __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t* __restrict__ data,
     uint8_t* __restrict__ raw, uint64_t nblocks, const uint8_t* __restrict__ tables, uint32_t* __restrict__ ctr,
@@ -305,13 +300,11 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
         PPFS_TK_MARK(1);
         if (wave == 0)
             *(uint64_t*)(lds + D::OFF_PAR + (pc ^ 1u) * 512u + 8u * lane) = 0;
-        if constexpr (PPFS_TK_EPRIO)
-            __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(0);
         phase_remainder<T2, K, D::NMAP, D::OFF_SLX, T5>(lds, buf, par, wave, row);
         PPFS_TK_MARK(2);
         barrier_lds(); // B: parity slots complete
-        if constexpr (PPFS_TK_EPRIO)
-            __builtin_amdgcn_s_setprio(2);
+        __builtin_amdgcn_s_setprio(2);
         PPFS_TK_MARK(3);
         if (tk_lane && iter)
             s_tk[(iter + 3u) & 3u] = (uint32_t)tk_tile(tk + 3u * g.gx, g, nfull); // the tile of iteration iter + 3
@@ -404,15 +397,6 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
 // (taken at the top of iteration j - 1, read at the top of iteration j for the DMA one tile ahead).
 // Counter sets: the decode halves of the stream's pair (api.cpp ctr_for).
 // ------------------------------------------------------------------------------------
-#ifndef PPFS_TK_PRIO
-#define PPFS_TK_PRIO 0 // decode ablation: wave 0 at s_setprio 2 through the corrections
-#endif
-#ifndef PPFS_TK_LATE_ST
-#define PPFS_TK_LATE_ST 0 // decode A/B: wave 0 stores the tile's status bytes after its emission stores
-#endif
-#ifndef PPFS_TK_LATE_WB
-#define PPFS_TK_LATE_WB 0 // decode A/B: wave 0 writes a single error's byte back after its emission stores
-#endif
 template <int T2, int WPC = 3, int NTST = 1>
 __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
     uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables, int write_back,
@@ -478,27 +462,19 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         if (dmaw && q1 < nfull)
             dma_tile192<IN_PIECES>(lds + D::OFF_BUF + (cur ^ 1u) * BUF + PAD, raw + q1 * (TB * 255), tid, raw,
                 nblocks * 255u);
-        uint32_t st_tile = 0, wb_late = ~0u;
         PPFS_TK_MARK(1);
         if (wave == 0)
             *(uint64_t*)(lds + D::OFF_PAR + (pc ^ 1u) * 512u + 8u * lane) = 0;
-        if constexpr (PPFS_TK_EPRIO)
-            __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(0);
         phase_remainder<T2, 255, D::NMAP, D::OFF_SLX>(lds, buf, par, wave, row);
         PPFS_TK_MARK(2);
         barrier_lds(); // B: remainders complete
-        if constexpr (PPFS_TK_EPRIO)
-            __builtin_amdgcn_s_setprio(2);
+        __builtin_amdgcn_s_setprio(2);
         PPFS_TK_MARK(3);
         if (wave == 0) {
-            if constexpr (PPFS_TK_PRIO)
-                __builtin_amdgcn_s_setprio(2); // the workgroup's other waves wait at barrier C for it
-            st_tile = phase_correct<T2>(lds, buf, par, row, true, raw, q0 * TB + row, wb, nblocks * 255u,
-                PPFS_TK_LATE_WB && wb ? &wb_late : nullptr);
-            if (!PPFS_TK_LATE_ST && status && PPFS_DBG_OK(status + q0 * TB + row, 1, status, nblocks))
+            const uint32_t st_tile = phase_correct<T2>(lds, buf, par, row, true, raw, q0 * TB + row, wb, nblocks * 255u);
+            if (status && PPFS_DBG_OK(status + q0 * TB + row, 1, status, nblocks))
                 status[q0 * TB + row] = (uint8_t)st_tile;
-            if constexpr (PPFS_TK_PRIO)
-                __builtin_amdgcn_s_setprio(0);
         }
         barrier_lds(); // C: corrections patched into the LDS rows
         PPFS_TK_MARK(4);
@@ -512,11 +488,6 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
                     st_nt<NTST>(dst + 16u * p, o);
             }
         }
-        if (PPFS_TK_LATE_WB && wave == 0 && wb_late != ~0u
-            && PPFS_DBG_OK(raw + (q0 * TB + row) * 255u + (wb_late >> 8), 1, raw, nblocks * 255u))
-            wb_byte(raw + (q0 * TB + row) * 255u + (wb_late >> 8), (uint8_t)wb_late);
-        if (PPFS_TK_LATE_ST && wave == 0 && status && PPFS_DBG_OK(status + q0 * TB + row, 1, status, nblocks))
-            status[q0 * TB + row] = (uint8_t)st_tile;
         ++iter;
         PPFS_TK_MARK(5);
         if (dmaw) { // the next tile's DMA landed; this tile's stores may fly

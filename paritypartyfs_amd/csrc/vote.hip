@@ -116,13 +116,8 @@ extern "C" hipError_t ppfs_copy_launch(uint8_t* dst, const uint8_t* src, uint64_
 // costs ~2x this kernel.  Each thread takes 4 consecutive blocks: one
 // 4-byte load of their positions and one of their values, then four byte stores.  (Round 4: store
 // instructions over 64 consecutive blocks instead, 16 KiB spans: 33 vs 30 us, r4zj; 8 or 16 blocks
-// per thread with byte loads: 31.3 vs 30.0 us, r4zk.)
-#ifndef PPFS_INJECT_NT
-#define PPFS_INJECT_NT 0 // ablation builds: non-temporal byte stores
-#endif
-#ifndef PPFS_INJECT_REV
-#define PPFS_INJECT_REV 0 // ablation builds: the first workgroups take the last blocks
-#endif
+// per thread with byte loads: 31.3 vs 30.0 us, r4zk; round 5: non-temporal byte stores and the
+// blocks in reverse order, no gain, r5k.)
 namespace ppfs {
 template <int MODE>
 __global__ __launch_bounds__(256) void inject_kernel(uint8_t* __restrict__ raw, uint64_t stride, uint64_t nblocks,
@@ -131,7 +126,7 @@ __global__ __launch_bounds__(256) void inject_kernel(uint8_t* __restrict__ raw, 
     const uint64_t nq = (nblocks + 3) / 4, qi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (qi >= nq)
         return;
-    const uint64_t q = PPFS_INJECT_REV ? nq - 1 - qi : qi, b0 = 4 * q;
+    const uint64_t b0 = 4 * qi;
     uint32_t p4, v4;
     if (b0 + 4 <= nblocks && ((uintptr_t)(pos + b0) & 3u) == 0 && ((uintptr_t)(val + b0) & 3u) == 0) {
         p4 = *(const uint32_t*)(pos + b0);
@@ -151,11 +146,7 @@ __global__ __launch_bounds__(256) void inject_kernel(uint8_t* __restrict__ raw, 
         uint8_t* d = raw + (b0 + j) * stride + p;
         const uint8_t v = (uint8_t)(v4 >> (8 * j));
         const uint8_t w = MODE == 0 ? v : (uint8_t)(*d ^ v);
-#if PPFS_INJECT_NT
-        __builtin_nontemporal_store(w, d);
-#else
         *d = w;
-#endif
     }
 }
 } // namespace ppfs
