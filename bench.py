@@ -221,6 +221,12 @@ def cpu_baseline(bs, t, nblocks, nfaithful, seed=1234):
 # ------------------------------------------------------------------------------------------
 # timing helpers
 # ------------------------------------------------------------------------------------------
+def _hip_ok(rc, what):
+    """A HIP runtime call's status, checked explicitly (not by assert: `python -O` would drop the call)."""
+    if rc != 0:
+        raise RuntimeError(f"{what}: hipError {rc}")
+
+
 class HipEvents:
     """Timing events without the system-scope fence (hipEventDisableSystemFence): a default event
     record writes back and invalidates the caches, which charges the previous kernel's dirty lines
@@ -235,17 +241,14 @@ class HipEvents:
         self.L = ctypes.CDLL("libamdhip64.so")
         self.ev = [ctypes.c_void_p() for _ in range(n)]
         for e in self.ev:
-            rc = self.L.hipEventCreateWithFlags(ctypes.byref(e), ctypes.c_uint(self.FLAGS))
-            assert rc == 0, f"hipEventCreateWithFlags: {rc}"
+            _hip_ok(self.L.hipEventCreateWithFlags(ctypes.byref(e), ctypes.c_uint(self.FLAGS)), "hipEventCreateWithFlags")
 
     def record(self, i, stream):
-        rc = self.L.hipEventRecord(self.ev[i], self.ct.c_void_p(stream.cuda_stream))
-        assert rc == 0, f"hipEventRecord: {rc}"
+        _hip_ok(self.L.hipEventRecord(self.ev[i], self.ct.c_void_p(stream.cuda_stream)), "hipEventRecord")
 
     def ms(self, i, j):
         f = self.ct.c_float()
-        rc = self.L.hipEventElapsedTime(self.ct.byref(f), self.ev[i], self.ev[j])
-        assert rc == 0, f"hipEventElapsedTime: {rc}"
+        _hip_ok(self.L.hipEventElapsedTime(self.ct.byref(f), self.ev[i], self.ev[j]), "hipEventElapsedTime")
         return f.value
 
     def close(self):
@@ -334,27 +337,27 @@ def host_link_ceilings(dev, nb, k, n, reps=3):
     h_in, h_out, d_in, d_out = vp(), vp(), vp(), vp()
     streams = [vp(), vp()]
     try:
-        assert L.hipHostMalloc(ctypes.byref(h_in), ctypes.c_size_t(big), 0) == 0
-        assert L.hipHostMalloc(ctypes.byref(h_out), ctypes.c_size_t(big), 0) == 0
-        assert L.hipMalloc(ctypes.byref(d_in), ctypes.c_size_t(big)) == 0
-        assert L.hipMalloc(ctypes.byref(d_out), ctypes.c_size_t(big)) == 0
+        _hip_ok(L.hipHostMalloc(ctypes.byref(h_in), ctypes.c_size_t(big), 0), "hipHostMalloc")
+        _hip_ok(L.hipHostMalloc(ctypes.byref(h_out), ctypes.c_size_t(big), 0), "hipHostMalloc")
+        _hip_ok(L.hipMalloc(ctypes.byref(d_in), ctypes.c_size_t(big)), "hipMalloc")
+        _hip_ok(L.hipMalloc(ctypes.byref(d_out), ctypes.c_size_t(big)), "hipMalloc")
         for st in streams:
-            assert L.hipStreamCreateWithFlags(ctypes.byref(st), 1) == 0  # hipStreamNonBlocking
+            _hip_ok(L.hipStreamCreateWithFlags(ctypes.byref(st), 1), "hipStreamCreateWithFlags")  # non-blocking
         H2D, D2H = 1, 2  # hipMemcpyHostToDevice, hipMemcpyDeviceToHost
 
         def copy(dst, src, nbytes, kind, st):
-            assert L.hipMemcpyAsync(dst, src, ctypes.c_size_t(nbytes), kind, st) == 0
+            _hip_ok(L.hipMemcpyAsync(dst, src, ctypes.c_size_t(nbytes), kind, st), "hipMemcpyAsync")
 
         def best(fn):
             ts = []
             for _ in range(reps):
                 fn()  # one untimed pass each time: both directions' DMA engines warm
                 for st in streams:
-                    assert L.hipStreamSynchronize(st) == 0
+                    _hip_ok(L.hipStreamSynchronize(st), "hipStreamSynchronize")
                 t0 = time.perf_counter()
                 fn()
                 for st in streams:
-                    assert L.hipStreamSynchronize(st) == 0
+                    _hip_ok(L.hipStreamSynchronize(st), "hipStreamSynchronize")
                 ts.append(time.perf_counter() - t0)
             return min(ts)
 
@@ -397,6 +400,54 @@ def host_link_ceilings(dev, nb, k, n, reps=3):
         "method": "hipMemcpyAsync between hipHostMalloc'd and hipMalloc'd buffers; both directions at once: 8 MiB "
                   f"pieces issued alternately on two non-blocking streams; best of {reps}",
     }
+
+
+# SURVEY 6 (measured in the dev container, 8-vCPU Xeon, reference sources at -O2, one thread):
+# RS(255,249) writeBlock (encode, incl. the old-block decode) and readBlock (clean decode) rates
+REF_CPU_CFG1 = {"writeBlock_blocks_per_s": 2422, "readBlock_clean_blocks_per_s": 95162,
+                "source": "SURVEY.md 6: reference C++ compiled here, 1 thread, HeapDisk, dev container (not the GPU box)"}
+
+
+def cfg1_leg(min_s=0.05, timeout_s=240):
+    """BASELINE configs[0] (performance_tests/bench_blockdevice.cpp:12-110 on the GPU-backed C++
+    adapter, tests/cpp/bench_blockdevice.cpp, built by __graft_entry__.build): per-block readBlock /
+    writeBlock of RS(255,249) over 4096 blocks and the batched readBlocks / writeBlocks, plus the
+    reference bench's raw / crc(0xea) / hamming(2^8) / rs(t=16) sweep over 1..256-byte calls on
+    256-byte blocks, beside the reference CPU rates.  A child process (it opens its own context)."""
+    exe = os.path.join(ROOT, "tests", "cpp", "_build", "bench_blockdevice")
+    if not os.path.exists(exe):
+        return {"error": "tests/cpp/_build/bench_blockdevice not built (__graft_entry__.build)"}
+    try:
+        r = subprocess.run([exe, str(min_s)], capture_output=True, text=True, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return {"error": f"bench_blockdevice exceeded {timeout_s} s"}
+    if r.returncode != 0:
+        return {"error": f"bench_blockdevice rc {r.returncode}: {r.stderr[-300:]}"}
+    rows = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    out = {"sweep": {}, "reference_cpu": REF_CPU_CFG1}
+    for row in rows:
+        name = row.get("bench", "")
+        if name.startswith("BM_BlockDevice_"):
+            op, rest = name[len("BM_BlockDevice_"):].split("/", 1)
+            dev_, n = rest.split("/")
+            d = out["sweep"].setdefault(dev_.replace("_test", ""), {})
+            rate = row.get("BytesRead_per_s", row.get("BytesWritten_per_s"))
+            d[f"{op.lower()}_{n}"] = {"us_per_call": row["us_per_call"], "KiB_per_s": round(rate / 1024.0, 1),
+                                      "ok": row["ok"]}
+        elif name.startswith("cfg1"):
+            out["rs255_249_4096_blocks"] = {k_: v for k_, v in row.items() if k_ != "bench"}
+        elif name.startswith("MappedFileDisk"):
+            out["mapped_file_disk_2p20_blocks"] = {k_: v for k_, v in row.items() if k_ != "bench"}
+    c = out.get("rs255_249_4096_blocks")
+    if c:
+        out["per_block_read_vs_reference_cpu"] = round(c["per_block_read_blocks_per_s"]
+                                                       / REF_CPU_CFG1["readBlock_clean_blocks_per_s"], 2)
+        out["per_block_write_vs_reference_cpu"] = round(c["per_block_write_blocks_per_s"]
+                                                        / REF_CPU_CFG1["writeBlock_blocks_per_s"], 2)
+    out["note"] = ("BASELINE configs[0]: the reference bench's calls through the C++ IBlockDevice adapter on the GPU "
+                   "(per-block calls served by the resident server kernel); KiB_per_s as google/benchmark's "
+                   "BytesRead / BytesWritten counters; outside the timed region")
+    return out
 
 
 def rank_fields(mine, alg_step_bytes, world, elapsed_s, steps):
@@ -452,12 +503,18 @@ def dry_run(args, world, rank):
     if dist.is_initialized():
         gathered = [None] * dist.get_world_size()
         dist.all_gather_object(gathered, mine)
-    # the N-rank fields of the real line, over the stand-in's times and the RS(255,249) byte count
-    per_rank, agg = rank_fields(mine, 2 * 504 * args.blocks, world, elapsed, args.steps)
+    # the N-rank fields of the real line, over the stand-in's times and the workload's byte count
+    # (RS codeword n = min(block_size, 255), k = n - 2t: rs_block_device.cpp:57)
+    n = min(args.block_size, 255)
+    k = n - 2 * args.t
+    per_rank, agg = rank_fields(mine, 2 * (k + n) * args.blocks, world, elapsed, args.steps)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "dry_run": True, "value": None, "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
                           "scaling": "weak", "note": "CPU stand-in for the engine: launcher / timing test only",
+                          "config": {"workload": f"RS({n},{k}) t={args.t} block_size={args.block_size} (stand-in)",
+                                     "blocks_per_gpu": args.blocks, "global_blocks": args.blocks * world,
+                                     "parallelism": f"shard{world}"},
                           "per_rank_kernels_ms": per_rank, **agg,
                           # what every rank parsed: the driver's argv must reach the ranks unchanged
                           "rank_args": [{k: g[k] for k in ("rank", "block_size", "t", "blocks")} for g in gathered]}),
@@ -805,9 +862,12 @@ def main(argv=None):
             host_incl[mode] = {"encode_GiBps": round(alg_launch / min(t_enc) / GIB, 3),
                                "decode_1err_GiBps": round(alg_launch / min(t_dec) / GIB, 3), "verified": ok,
                                "reps": args.host_reps}
-        host_incl["link"] = host_link_ceilings(dev, nb, k, n)
+        try:
+            host_incl["link"] = host_link_ceilings(dev, nb, k, n)
+        except RuntimeError as e:  # a failed link measurement must not cost the headline line
+            host_incl["link"] = {"error": str(e)}
         lk = host_incl["link"]
-        for mode in ("pageable", "pinned"):
+        for mode in ("pageable", "pinned") if "error" not in lk else ():
             # each call's copies alone, both directions at once over page-locked memory: the ceiling
             # the host path can reach (decode with write-back also returns every changed codeword)
             host_incl[mode]["encode_frac_of_link"] = round(host_incl[mode]["encode_GiBps"] / lk["encode_ceiling_GiBps"], 3)
@@ -832,12 +892,23 @@ def main(argv=None):
                 continue  # (the bench's own workload stays in: its 1-error decode, timed in-step style,
                 # must agree with kernels_ms.decode)
             cfg_lines[want[name]] = run_config(name, typ, cbs, ct, poly, 1 << 20, args.config_reps, stream, dev)
-        cfg_lines["note"] = ("BASELINE configs measured outside the timed region: median of back-to-back launches "
-                             "of one kernel over 2^20 blocks (each kernel's dispatch-packet start / stop), algorithmic bytes (payload + raw "
-                             "per block) / time, fraction of 8 TB/s; each 1-error decode is timed right after an "
-                             "untimed encode of the same batch and a one-byte-per-block injection, as in the headline "
-                             "step; roundtrip_ok = decode(encode(x)) == x with the "
-                             "expected statuses")
+        if (args.block_size, args.t) != (4096, 16):
+            # configs[4]'s shard in its own bench step (encode -> inject -> decode, K steps): the
+            # in-step fractions rocprofv3's profile of `--block-size 4096 --t 16` reproduces
+            from tools.bench_configs import step_leg
+
+            cfg_lines["cfg5_step"] = step_leg(4096, 16, 1 << 20, max(10, args.config_reps), dev, stream)
+        cfg_lines["note"] = ("BASELINE configs measured outside the timed region: median kernel time over launches "
+                             "of one kernel over 2^20 blocks (each kernel's dispatch-packet start / stop), algorithmic "
+                             "bytes (payload + raw per block) / time, fraction of 8 TB/s; encodes and clean decodes "
+                             "rotate over cold_sets buffer sets (inputs from HBM, not the Infinity Cache); each "
+                             "1-error decode is timed right after an untimed encode of the same batch and a "
+                             "one-byte-per-block injection, as in the headline step; cfg5_step = configs[4]'s shard "
+                             "in its own bench step (per-step kernel means); roundtrip_ok = decode(encode(x)) == x "
+                             "with the expected statuses")
+
+    # (6) BASELINE configs[0]: the reference's bench_blockdevice workload on the C++ adapter
+    cfg1 = cfg1_leg() if args.configs and rank == 0 and world == 1 else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -884,6 +955,7 @@ def main(argv=None):
             },
             "cpu_baseline": cpu,
             "configs": cfg_lines,
+            "cfg1": cfg1,
             "kernels_ms": {"encode": round(enc_avg, 5), "inject": round(inj_avg, 5), "decode": round(dec_avg, 5)},
             "in_step_frac": {"encode": frac(enc_avg), "decode": frac(dec_avg)},
             # the timed region's algorithmic bytes over all ranks / (N x 8 TB/s), and the

@@ -90,9 +90,10 @@ size_t ppfs_ecc_data_size(const ppfs_ecc_ctx* ctx);
 /* Short human-readable name of the kernel path the context dispatches to (for logs/tests). */
 const char* ppfs_ecc_kernel_name(const ppfs_ecc_ctx* ctx);
 /* The kernel path a device call of ctx on `stream` takes: as ppfs_ecc_kernel_name, except for
- * RS 2t <= 8, whose ticket-counter kernels need one of the context's 16 per-stream counter sets:
- * a 17th distinct stream, and any stream capturing a hipGraph, get the static-walk kernels
- * ("rs255-wg-seg4-lds").  Engine extension, no reference counterpart. */
+ * RS 2t <= 8 and 2t = 32, whose ticket-counter kernels need one of the context's 16 per-stream
+ * counter sets: a 17th distinct stream, and any stream capturing a hipGraph, get the static-walk
+ * kernels ("rs255-wg-seg4-lds" / "rs255-bs-byte-lds-static").  Engine extension, no reference
+ * counterpart. */
 const char* ppfs_ecc_stream_kernel_name(ppfs_ecc_ctx* ctx, void* stream);
 
 /*

@@ -24,7 +24,13 @@
 #include <string>
 #include <thread>
 #include <unistd.h>
+#if defined(__x86_64__) || defined(__i386__)
 #include <immintrin.h>
+#define PPFS_HOST_X86 1
+#else
+#define PPFS_HOST_X86 0
+#endif
+#include <pthread.h>
 #include <vector>
 
 #include "../../include/ppfs_ecc.h"
@@ -1419,11 +1425,13 @@ extern "C" const char* ppfs_ecc_stream_kernel_name(ppfs_ecc_ctx* c, void* stream
 {
     if (!c)
         return "";
-    if (c->d_ctr && c->rs_t2 <= 8) { // 2t <= 8: ticket kernels while the stream has (or can get) a counter set
+    if (c->d_ctr && (c->rs_t2 <= 8 || c->rs_t2 == 32)) {
+        // 2t <= 8 and 2t = 32: ticket walks while the stream has (or can get) a counter set
         const hipStream_t s = (hipStream_t)stream;
         const bool evok = ev_slot(c, s, false) >= 0 || c->ev_n < ppfs_ecc_ctx::kEvSlots;
         if (!evok || tk_slot(c, s, false) < 0)
-            return "rs255-wg-seg4-lds"; // rs_wg.hpp static walk
+            return c->rs_t2 <= 8 ? "rs255-wg-seg4-lds" // rs_wg.hpp static walk
+                                 : "rs255-bs-byte-lds-static"; // rs_bs.hpp, BsWalk without counters
     }
     return c->kname;
 }
@@ -1483,7 +1491,8 @@ int copy_threads()
 // its bytes once instead of twice -- the destinations (the page-locked staging the DMA reads, or
 // a multi-MB caller buffer) do not fit in the caches anyway.  AVX-512 or AVX2 by the CPU, memcpy
 // for the unaligned head and the tail; an sfence makes the stores visible before the job's
-// completion is published.
+// completion is published.  x86 hosts only; elsewhere piece_copy is a memcpy.
+#if PPFS_HOST_X86
 __attribute__((target("avx512f"))) void nt_copy512(uint8_t* d, const uint8_t* s, size_t n)
 {
     size_t i = 0;
@@ -1514,8 +1523,12 @@ __attribute__((target("avx2"))) void nt_copy256(uint8_t* d, const uint8_t* s, si
     if (i < n)
         std::memcpy(d + i, s + i, n - i);
 }
+#endif
 void piece_copy(void* dst, const void* src, size_t n)
 {
+#if !PPFS_HOST_X86
+    std::memcpy(dst, src, n);
+#else
     static const int mode = [] { // 2 AVX-512, 1 AVX2, 0 memcpy
         const char* e = std::getenv("PPFS_ECC_COPY_NT");
         if (e && *e == '0')
@@ -1548,6 +1561,7 @@ void piece_copy(void* dst, const void* src, size_t n)
     else
         nt_copy256(d + head, s + head, n - head);
     _mm_sfence();
+#endif
 }
 
 struct CopySeg {
@@ -1562,17 +1576,11 @@ public:
     static constexpr int kMaxSegs = 4;
 
     // one pool per process, its workers blocked on cv_ between jobs; leaked at exit (the workers
-    // never touch freed state).  A forked child starts its own (the parent's threads do not exist)
+    // never touch freed state).  Never used in a forked child (par_memcpy_n): the parent's workers
+    // do not exist there, and a mutex another parent thread held at the fork stays locked.
     static CopyPool& get()
     {
-        static std::mutex mu;
-        static CopyPool* pool = nullptr;
-        static pid_t owner = 0;
-        std::lock_guard<std::mutex> g(mu);
-        if (!pool || owner != getpid()) {
-            pool = new CopyPool(copy_threads() - 1);
-            owner = getpid();
-        }
+        static CopyPool* pool = new CopyPool(copy_threads() - 1);
         return *pool;
     }
 
@@ -1657,12 +1665,16 @@ private:
     Job* job_ = nullptr;
 };
 
+// Set in a forked child (pthread_atfork, registered at load): its copies run single-threaded.
+std::atomic<bool> g_fork_child { false };
+[[maybe_unused]] const int g_atfork_registered = pthread_atfork(nullptr, nullptr, [] { g_fork_child.store(true); });
+
 void par_memcpy_n(const CopySeg* segs, int nseg)
 {
     size_t total = 0;
     for (int i = 0; i < nseg; ++i)
         total += segs[i].n;
-    if (copy_threads() == 1 || total < (2u << 20)) {
+    if (g_fork_child.load(std::memory_order_relaxed) || copy_threads() == 1 || total < (2u << 20)) {
         for (int i = 0; i < nseg; ++i)
             std::memcpy(segs[i].dst, segs[i].src, segs[i].n);
         return;

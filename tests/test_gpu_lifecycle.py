@@ -139,13 +139,13 @@ def _capture(eng, data, cw, out, st, nb, static=STATIC):
 
 
 @pytest.mark.parametrize("bs,t,kname,static", [(512, 3, "rs255-wg-tk-lds", STATIC),
-                                               (4096, 16, "rs255-bs-byte-lds", "rs255-bs-byte-lds")], ids=["t3", "t16"])
+                                               (4096, 16, "rs255-bs-byte-lds", "rs255-bs-byte-lds-static")], ids=["t3", "t16"])
 def test_graph_replays_on_two_streams_at_once(oracle, bs, t, kname, static):
     """Two graphs of encode + decode (each its own buffers) replayed concurrently on two streams,
     and one replayed beside eager launches on its capture's stream: bit-exact every time.  With the
     capture stream's ticket set baked into the graphs, the concurrent replays would share counters
     and skip or repeat tiles.  t = 16: the byte-slice kernels' per-wave tickets (round 5) take the
-    static walk inside a capture the same way (the kernel name does not change for them)."""
+    static walk inside a capture the same way, reported as "rs255-bs-byte-lds-static"."""
     nb = (1 << 18) + 5
     n, k, data, cw = _rs_batch(oracle, nb, 34, bs, t)
     eng = EccEngine(ECC_REED_SOLOMON, bs, t)
@@ -208,7 +208,7 @@ def test_stream_slots_are_recycled_past_16_streams(oracle):
     for o in outs[:4]:
         assert np.array_equal(o.cpu().numpy(), cw)
     eng.close()
-    hm = EccEngine(ECC_REED_SOLOMON, 4096, 16)  # no ticket kernels: always its own path
+    hm = EccEngine(ECC_REED_SOLOMON, 4096, 16)  # a fresh context: the stream gets a free counter set
     assert hm.stream_kernel_name(streams[16]) == hm.kernel_name == "rs255-bs-byte-lds"
     hm.close()
 

@@ -12,6 +12,7 @@ import shutil
 import subprocess
 
 import pytest
+import yaml
 
 LLVM = "/opt/rocm/lib/llvm/bin"
 LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "paritypartyfs_amd", "_lib",
@@ -40,17 +41,13 @@ def kernel_descriptors(tmp_path):
     for o in objs:
         notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", o], cwd=tmp_path, check=True,
                                capture_output=True, text=True).stdout
-        name = None
-        for line in notes.splitlines():
-            m = re.match(r"\s+\.name:\s+(\S+)", line)
-            if m:
-                name = m.group(1)
-                out.setdefault(name, {})
-                continue
-            m = re.match(r"\s+\.(private_segment_fixed_size|vgpr_spill_count|sgpr_spill_count|vgpr_count):\s+(\d+)",
-                         line)
-            if m and name:
-                out[name][m.group(1)] = int(m.group(2))
+        # the AMDGPU metadata is one YAML document ("---" ... "..."); read amdhsa.kernels[*] as YAML
+        # so a kernel's fields are never confused with its arguments' (.args[*].name)
+        m = re.search(r"^\s*---\s*$(.*?)^\s*\.\.\.\s*$", notes, re.S | re.M)
+        assert m, f"no AMDGPU metadata in {o}"
+        for kd in yaml.safe_load(m.group(1))["amdhsa.kernels"]:
+            out[kd[".name"]] = {f: int(kd.get("." + f, 0)) for f in
+                                ("private_segment_fixed_size", "vgpr_spill_count", "sgpr_spill_count", "vgpr_count")}
     return out
 
 

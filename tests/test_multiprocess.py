@@ -114,3 +114,32 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--dry-run-cpu"],
                        capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
+
+
+def test_bench_gpus4_cfg5_shape():
+    """configs[4]'s command shape at four ranks, `python bench.py --gpus 4 --block-size 4096 --t 16`
+    (CPU stand-in over gloo): every rank reports, the job's blocks are 4 x 2^20 RS(255,223)
+    codewords, and aggregate_frac is taken against 4 x 8 TB/s."""
+    import json
+    import subprocess
+
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "3", "--warmup", "1",
+                        "--block-size", "4096", "--t", "16", "--dry-run-cpu"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    line = lines[0]
+    assert line["n_gpus"] == 4 and line["ranks_reporting"] == 4
+    assert line["config"]["global_blocks"] == 4 * (1 << 20) and line["config"]["blocks_per_gpu"] == 1 << 20
+    assert "RS(255,223)" in line["config"]["workload"]
+    per = line["per_rank_kernels_ms"]
+    assert all(len(per[key]["by_rank"]) == 4 for key in ("encode", "decode"))
+    assert per["decode"]["by_rank"][3] > per["decode"]["by_rank"][0]  # rank r's stand-in sleeps (r + 1) ms
+    assert line["aggregate_peak_GBps"] == 4 * 8000.0
+    assert line["aggregate_bytes"] == 2 * 478 * (1 << 20) * 4 * 3
+    exp = line["aggregate_bytes"] / (line["ms_per_step"] * 1e-3 * 3) / 1e9 / (4 * 8000.0)
+    assert abs(line["aggregate_frac"] - exp) <= 1e-3 * exp + 1e-4
+    assert sorted(a["rank"] for a in line["rank_args"]) == [0, 1, 2, 3]
+    assert all(a["block_size"] == 4096 and a["t"] == 16 for a in line["rank_args"])
