@@ -1469,7 +1469,37 @@ static int ensure_staging(ppfs_ecc_ctx* c, size_t bytes)
 }
 
 namespace {
-constexpr size_t kChunkBlocks = 1u << 15; // 32 Ki blocks per chunk (~8 MiB of RS codewords)
+// 64 Ki blocks per chunk (~16 MiB of RS codewords; round 6, r6e: page-locked encode / 1-error decode
+// 75.9-76.1 / 42.9-43.1 GiB/s vs 71.9-72.1 / 40.9-41.0 at 32 Ki, 98-262 Ki no better)
+constexpr size_t kChunkBlocks = 1u << 16;
+// Chunk sizes of a pipelined host call of at least 8 chunks: the first chunks ramp up (chunk / 8,
+// / 4, / 2) and the last ones ramp down (halving the remainder), so the pipeline's fill (the first
+// H2D before any kernel or D2H) and drain (the last D2H with no H2D beside it) move small chunks,
+// not whole ones.  r6g (page-locked, 2 rounds x 7 reps): clean decode 70.3-72.3 vs 64.0-65.3 GiB/s,
+// 1-error decode 41.6-42.6 vs 41.3-42.7, encode 71.5-75.4 vs 71.6-76.1.  (Four staging slots
+// instead of three: encode 51-52, decode 31-37 GiB/s; a decode's codewords returned on the H2D
+// stream: 26 GiB/s -- both dropped.)
+size_t ramp_chunk(size_t index, size_t remaining, size_t chunk)
+{
+    const size_t least = std::max<size_t>(chunk / 8, 1024);
+    size_t nb = chunk;
+    if (index < 3)
+        nb = std::max(least, chunk >> (3 - index));
+    if (remaining < 2 * nb) // ramp down: half of what is left (at least `least`)
+        nb = std::max(least, (remaining / 2 + 1023) & ~(size_t)1023);
+    return remaining < nb + least ? remaining : nb; // no piece smaller than `least` after it
+}
+// PPFS_ECC_CHUNK_BLOCKS (1 Ki .. 4 Mi): another chunk size (the r6e sweep)
+size_t chunk_blocks()
+{
+    static const size_t n = [] {
+        const char* e = std::getenv("PPFS_ECC_CHUNK_BLOCKS");
+        const long v = e ? std::atol(e) : 0;
+        return v >= 1024 && v <= (1l << 22) ? (size_t)v : kChunkBlocks;
+    }();
+    return n;
+}
+
 
 // Host staging copies of the pageable host path (caller buffer <-> page-locked staging): one CPU
 // thread moves ~10 GB/s, well under the link rate the page-locked path reaches, so copies of
@@ -2100,7 +2130,7 @@ static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t*
 static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t* data_out, uint8_t* raw,
     uint8_t* status, uint8_t* spill, size_t nblocks, int write_back)
 {
-    const size_t chunk = std::min(nblocks, kChunkBlocks);
+    const size_t chunk = std::min(nblocks, chunk_blocks());
     const Layout L = layout_for(c, chunk);
     int r = ensure_staging(c, L.total);
     if (r)
@@ -2203,8 +2233,9 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
     // a slot is reused only after drain() saw its outputs land: its H2D then never overwrites
     // staging an earlier chunk's kernel or D2H still reads
     int slot = 0;
-    for (size_t b0 = 0; b0 < nblocks; b0 += chunk, slot = (slot + 1) % NS) {
-        const size_t nb = std::min(chunk, nblocks - b0);
+    size_t nb = 0;
+    for (size_t b0 = 0, ci = 0; b0 < nblocks; b0 += nb, slot = (slot + 1) % NS, ++ci) {
+        nb = nblocks >= 8 * chunk ? ramp_chunk(ci, nblocks - b0, chunk) : std::min(chunk, nblocks - b0);
         if ((r = drain(slot)))
             return r;
         uint8_t* h = c->h_pin[slot];

@@ -496,9 +496,14 @@ def test_write_rmw_matches_oracle(oracle, codec):
 # ------------------------------------------------------------------------------------
 # host-memory path (pinned staging, several chunks)
 # ------------------------------------------------------------------------------------
-def test_host_path_multichunk(oracle):
-    # 5 chunks of 32 Ki blocks (the last one ragged): every staging slot is reused at least once
-    bs, t, nb = 512, 3, 4 * 32768 + 8001
+HOST_CHUNK = 1 << 16  # api.cpp kChunkBlocks: blocks per staging chunk of the host calls
+
+
+@pytest.mark.parametrize("nb", [4 * HOST_CHUNK + 8001, 8 * HOST_CHUNK + 12345], ids=["5chunks", "ramp"])
+def test_host_path_multichunk(oracle, nb):
+    # 5 chunks of 64 Ki blocks (the last one ragged): every staging slot is reused at least once;
+    # 8+ chunks: the ramped chunk sizes (api.cpp ramp_chunk: 8 Ki, 16 Ki, 32 Ki, 64 Ki ... halving tail)
+    bs, t = 512, 3
     n, k, _ = oracle.rs_sizes(bs, t)
     eng = EccEngine(ECC_REED_SOLOMON, bs, t)
     rng = rng_for("host")
@@ -562,14 +567,14 @@ def test_host_path_pinned_equals_pageable(typ, bs, t, poly):
 def test_host_decode_returns_only_changed_codewords(oracle, kind, codec, prior):
     """decode_host with write-back fetches codewords back only where the decode changed them
     (status 1): not at all for a clean chunk, as a packed gather for a few, as the whole range for
-    many.  Chunks of 32 Ki blocks: clean / 100 errors / every block / 5,000 blocks / a short tail;
+    many.  Chunks of 64 Ki blocks: clean / 100 errors / every block / 5,000 blocks / a short tail;
     every path must leave the caller's image equal to the oracle's write-back.  prior="eager": the
     context's previous call ended on a chunk where every block changed, so this call's first chunks
     (queued before any has landed: api.cpp host_run_chunks, three staging slots) fetch their
     codewords eagerly."""
     from paritypartyfs_amd import pinned
 
-    ch = 1 << 15
+    ch = HOST_CHUNK
     nb = 4 * ch + 777
     rng = rng_for("lazyraw", codec, kind)
     if codec == "rs512":
