@@ -379,6 +379,9 @@ def host_link_ceilings(dev, nb, k, n, reps=3):
         t_d2h = best(lambda: copy(h_out, d_out, n * nb, D2H, streams[1]))
         t_enc = best(lambda: both(k * nb, n * nb))
         t_dec = best(lambda: both(n * nb, (k + n) * nb))
+        # a decode whose write-back comes back as a patch list (api.cpp patch_slots: 2 slots of 4 B
+        # per block for RS(255, k)) moves n B in, k + 8 B out
+        t_decp = best(lambda: both(n * nb, (k + 8) * nb))
     finally:
         for st in streams:
             if st.value:
@@ -397,6 +400,7 @@ def host_link_ceilings(dev, nb, k, n, reps=3):
         "bidir_decode_bytes_GBps": round((k + 2 * n) * nb / t_dec / 1e9, 2),
         "encode_ceiling_GiBps": round(alg / t_enc / GIB, 3),
         "decode_1err_ceiling_GiBps": round(alg / t_dec / GIB, 3),
+        "decode_1err_patch_ceiling_GiBps": round(alg / t_decp / GIB, 3),
         "method": "hipMemcpyAsync between hipHostMalloc'd and hipMalloc'd buffers; both directions at once: 8 MiB "
                   f"pieces issued alternately on two non-blocking streams; best of {reps}",
     }
@@ -873,9 +877,14 @@ def main(argv=None):
             host_incl[mode]["encode_frac_of_link"] = round(host_incl[mode]["encode_GiBps"] / lk["encode_ceiling_GiBps"], 3)
             host_incl[mode]["decode_1err_frac_of_link"] = round(host_incl[mode]["decode_1err_GiBps"]
                                                                 / lk["decode_1err_ceiling_GiBps"], 3)
+            # the same against the copies the call makes now (write-back as a patch list, round 6)
+            host_incl[mode]["decode_1err_frac_of_patch_link"] = round(host_incl[mode]["decode_1err_GiBps"]
+                                                                      / lk["decode_1err_patch_ceiling_GiBps"], 3)
         host_incl["note"] = ("ppfs_ecc_{encode,decode}_host over the same 2^20 blocks: H2D + kernel + D2H wall "
                              "time (best of reps calls), algorithmic bytes; never `value`; *_frac_of_link = rate / "
-                             "the same call's copies alone over page-locked memory (link)")
+                             "the call's copies alone over page-locked memory (link) when every changed codeword "
+                             "comes back whole (n in, k + n out); *_frac_of_patch_link = against the copies of the "
+                             "patch-list write-back the engine uses (n in, k + 8 out)")
 
     # (5) the other BASELINE configs (driver-visible per-config kernel rates): configs[3] Hamming and
     # CRC 0x9960034c at block_size 4096 and configs[4] RS(255,223), 2^20 blocks each, back-to-back

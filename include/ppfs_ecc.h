@@ -136,6 +136,11 @@ int ppfs_ecc_decode_host(ppfs_ecc_ctx* ctx, uint8_t* raw, uint8_t* data, uint8_t
     int write_back, uint8_t* spill);
 int ppfs_ecc_write_host(ppfs_ecc_ctx* ctx, const uint8_t* data, uint8_t* raw, uint8_t* status,
     size_t nblocks);
+/* Blocks per staging chunk of the host calls above (16 MiB of codewords, a multiple of 1 Ki).  A
+ * decode with write-back of RS(255, k) or Hamming returns the bytes its write-back changed as a
+ * patch list that the host writes into raw; other codecs return the changed codewords whole.
+ * Engine extension, no reference counterpart. */
+size_t ppfs_ecc_host_chunk_blocks(ppfs_ecc_ctx* ctx);
 
 /*
  * Whole-image scrub: the disk-image effect of readBlock(i, 0, dataSize()) for

@@ -34,6 +34,7 @@ EXPORTED_SYMBOLS = (
     "ppfs_ecc_encode_host",
     "ppfs_ecc_decode_host",
     "ppfs_ecc_write_host",
+    "ppfs_ecc_host_chunk_blocks",
     "ppfs_ecc_scrub_host",
     "ppfs_ecc_scrub_device",
     "ppfs_vote3_device",
@@ -127,6 +128,8 @@ def lib() -> ctypes.CDLL:
                                          c_void_p]
     L.ppfs_ecc_write_device.restype = c_int
     L.ppfs_ecc_write_device.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
+    L.ppfs_ecc_host_chunk_blocks.restype = c_size_t
+    L.ppfs_ecc_host_chunk_blocks.argtypes = [c_void_p]
     L.ppfs_ecc_encode_host.restype = c_int
     L.ppfs_ecc_encode_host.argtypes = [c_void_p, c_void_p, c_void_p, c_size_t]
     L.ppfs_ecc_decode_host.restype = c_int

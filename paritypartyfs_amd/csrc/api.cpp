@@ -79,6 +79,8 @@ hipError_t ppfs_gather_rows_launch(const uint8_t* src, uint64_t src_rows, uint8_
 hipError_t ppfs_vote3_launch(const uint8_t* a, const uint8_t* b, const uint8_t* c, uint8_t* out, uint64_t rec_bytes,
     uint64_t nrec, uint32_t* damaged, hipStream_t s);
 hipError_t ppfs_copy_launch(uint8_t* dst, const uint8_t* src, uint64_t bytes, hipStream_t s);
+hipError_t ppfs_patch_list_launch(const uint8_t* cur, const uint8_t* orig, const uint8_t* status, uint32_t n, uint64_t nb,
+    uint32_t S, uint32_t* patch, hipStream_t s);
 hipError_t ppfs_inject_launch(uint8_t* raw, uint64_t stride, uint64_t nblocks, const uint8_t* pos, const uint8_t* val,
     int mode, hipStream_t s);
 }
@@ -1469,9 +1471,10 @@ static int ensure_staging(ppfs_ecc_ctx* c, size_t bytes)
 }
 
 namespace {
-// 64 Ki blocks per chunk (~16 MiB of RS codewords; round 6, r6e: page-locked encode / 1-error decode
-// 75.9-76.1 / 42.9-43.1 GiB/s vs 71.9-72.1 / 40.9-41.0 at 32 Ki, 98-262 Ki no better)
-constexpr size_t kChunkBlocks = 1u << 16;
+// 16 MiB of codewords per chunk: 64 Ki RS(255, k) blocks (round 6, r6e: page-locked encode / 1-error
+// decode 75.9-76.1 / 42.9-43.1 GiB/s vs 71.9-72.1 / 40.9-41.0 at 32 Ki, 98-262 Ki no better), 4 Ki
+// blocks of 4 KiB
+constexpr size_t kChunkBytes = 16u << 20;
 // Chunk sizes of a pipelined host call of at least 8 chunks: the first chunks ramp up (chunk / 8,
 // / 4, / 2) and the last ones ramp down (halving the remainder), so the pipeline's fill (the first
 // H2D before any kernel or D2H) and drain (the last D2H with no H2D beside it) move small chunks,
@@ -1489,15 +1492,16 @@ size_t ramp_chunk(size_t index, size_t remaining, size_t chunk)
         nb = std::max(least, (remaining / 2 + 1023) & ~(size_t)1023);
     return remaining < nb + least ? remaining : nb; // no piece smaller than `least` after it
 }
+// Blocks per chunk of a context's host calls (a multiple of 1 Ki, at least 1 Ki);
 // PPFS_ECC_CHUNK_BLOCKS (1 Ki .. 4 Mi): another chunk size (the r6e sweep)
-size_t chunk_blocks()
+size_t chunk_blocks(const ppfs_ecc_ctx* c)
 {
-    static const size_t n = [] {
+    static const size_t env = [] {
         const char* e = std::getenv("PPFS_ECC_CHUNK_BLOCKS");
         const long v = e ? std::atol(e) : 0;
-        return v >= 1024 && v <= (1l << 22) ? (size_t)v : kChunkBlocks;
+        return v >= 1024 && v <= (1l << 22) ? (size_t)v : 0;
     }();
-    return n;
+    return env ? env : std::max<size_t>(1024, (kChunkBytes / std::max<size_t>(c->raw, 1)) & ~(size_t)1023);
 }
 
 
@@ -1601,6 +1605,8 @@ struct CopySeg {
 };
 
 class CopyPool {
+    struct Job;
+
 public:
     static constexpr size_t kPiece = 512u << 10;
     static constexpr int kMaxSegs = 4;
@@ -1623,6 +1629,21 @@ public:
         }
         j.nseg = nseg;
         j.total = j.first[nseg];
+        submit(j);
+    }
+
+    // fn(i) for i in [0, n), spread over the workers and the caller
+    void run_for(size_t n, const std::function<void(size_t)>& fn)
+    {
+        Job j;
+        j.fn = &fn;
+        j.total = n;
+        submit(j);
+    }
+
+private:
+    void submit(Job& j)
+    {
         {
             std::lock_guard<std::mutex> g(m_);
             job_ = &j;
@@ -1636,7 +1657,6 @@ public:
         done_.wait(lk, [&] { return j.finished.load() == j.total && j.users == 0; });
     }
 
-private:
     struct Job {
         CopySeg seg[kMaxSegs] {};
         size_t first[kMaxSegs + 1] {}; // first piece of each segment
@@ -1644,6 +1664,7 @@ private:
         size_t total = 0;
         std::atomic<size_t> next { 0 }, finished { 0 };
         int users = 0; // workers holding the job (guarded by m_)
+        const std::function<void(size_t)>* fn = nullptr; // run_for: item p is fn(p), not a copy piece
     };
 
     explicit CopyPool(int workers)
@@ -1656,6 +1677,10 @@ private:
     {
         size_t done = 0;
         for (size_t p; (p = j.next.fetch_add(1)) < j.total; ++done) {
+            if (j.fn) {
+                (*j.fn)(p);
+                continue;
+            }
             int s = 0;
             while (p >= j.first[s + 1])
                 ++s;
@@ -1719,8 +1744,28 @@ void par_memcpy(void* dst, const void* src, size_t n)
 }
 
 struct Layout { // offsets inside one staging buffer
-    size_t data, raw, status, spill, idx, gat, total;
+    size_t data, raw, status, spill, idx, gat, orig, patch, total;
 };
+
+// Slots per block of a decode's patch list (vote.hip patch_list_kernel) -- RS(255, k): 2 (a block
+// with more changed bytes -- up to 2t, one per root of sigma -- comes back whole); Hamming: 1, the
+// one corrected byte -- or 0: the codec returns whole codewords (shortened RS, whose write-back
+// also spills past the block, and the codecs without a write-back).  PPFS_ECC_PATCH=0: always whole
+// codewords (A/B).
+uint32_t patch_slots(const ppfs_ecc_ctx* c)
+{
+    static const bool off = [] {
+        const char* e = std::getenv("PPFS_ECC_PATCH");
+        return e && *e == '0';
+    }();
+    if (off)
+        return 0;
+    if (c->p.ecc_type == PPFS_ECC_REED_SOLOMON && c->rs_n == 255)
+        return 2; // one or two changed bytes (at most 2t; more come back whole)
+    if (c->p.ecc_type == PPFS_ECC_HAMMING)
+        return 1;
+    return 0;
+}
 
 // a decode with write-back returns only the codewords it changed (status 1): as a packed gather
 // when at most nb / kGatherDiv blocks changed, else the chunk's whole codeword range
@@ -1736,7 +1781,10 @@ Layout layout_for(const ppfs_ecc_ctx* c, size_t nb)
     L.spill = al(L.status + nb);
     L.idx = al(L.spill + nb * (256 - std::min<size_t>(c->raw, 255)));
     L.gat = al(L.idx + (nb / kGatherDiv + 1) * sizeof(uint32_t));
-    L.total = al(L.gat + (nb / kGatherDiv + 1) * c->raw);
+    const uint32_t S = patch_slots(c);
+    L.orig = al(L.gat + (nb / kGatherDiv + 1) * c->raw);
+    L.patch = al(L.orig + (S ? nb * c->raw : 0));
+    L.total = al(L.patch + nb * S * sizeof(uint32_t));
     return L;
 }
 } // namespace
@@ -2130,7 +2178,7 @@ static int host_run(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t*
 static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, uint8_t* data_out, uint8_t* raw,
     uint8_t* status, uint8_t* spill, size_t nblocks, int write_back)
 {
-    const size_t chunk = std::min(nblocks, chunk_blocks());
+    const size_t chunk = std::min(nblocks, chunk_blocks(c));
     const Layout L = layout_for(c, chunk);
     int r = ensure_staging(c, L.total);
     if (r)
@@ -2140,7 +2188,7 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
     hipStream_t s_in = c->hs[0], s_out = c->hs[1];
     size_t pending_first[NS] = {}, pending_n[NS] = {};
     // fetched: the chunk's codewords already came back (staging, or the caller's page-locked image)
-    bool busy[NS] = {}, fetched[NS] = {};
+    bool busy[NS] = {}, fetched[NS] = {}, patched[NS] = {};
     // every caller buffer page-locked: DMA straight between it and the device staging buffers
     const bool direct = host_pinned(data_in, nblocks * c->data) && host_pinned(data_out, nblocks * c->data)
         && host_pinned(raw, nblocks * c->raw) && host_pinned(status, nblocks) && host_pinned(spill, nblocks * spill_b);
@@ -2148,6 +2196,9 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
     // decode with write-back: the codewords come back only where the decode changed them
     // (status 1), read from the chunk's status once it has landed
     const bool lazy_raw = op == OP_DECODE && write_back;
+    // ... and as a patch list (the changed bytes) where the codec bounds them (patch_slots): the
+    // host writes those bytes into its image instead of taking back whole codewords
+    const uint32_t S = lazy_raw ? patch_slots(c) : 0u;
     // predictor: the last drained chunk changed many codewords -> fetch the next ones eagerly
     // (queued behind the kernel, as encode does) instead of after the status has landed.  It starts
     // where the context's previous call left it: the first kSlots chunks are queued before any has
@@ -2200,13 +2251,87 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
         return 0;
     };
 
+    // The chunk's patch list into the caller's image: taken back now unless it came behind the
+    // kernel (the predictor expected many changed blocks), nothing for a clean chunk; blocks with
+    // more changed bytes than their S slots come back whole, by one gather like fetch_changed's.
+    auto apply_patches = [&](int i, size_t b0, size_t nb) -> int {
+        uint8_t* h = c->h_pin[i];
+        uint8_t* d = c->d_stage[i];
+        const uint8_t* sts = (direct && status) ? status + b0 : h + L.status;
+        size_t nchg = 0;
+        for (size_t b = 0; b < nb; ++b)
+            nchg += sts[b] == 1;
+        eager = nchg > nb / kGatherDiv;
+        if (nchg == 0)
+            return 0;
+        if (!fetched[i]) {
+            HIP_TRY(dma_async(h + L.patch, d + L.patch, nb * S * sizeof(uint32_t), hipMemcpyDeviceToHost, s_in), "D2H patch");
+            HIP_TRY(hipStreamSynchronize(s_in), "sync");
+        }
+        const uint32_t* P = (const uint32_t*)(h + L.patch);
+        uint8_t* img = raw + b0 * c->raw;
+        const size_t n = c->raw;
+        constexpr size_t kPart = 4096; // blocks per pool item
+        std::atomic<bool> overflow { false };
+        const std::function<void(size_t)> part = [&](size_t p) {
+            const size_t e = std::min(nb, (p + 1) * kPart);
+            for (size_t b = p * kPart; b < e; ++b) {
+                if (sts[b] != 1)
+                    continue;
+                const uint32_t* q = P + b * S;
+                if (q[0] == 0xFFFFFFFEu) {
+                    overflow.store(true, std::memory_order_relaxed);
+                    continue;
+                }
+                for (uint32_t j = 0; j < S && q[j] != 0xFFFFFFFFu; ++j)
+                    img[b * n + (q[j] >> 8)] = (uint8_t)q[j];
+            }
+        };
+        const size_t parts = (nb + kPart - 1) / kPart;
+        if (parts > 1 && nchg > 4 * kPart && !g_fork_child.load(std::memory_order_relaxed) && copy_threads() > 1)
+            CopyPool::get().run_for(parts, part);
+        else
+            for (size_t p = 0; p < parts; ++p)
+                part(p);
+        if (!overflow.load())
+            return 0;
+        uint32_t* ix = (uint32_t*)(h + L.idx);
+        const size_t cap = nb / kGatherDiv + 1; // the gather region's rows
+        size_t nov = 0;
+        for (size_t b = 0; b < nb; ++b) {
+            if (sts[b] != 1 || P[b * S] != 0xFFFFFFFEu)
+                continue;
+            ix[nov++] = (uint32_t)b;
+            if (nov == cap || b + 1 == nb) {
+                HIP_TRY(dma_async(d + L.idx, ix, nov * sizeof(uint32_t), hipMemcpyHostToDevice, s_in), "H2D idx");
+                HIP_TRY(ppfs_gather_rows_launch(d + L.raw, nb, d + L.gat, (const uint32_t*)(d + L.idx), (uint32_t)nov,
+                            (uint32_t)n, s_in), "gather");
+                HIP_TRY(dma_async(h + L.gat, d + L.gat, nov * n, hipMemcpyDeviceToHost, s_in), "D2H gather");
+                HIP_TRY(hipStreamSynchronize(s_in), "sync");
+                for (size_t j = 0; j < nov; ++j)
+                    std::memcpy(img + (size_t)ix[j] * n, h + L.gat + j * n, n);
+                nov = 0;
+            }
+        }
+        if (nov) {
+            HIP_TRY(dma_async(d + L.idx, ix, nov * sizeof(uint32_t), hipMemcpyHostToDevice, s_in), "H2D idx");
+            HIP_TRY(ppfs_gather_rows_launch(d + L.raw, nb, d + L.gat, (const uint32_t*)(d + L.idx), (uint32_t)nov,
+                        (uint32_t)n, s_in), "gather");
+            HIP_TRY(dma_async(h + L.gat, d + L.gat, nov * n, hipMemcpyDeviceToHost, s_in), "D2H gather");
+            HIP_TRY(hipStreamSynchronize(s_in), "sync");
+            for (size_t j = 0; j < nov; ++j)
+                std::memcpy(img + (size_t)ix[j] * n, h + L.gat + j * n, n);
+        }
+        return 0;
+    };
+
     auto drain = [&](int i) -> int {
         if (!busy[i])
             return 0;
         HIP_TRY(hipEventSynchronize(c->hev[i][1]), "sync");
         const size_t b0 = pending_first[i], nb = pending_n[i];
         if (lazy_raw) {
-            const int e = fetch_changed(i, b0, nb);
+            const int e = patched[i] ? apply_patches(i, b0, nb) : fetch_changed(i, b0, nb);
             if (e)
                 return e;
         }
@@ -2263,6 +2388,11 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
             const size_t in_hi = need_raw ? L.raw + nb * c->raw : L.data + nb * c->data;
             HIP_TRY(dma_async(d + in_lo, h + in_lo, in_hi - in_lo, hipMemcpyHostToDevice, s), "H2D");
         }
+        // patch lists for the big chunks (the small-batch path takes its whole staging span back)
+        const bool patch_now = S && (direct || nb * (c->raw + c->data) > (64u << 10));
+        if (patch_now) // the codewords as they came, for the patch list after the decode (on the input
+            // stream, which a decode leaves half idle, not ahead of the kernel on the output stream)
+            HIP_TRY(ppfs_copy_launch(d + L.orig, d + L.raw, nb * c->raw, s_in), "orig copy");
         HIP_TRY(hipEventRecord(ev[0], s_in), "event");
         HIP_TRY(hipStreamWaitEvent(s_out, ev[0], 0), "wait");
         s = s_out;
@@ -2281,7 +2411,8 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
         if (r)
             return r;
         // outputs device -> pinned staging (or straight to page-locked caller buffers)
-        const bool want_raw = op == OP_ENCODE || op == OP_WRITE || (lazy_raw && eager);
+        const bool want_raw = op == OP_ENCODE || op == OP_WRITE || (lazy_raw && eager && !patch_now);
+        patched[slot] = patch_now;
         const bool want_data = op == OP_DECODE && data_out;
         const bool want_st = (status || lazy_raw) && op != OP_ENCODE;
         if (!direct && nb * (c->raw + c->data) <= (64u << 10)) {
@@ -2305,6 +2436,13 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
                 HIP_TRY(dma_async(o_st, d + L.status, nb, hipMemcpyDeviceToHost, s), "D2H status");
             if (spill)
                 HIP_TRY(dma_async(o_sp, d + L.spill, nb * spill_b, hipMemcpyDeviceToHost, s), "D2H spill");
+            if (patch_now) {
+                HIP_TRY(ppfs_patch_list_launch(d + L.raw, d + L.orig, d + L.status, c->raw, nb, S, (uint32_t*)(d + L.patch), s),
+                    "patch list");
+                if (eager) // the list comes back behind the kernel (fetched: apply_patches takes it as landed)
+                    HIP_TRY(dma_async(h + L.patch, d + L.patch, nb * S * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H patch");
+                fetched[slot] = eager;
+            }
         }
         HIP_TRY(hipEventRecord(ev[1], s_out), "event");
         pending_first[slot] = b0;
@@ -2318,6 +2456,8 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
         c->host_eager = eager;
     return 0;
 }
+
+extern "C" size_t ppfs_ecc_host_chunk_blocks(ppfs_ecc_ctx* c) { return c ? chunk_blocks(c) : 0; }
 
 extern "C" int ppfs_ecc_encode_host(ppfs_ecc_ctx* c, const uint8_t* data, uint8_t* raw, size_t nblocks)
 {

@@ -71,6 +71,60 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* __restr
 }
 } // namespace ppfs
 
+// ---- patch list of a decode's write-back (api.cpp host_run_chunks) ----
+// The bytes a decode with write-back changed, for the host to patch into its image instead of
+// copying every changed codeword back: block b with status[b] == 1 gets (pos << 8 | byte) for each
+// byte where cur differs from orig (the codeword before the decode) in patch[b S .. b S + S - 1],
+// in position order, its unused slots ~0; a block with more than S changed bytes gets 0xFFFFFFFE in
+// slot 0 (the host fetches that codeword whole).  Other blocks' slots are not written.  One wave
+// per block, byte loads coalesced across the lanes, a ballot prefix for the slot of each change.
+namespace ppfs {
+__global__ __launch_bounds__(256) void patch_list_kernel(const uint8_t* __restrict__ cur, const uint8_t* __restrict__ orig,
+    const uint8_t* __restrict__ status, uint32_t n, uint64_t nb, uint32_t S, uint32_t* __restrict__ patch)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t b = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); b < nb; b += nw) {
+        if (!PPFS_DBG_OK(status + b, 1, status, nb) || status[b] != 1)
+            continue;
+        const uint8_t* c = cur + b * n;
+        const uint8_t* o = orig + b * n;
+        uint32_t* slot = patch + b * S;
+        uint32_t cnt = 0;
+        for (uint32_t j0 = 0; j0 < n; j0 += 64u) {
+            const uint32_t j = j0 + lane;
+            const uint32_t cv = j < n && PPFS_DBG_OK(c + j, 1, cur, nb * n) ? c[j] : 0u;
+            const uint32_t ov = j < n && PPFS_DBG_OK(o + j, 1, orig, nb * n) ? o[j] : 0u;
+            const bool d = j < n && cv != ov;
+            const uint64_t m = __builtin_amdgcn_ballot_w64(d);
+            const uint32_t idx = cnt + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+            if (d && idx < S && PPFS_DBG_OK(slot + idx, 4, patch, nb * S * 4))
+                slot[idx] = j << 8 | cv;
+            cnt += (uint32_t)__builtin_popcountll(m);
+        }
+        if (cnt > S) {
+            if (lane == 0 && PPFS_DBG_OK(slot, 4, patch, nb * S * 4))
+                slot[0] = 0xFFFFFFFEu;
+        } else {
+            for (uint32_t j = cnt + lane; j < S; j += 64u)
+                if (PPFS_DBG_OK(slot + j, 4, patch, nb * S * 4))
+                    slot[j] = 0xFFFFFFFFu;
+        }
+    }
+}
+} // namespace ppfs
+
+extern "C" hipError_t ppfs_patch_list_launch(const uint8_t* cur, const uint8_t* orig, const uint8_t* status, uint32_t n,
+    uint64_t nb, uint32_t S, uint32_t* patch, hipStream_t s)
+{
+    if (nb == 0)
+        return hipSuccess;
+    const uint64_t want = (nb + 3) / 4;
+    const uint32_t grid = (uint32_t)(want < 8192 ? want : 8192);
+    hipLaunchKernelGGL(ppfs::patch_list_kernel, dim3(grid), dim3(256), 0, s, cur, orig, status, n, nb, S, patch);
+    return hipGetLastError();
+}
+
 // ---- device copy at the HBM ceiling (measurement reference for bench.py's roofline) ----
 // One thread per 16 bytes over a full grid (workgroups dispatched in address order: one
 // contiguous window of HBM in flight), plain 16-byte loads and stores; ragged ends by bytes.

@@ -149,6 +149,10 @@ class EccEngine:
         self._check("host", n, data, raw, status)
         check(lib().ppfs_ecc_write_host(self._h, _ptr(data), _ptr(raw), _ptr(status), n))
 
+    def host_chunk_blocks(self) -> int:
+        """Blocks per staging chunk of the *_host calls (ppfs_ecc_host_chunk_blocks)."""
+        return int(lib().ppfs_ecc_host_chunk_blocks(self._h))
+
     def spill_bytes_per_block(self) -> int:
         return 256 - min(self.raw_block_size, 255)
 

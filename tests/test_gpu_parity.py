@@ -496,16 +496,16 @@ def test_write_rmw_matches_oracle(oracle, codec):
 # ------------------------------------------------------------------------------------
 # host-memory path (pinned staging, several chunks)
 # ------------------------------------------------------------------------------------
-HOST_CHUNK = 1 << 16  # api.cpp kChunkBlocks: blocks per staging chunk of the host calls
-
-
-@pytest.mark.parametrize("nb", [4 * HOST_CHUNK + 8001, 8 * HOST_CHUNK + 12345], ids=["5chunks", "ramp"])
-def test_host_path_multichunk(oracle, nb):
-    # 5 chunks of 64 Ki blocks (the last one ragged): every staging slot is reused at least once;
-    # 8+ chunks: the ramped chunk sizes (api.cpp ramp_chunk: 8 Ki, 16 Ki, 32 Ki, 64 Ki ... halving tail)
+@pytest.mark.parametrize("chunks", [4, 8], ids=["5chunks", "ramp"])
+def test_host_path_multichunk(oracle, chunks):
+    # 4 chunks of ppfs_ecc_host_chunk_blocks (64 Ki RS(255,249) blocks) and a ragged one: every
+    # staging slot is reused at least once; 8+ chunks: the ramped chunk sizes (api.cpp ramp_chunk:
+    # 8 Ki, 16 Ki, 32 Ki, 64 Ki ... halving tail).  The 1-error decode returns patch lists.
     bs, t = 512, 3
     n, k, _ = oracle.rs_sizes(bs, t)
     eng = EccEngine(ECC_REED_SOLOMON, bs, t)
+    assert eng.host_chunk_blocks() == 1 << 16
+    nb = chunks * eng.host_chunk_blocks() + (8001 if chunks == 4 else 12345)
     rng = rng_for("host")
     data = rng.integers(0, 256, nb * k, dtype=np.uint8)
     raw = np.zeros(nb * n, np.uint8)
@@ -567,20 +567,21 @@ def test_host_path_pinned_equals_pageable(typ, bs, t, poly):
 def test_host_decode_returns_only_changed_codewords(oracle, kind, codec, prior):
     """decode_host with write-back fetches codewords back only where the decode changed them
     (status 1): not at all for a clean chunk, as a packed gather for a few, as the whole range for
-    many.  Chunks of 64 Ki blocks: clean / 100 errors / every block / 5,000 blocks / a short tail;
+    many (RS(255, k) and Hamming: as patch lists of the changed bytes).  One set per chunk
+    (ppfs_ecc_host_chunk_blocks): clean / 100 errors / every block / 5,000 blocks / a short tail;
     every path must leave the caller's image equal to the oracle's write-back.  prior="eager": the
     context's previous call ended on a chunk where every block changed, so this call's first chunks
     (queued before any has landed: api.cpp host_run_chunks, three staging slots) fetch their
     codewords eagerly."""
     from paritypartyfs_amd import pinned
 
-    ch = HOST_CHUNK
-    nb = 4 * ch + 777
     rng = rng_for("lazyraw", codec, kind)
     if codec == "rs512":
         eng = EccEngine(ECC_REED_SOLOMON, 512, 3)
     else:
         eng = EccEngine(ECC_HAMMING, 1024, 0)
+    ch = eng.host_chunk_blocks()
+    nb = 4 * ch + 777
     n, k = eng.raw_block_size, eng.data_size
     data = rng.integers(0, 256, nb * k, dtype=np.uint8)
     raw = np.zeros(nb * n, np.uint8)
@@ -717,3 +718,43 @@ def test_crc4096_small_batches_match_oracle(oracle, nb):
     eng.decode(dev(bad), data_d, st_d, nblocks=nb)
     assert np.array_equal(host(st_d), o_st)
     assert np.array_equal(host(data_d), o_data)
+
+
+@pytest.mark.parametrize("bs,t", [(512, 3), (4096, 16)], ids=["t3", "t16"])
+@pytest.mark.parametrize("kind", ["pageable", "pinned"])
+def test_host_decode_patch_lists_many_errors(oracle, bs, t, kind):
+    """decode_host with write-back over two chunks with 0 .. t + 3 byte errors per block: the patch
+    lists carry every byte the write-back changed, miscorrections (more than t errors) included --
+    the caller's image must equal the oracle's write-back exactly."""
+    from paritypartyfs_amd import pinned
+
+    eng = EccEngine(ECC_REED_SOLOMON, bs, t)
+    n, k = eng.raw_block_size, eng.data_size
+    nb = 2 * eng.host_chunk_blocks() + 333
+    rng = rng_for("patch-many", bs, kind)
+    data = rng.integers(0, 256, nb * k, dtype=np.uint8)
+    raw = np.zeros(nb * n, np.uint8)
+    eng.encode_host(data, raw)
+    bad = raw.reshape(nb, n).copy()
+    ne = np.arange(nb) % (t + 4)
+    for e in range(1, t + 4):
+        rows = np.nonzero(ne == e)[0]
+        cols = np.argsort(rng.random((rows.size, n)), axis=1)[:, :e]
+        bad[rows[:, None], cols] ^= rng.integers(1, 256, (rows.size, e), dtype=np.uint8)
+    bad = bad.reshape(-1)
+    o_data, o_st, o_fixed, _, _ = oracle.rs_decode(bs, t, bad)
+    img = bad.copy()
+    out = np.zeros(nb * k, np.uint8)
+    st = np.full(nb, 77, np.uint8)
+    ctx = pinned(img, out, st) if kind == "pinned" else None
+    if ctx:
+        ctx.__enter__()
+    try:
+        eng.decode_host(img, out, st, write_back=True)
+    finally:
+        if ctx:
+            ctx.__exit__(None, None, None)
+    assert np.array_equal(st, o_st)
+    assert np.array_equal(img, o_fixed)
+    assert np.array_equal(out, o_data)
+    eng.close()
