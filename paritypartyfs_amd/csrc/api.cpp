@@ -80,7 +80,7 @@ hipError_t ppfs_vote3_launch(const uint8_t* a, const uint8_t* b, const uint8_t* 
     uint64_t nrec, uint32_t* damaged, hipStream_t s);
 hipError_t ppfs_copy_launch(uint8_t* dst, const uint8_t* src, uint64_t bytes, hipStream_t s);
 hipError_t ppfs_patch_list_launch(const uint8_t* cur, const uint8_t* orig, const uint8_t* status, uint32_t n, uint64_t nb,
-    uint32_t S, uint32_t* patch, hipStream_t s);
+    uint32_t S, uint32_t* patch, uint8_t* image, hipStream_t s);
 hipError_t ppfs_inject_launch(uint8_t* raw, uint64_t stride, uint64_t nblocks, const uint8_t* pos, const uint8_t* val,
     int mode, hipStream_t s);
 }
@@ -2188,7 +2188,7 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
     hipStream_t s_in = c->hs[0], s_out = c->hs[1];
     size_t pending_first[NS] = {}, pending_n[NS] = {};
     // fetched: the chunk's codewords already came back (staging, or the caller's page-locked image)
-    bool busy[NS] = {}, fetched[NS] = {}, patched[NS] = {};
+    bool busy[NS] = {}, fetched[NS] = {}, patched[NS] = {}, landed[NS] = {};
     // every caller buffer page-locked: DMA straight between it and the device staging buffers
     const bool direct = host_pinned(data_in, nblocks * c->data) && host_pinned(data_out, nblocks * c->data)
         && host_pinned(raw, nblocks * c->raw) && host_pinned(status, nblocks) && host_pinned(spill, nblocks * spill_b);
@@ -2199,6 +2199,13 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
     // ... and as a patch list (the changed bytes) where the codec bounds them (patch_slots): the
     // host writes those bytes into its image instead of taking back whole codewords
     const uint32_t S = lazy_raw ? patch_slots(c) : 0u;
+    // a page-locked caller image the device can address: the patch kernel stores the changed bytes
+    // straight into it (no list, no host work); else the list comes back and the host applies it
+    uint8_t* img_dev = nullptr;
+    if (S && direct && hipHostGetDevicePointer((void**)&img_dev, raw, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        img_dev = nullptr;
+    }
     // predictor: the last drained chunk changed many codewords -> fetch the next ones eagerly
     // (queued behind the kernel, as encode does) instead of after the status has landed.  It starts
     // where the context's previous call left it: the first kSlots chunks are queued before any has
@@ -2331,7 +2338,7 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
         HIP_TRY(hipEventSynchronize(c->hev[i][1]), "sync");
         const size_t b0 = pending_first[i], nb = pending_n[i];
         if (lazy_raw) {
-            const int e = patched[i] ? apply_patches(i, b0, nb) : fetch_changed(i, b0, nb);
+            const int e = landed[i] ? 0 : patched[i] ? apply_patches(i, b0, nb) : fetch_changed(i, b0, nb);
             if (e)
                 return e;
         }
@@ -2412,7 +2419,8 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
             return r;
         // outputs device -> pinned staging (or straight to page-locked caller buffers)
         const bool want_raw = op == OP_ENCODE || op == OP_WRITE || (lazy_raw && eager && !patch_now);
-        patched[slot] = patch_now;
+        patched[slot] = patch_now && !img_dev;
+        landed[slot] = patch_now && img_dev; // the write-back goes straight into the caller's image
         const bool want_data = op == OP_DECODE && data_out;
         const bool want_st = (status || lazy_raw) && op != OP_ENCODE;
         if (!direct && nb * (c->raw + c->data) <= (64u << 10)) {
@@ -2437,11 +2445,11 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
             if (spill)
                 HIP_TRY(dma_async(o_sp, d + L.spill, nb * spill_b, hipMemcpyDeviceToHost, s), "D2H spill");
             if (patch_now) {
-                HIP_TRY(ppfs_patch_list_launch(d + L.raw, d + L.orig, d + L.status, c->raw, nb, S, (uint32_t*)(d + L.patch), s),
-                    "patch list");
-                if (eager) // the list comes back behind the kernel (fetched: apply_patches takes it as landed)
+                HIP_TRY(ppfs_patch_list_launch(d + L.raw, d + L.orig, d + L.status, c->raw, nb, S, (uint32_t*)(d + L.patch),
+                            img_dev ? img_dev + b0 * c->raw : nullptr, s), "patch list");
+                if (eager && !img_dev) // the list comes back behind the kernel (fetched: apply_patches takes it as landed)
                     HIP_TRY(dma_async(h + L.patch, d + L.patch, nb * S * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H patch");
-                fetched[slot] = eager;
+                fetched[slot] = eager && !img_dev;
             }
         }
         HIP_TRY(hipEventRecord(ev[1], s_out), "event");

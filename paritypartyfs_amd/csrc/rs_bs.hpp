@@ -194,9 +194,10 @@ __device__ __forceinline__ void bs_cmodg(uint32_t (&s)[4], const uint8_t* lds, u
 // data exchanged through DPP instead of an LDS slot (both lanes of a pair take this path together).
 // Lane c computes S_i, i = 16c+1 .. 16c+16, over the whole c mod g state (coefficient q has
 // exponent i q); lane 0 then holds S_1..S_32 and runs BM / roots / Forney.
-template <int T2>
-__device__ __noinline__ void bs_correct_general(uint8_t* lds, const uint8_t* gfp, uint32_t row, uint32_t c, uint32_t s0,
-    uint32_t s1, uint32_t s2, uint32_t s3, uint8_t* __restrict__ raw_g, uint64_t gblk, bool wb, uint64_t raw_bytes)
+// fix(pos, e) is called (lane 0 of the pair) for every root of sigma.
+template <int T2, typename Fix>
+__device__ __noinline__ void bs_correct_general_f(const uint8_t* gfp, uint32_t c, uint32_t s0, uint32_t s1, uint32_t s2,
+    uint32_t s3, Fix fix)
 {
     static_assert(T2 == 32, "state byte q = coefficient q");
     const Gf gf { gfp };
@@ -232,8 +233,15 @@ __device__ __noinline__ void bs_correct_general(uint8_t* lds, const uint8_t* gfp
 #pragma unroll
         for (int i = 0; i < T2; ++i)
             S[i] = ((i < 16 ? sw[i >> 2] : hi[(i - 16) >> 2]) >> (8 * (i & 3))) & 0xFFu;
-        rs_correct_general<T2>(S, gf, [&](uint32_t pos, uint32_t ev) { col::col_fix(lds, row, raw_g, gblk, wb, pos, ev, raw_bytes); });
+        rs_correct_general<T2>(S, gf, fix);
     }
+}
+template <int T2>
+__device__ __forceinline__ void bs_correct_general(uint8_t* lds, const uint8_t* gfp, uint32_t row, uint32_t c, uint32_t s0,
+    uint32_t s1, uint32_t s2, uint32_t s3, uint8_t* __restrict__ raw_g, uint64_t gblk, bool wb, uint64_t raw_bytes)
+{
+    bs_correct_general_f<T2>(gfp, c, s0, s1, s2, s3,
+        [=](uint32_t pos, uint32_t ev) { col::col_fix(lds, row, raw_g, gblk, wb, pos, ev, raw_bytes); });
 }
 
 // Decode correction for the pair's block: rs_pair.hpp pair_correct (single error: X = S_2/S_1,

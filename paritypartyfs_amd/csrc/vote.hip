@@ -76,11 +76,14 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const uint8_t* __restr
 // copying every changed codeword back: block b with status[b] == 1 gets (pos << 8 | byte) for each
 // byte where cur differs from orig (the codeword before the decode) in patch[b S .. b S + S - 1],
 // in position order, its unused slots ~0; a block with more than S changed bytes gets 0xFFFFFFFE in
-// slot 0 (the host fetches that codeword whole).  Other blocks' slots are not written.  One wave
-// per block, byte loads coalesced across the lanes, a ballot prefix for the slot of each change.
+// slot 0 (the host fetches that codeword whole).  Other blocks' slots are not written.  With
+// `image` (a device pointer to the caller's page-locked image, row b at image + b n) the changed
+// bytes are stored there instead, over the link, and no list is made.  One wave per block, byte
+// loads coalesced across the lanes, a ballot prefix for the slot of each change.
 namespace ppfs {
 __global__ __launch_bounds__(256) void patch_list_kernel(const uint8_t* __restrict__ cur, const uint8_t* __restrict__ orig,
-    const uint8_t* __restrict__ status, uint32_t n, uint64_t nb, uint32_t S, uint32_t* __restrict__ patch)
+    const uint8_t* __restrict__ status, uint32_t n, uint64_t nb, uint32_t S, uint32_t* __restrict__ patch,
+    uint8_t* __restrict__ image)
 {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -96,12 +99,19 @@ __global__ __launch_bounds__(256) void patch_list_kernel(const uint8_t* __restri
             const uint32_t cv = j < n && PPFS_DBG_OK(c + j, 1, cur, nb * n) ? c[j] : 0u;
             const uint32_t ov = j < n && PPFS_DBG_OK(o + j, 1, orig, nb * n) ? o[j] : 0u;
             const bool d = j < n && cv != ov;
+            if (image) {
+                if (d)
+                    image[b * n + j] = (uint8_t)cv;
+                continue;
+            }
             const uint64_t m = __builtin_amdgcn_ballot_w64(d);
             const uint32_t idx = cnt + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
             if (d && idx < S && PPFS_DBG_OK(slot + idx, 4, patch, nb * S * 4))
                 slot[idx] = j << 8 | cv;
             cnt += (uint32_t)__builtin_popcountll(m);
         }
+        if (image)
+            continue;
         if (cnt > S) {
             if (lane == 0 && PPFS_DBG_OK(slot, 4, patch, nb * S * 4))
                 slot[0] = 0xFFFFFFFEu;
@@ -115,13 +125,13 @@ __global__ __launch_bounds__(256) void patch_list_kernel(const uint8_t* __restri
 } // namespace ppfs
 
 extern "C" hipError_t ppfs_patch_list_launch(const uint8_t* cur, const uint8_t* orig, const uint8_t* status, uint32_t n,
-    uint64_t nb, uint32_t S, uint32_t* patch, hipStream_t s)
+    uint64_t nb, uint32_t S, uint32_t* patch, uint8_t* image, hipStream_t s)
 {
     if (nb == 0)
         return hipSuccess;
     const uint64_t want = (nb + 3) / 4;
     const uint32_t grid = (uint32_t)(want < 8192 ? want : 8192);
-    hipLaunchKernelGGL(ppfs::patch_list_kernel, dim3(grid), dim3(256), 0, s, cur, orig, status, n, nb, S, patch);
+    hipLaunchKernelGGL(ppfs::patch_list_kernel, dim3(grid), dim3(256), 0, s, cur, orig, status, n, nb, S, patch, image);
     return hipGetLastError();
 }
 
