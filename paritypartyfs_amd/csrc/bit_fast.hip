@@ -82,6 +82,25 @@ constexpr int BF_BPW = 1;
 
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 
+// Workgroup -> block range, XCD-local (round 6).  The dispatcher places workgroup b on XCD b % 8
+// (MI355X_MICROARCH.md: the placement is for speed only, so this is a bijection on [0, gridDim.x)
+// whatever it is); remapped, each XCD's workgroups take one contiguous range of blocks, so
+// neighbouring blocks -- which share the 128-B lines at their unaligned payload-row boundaries, where
+// each writes a partial 16-B piece -- meet in one L2 instead of two (the workgroups in flight are
+// then 8 contiguous HBM windows, one per XCD).  Configs leg, 3 interleaved rounds (r6m): Hamming
+// decode clean 1.471-1.473 vs 1.515-1.522 ms, 1-error 1.510-1.525 vs 1.586-1.597, encode
+// 1.403-1.413 vs 1.419; parity check 1.387-1.391 vs 1.438-1.445, encode 1.318-1.321 vs 1.327-1.329;
+// CRC check 1.584-1.600 vs 1.609-1.614; the CRC encode (24 blocks per workgroup, so its boundaries
+// were mostly inside one workgroup) 1.548-1.555 vs 1.543-1.547 keeps the dispatch order.
+template <bool XCD> __device__ __forceinline__ uint32_t bf_wg()
+{
+    const uint32_t b = blockIdx.x, G = gridDim.x;
+    if (!XCD || G < 64u)
+        return b;
+    const uint32_t x = b & 7u, r = b >> 3, per = G >> 3, rem = G & 7u;
+    return x * per + (x < rem ? x : rem) + r;
+}
+
 // Hamming decode: the LDS image stores issued before the syndrome reduction (round 5), so they
 // complete under its DPP chain (after it: configs leg, 3 interleaved rounds, r5hei: clean
 // 1.512-1.523 vs 1.531 ms, 1-error 1.582-1.590 vs 1.588-1.602 ms).  Status bytes and corrected-byte
@@ -203,7 +222,7 @@ __global__ __launch_bounds__(64 * WV) void ham_fast_encode_kernel(const uint8_t*
     const uint32_t lane = lane_id(), wave = wave_id();
     uint8_t* buf = lds + wave * BUF;
     const uint32_t nwords = a.bs / 4, lastw = nwords - 1;
-    const uint64_t wg0 = (uint64_t)blockIdx.x * (WV * BF_BPW);
+    const uint64_t wg0 = (uint64_t)bf_wg<true>() * (WV * BF_BPW);
     const uint64_t nblocks = nblocks_all < wg0 + WV * BF_BPW ? nblocks_all : wg0 + WV * BF_BPW;
     const uint64_t stride = WV;
     uint64_t blk = wg0 + wave;
@@ -389,7 +408,7 @@ __global__ __launch_bounds__(64 * WV) void ham_fast_decode_kernel(uint8_t* __res
     const uint32_t lane = lane_id(), wave = wave_id();
     uint8_t* img = lds + wave * BUF;
     const uint32_t lastw = a.bs / 4 - 1;
-    const uint64_t wg0 = (uint64_t)blockIdx.x * (WV * BF_BPW);
+    const uint64_t wg0 = (uint64_t)bf_wg<true>() * (WV * BF_BPW);
     const uint64_t nblocks = nblocks_all < wg0 + WV * BF_BPW ? nblocks_all : wg0 + WV * BF_BPW;
     const uint64_t stride = WV;
     uint64_t blk = wg0 + wave;
@@ -595,7 +614,7 @@ __global__ __launch_bounds__(64 * WV) void parity_fast_encode_kernel(const uint8
     const uint32_t lane = lane_id(), wave = wave_id();
     const uint32_t ds = a.bs - 1;
     const HamFast ha { a.bs, ds, 0, a.data_bytes };
-    const uint64_t wg0 = (uint64_t)blockIdx.x * (WV * BF_BPW);
+    const uint64_t wg0 = (uint64_t)bf_wg<true>() * (WV * BF_BPW);
     const uint64_t nblocks = nblocks_all < wg0 + WV * BF_BPW ? nblocks_all : wg0 + WV * BF_BPW;
     const uint64_t stride = WV;
     uint64_t blk = wg0 + wave;
@@ -643,7 +662,7 @@ __global__ __launch_bounds__(64 * WV) void parity_fast_check_kernel(const uint8_
 {
     const uint32_t lane = lane_id(), wave = wave_id();
     const uint32_t ds = a.bs - 1;
-    const uint64_t wg0 = (uint64_t)blockIdx.x * (WV * BF_BPW);
+    const uint64_t wg0 = (uint64_t)bf_wg<true>() * (WV * BF_BPW);
     const uint64_t nblocks = nblocks_all < wg0 + WV * BF_BPW ? nblocks_all : wg0 + WV * BF_BPW;
     const uint64_t stride = WV;
     uint64_t blk = wg0 + wave;
@@ -941,7 +960,7 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ENC_ATTR void crc_fast_encode_ker
     const uint32_t lane = lane_id(), wave = WV > 1 ? wave_id() : 0u;
     const HamFast ha { a.bs, a.ds, 0, a.data_bytes };
     const bool n32 = a.n == 32;
-    const uint64_t wg0 = (uint64_t)blockIdx.x * (WV * BPW);
+    const uint64_t wg0 = (uint64_t)bf_wg<false>() * (WV * BPW);
     const uint64_t nblocks = nblocks_all < wg0 + WV * BPW ? nblocks_all : wg0 + WV * BPW;
     const uint64_t stride = WV;
     uint64_t blk = wg0 + wave;
@@ -1023,7 +1042,7 @@ __global__ __launch_bounds__(64 * WV) PPFS_CRC_ATTR void crc_fast_check_kernel(c
     const uint32_t lane = lane_id(), wave = WV > 1 ? wave_id() : 0u;
     const bool n32 = a.n == 32;
     const uint32_t ds = a.ds;
-    const uint64_t wg0 = (uint64_t)blockIdx.x * (WV * BPW);
+    const uint64_t wg0 = (uint64_t)bf_wg<true>() * (WV * BPW);
     const uint64_t nblocks = nblocks_all < wg0 + WV * BPW ? nblocks_all : wg0 + WV * BPW;
     const uint64_t stride = WV;
     uint64_t blk = wg0 + wave;
