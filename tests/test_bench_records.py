@@ -33,6 +33,33 @@ def test_committed_pmc_summary_covers_the_bench_kernels():
         assert v["blocks"] > 0 and v["hbm_bytes_per_launch"] > 0
 
 
+def test_pmc_merge_keeps_each_kernels_in_step_entry():
+    """tools/pmc_summary.py merge_latest: profiles of one build merge, each kernel keeping the run
+    whose bench step launched it; another build replaces the file."""
+    from tools.pmc_summary import merge_latest
+
+    head = {"rs_wg_decode_tk_kernel<6>": {"blocks": 1 << 20, "hbm_bytes_per_launch": 567e6, "in_step_launches": 9466},
+            "rs_bs_decode_kernel<32>": {"blocks": 1 << 20, "hbm_bytes_per_launch": 510e6}}
+    cfg5 = {"rs_wg_decode_tk_kernel<6>": {"blocks": 1 << 20, "hbm_bytes_per_launch": 534e6},
+            "rs_bs_decode_kernel<32>": {"blocks": 1 << 20, "hbm_bytes_per_launch": 543e6, "in_step_launches": 7690}}
+    a = merge_latest({}, head, "s" * 64, "r6fin")
+    b = merge_latest(a, cfg5, "s" * 64, "r6fin_cfg5")
+    assert b["tag"] == "r6fin+r6fin_cfg5"
+    assert b["kernels"]["rs_wg_decode_tk_kernel<6>"]["hbm_bytes_per_launch"] == 567e6  # the headline run's
+    assert b["kernels"]["rs_bs_decode_kernel<32>"]["hbm_bytes_per_launch"] == 543e6  # the cfg5 run's
+    c = merge_latest(b, cfg5, "t" * 64, "r7")
+    assert c["tag"] == "r7" and c["kernels"] == cfg5
+
+
+def test_committed_pmc_headline_entries_are_in_step():
+    """The committed summary's headline kernels come from the headline profile: in-step launches, and
+    the 1-error decode's traffic carries its 2^20 one-byte write-backs (above the algorithmic bytes)."""
+    ks = json.load(open(bench.os.path.join(bench.ROOT, "profiles", "pmc_latest.json")))["kernels"]
+    for name in ("rs_wg_encode_tk_kernel<6>", "rs_wg_decode_tk_kernel<6>"):
+        assert ks[name].get("in_step_launches", 0) > 0
+    assert ks["rs_wg_decode_tk_kernel<6>"]["hbm_bytes_per_launch"] > 1.05 * 528482304
+
+
 def test_config_lines_carry_cold_per_leg_fractions():
     """tools/bench_configs.py's lines (bench.py `configs`): one fraction per leg, the cold-set count,
     no max-over-legs figure (round 6: roofline_frac_best dropped); cfg5_step's in-step fields."""

@@ -142,20 +142,23 @@ def main():
         old = json.load(open(path))
     except Exception:
         old = {}
-    if old.get("lib_sha256") == lib_sha and lib_sha:
-        # a kernel profiled in both runs keeps the entry of the run whose bench step launched it (more
-        # in-step launches): the headline profile's 1-error t = 3 decode, not the cfg5 run's clean
-        # configs-leg decode of the same kernel
-        merged_k = dict(old.get("kernels", {}))
-        for k, v in latest.items():
-            if v.get("in_step_launches", 0) >= merged_k.get(k, {}).get("in_step_launches", 0):
-                merged_k[k] = v
-        tags = old.get("tag", "")
-        tag_out = tags if tag in tags.split("+") else tags + "+" + tag
-        json.dump({"tag": tag_out, "lib_sha256": lib_sha, "kernels": merged_k}, open(path, "w"), indent=1)
-    else:
-        json.dump({"tag": tag, "lib_sha256": lib_sha, "kernels": latest}, open(path, "w"), indent=1)
+    json.dump(merge_latest(old, latest, lib_sha, tag), open(path, "w"), indent=1)
     print("\n".join(lines))
+
+
+def merge_latest(old, latest, lib_sha, tag):
+    """pmc_latest.json after a profile `tag` of library `lib_sha`: a new build starts afresh; on the
+    same build, a kernel profiled in both runs keeps the entry of the run whose bench step launched it
+    (more in-step launches) -- the headline profile's 1-error t = 3 decode, not the cfg5 run's clean
+    configs-leg decode of the same kernel."""
+    if not (lib_sha and old.get("lib_sha256") == lib_sha):
+        return {"tag": tag, "lib_sha256": lib_sha, "kernels": latest}
+    merged_k = dict(old.get("kernels", {}))
+    for k, v in latest.items():
+        if v.get("in_step_launches", 0) >= merged_k.get(k, {}).get("in_step_launches", 0):
+            merged_k[k] = v
+    tags = old.get("tag", "")
+    return {"tag": tags if tag in tags.split("+") else tags + "+" + tag, "lib_sha256": lib_sha, "kernels": merged_k}
 
 
 if __name__ == "__main__":
