@@ -781,6 +781,10 @@ using CE = CrcLds<16>;
 // (12 x 2: 1.545-1.549, 8 x 4: 1.551-1.556, 5 x 4: 1.567-1.573, 4 x 4: 1.570-1.593, 6 x 8: 1.627);
 // the check on its 14 KiB image in 2-wave workgroups x 4: 1.586-1.605 vs 1.603-1.628 ms for 4 x 4
 // (2 x 2: 1.70, 2 x 1: 1.89, 1-wave workgroups: 1.77-2.12 -- the image then caps a CU at 11 waves).
+// Round 6, with the XCD-local block ranges (r6s / r6t, configs leg, 3 interleaved rounds): the check
+// in 4-wave workgroups x 4 1.594-1.606 vs 1.609-1.613 ms for 2 x 4 (8 x 4: 1.602-1.608, 3 x 4:
+// 1.610-1.621, 4 x 2: 1.620-1.628, 4 x 8: 1.635-1.639, 6 x 4: 1.757-1.762); the encode's shapes
+// with the XCD-local ranges (6 x 2 / 4 x 4 / 6 x 8) and 8 x 4 all ran at or above its 6 x 4.
 // (Register prefetch of a wave's next block and output stores issued before the lookups: slower,
 // DESIGN.md Appendix A, r5cpf / r5est.)
 constexpr int CRC_BPW = 4, CRC_CHK_BPW = 4;
@@ -1193,7 +1197,7 @@ template <int NP> static constexpr uint32_t par_chk_dyn_lds()
 // CRC check: PPFS_BF_CRC_CHK_WV waves per workgroup, PPFS_CRC_CHK_BPW blocks per wave, at most
 // PPFS_BF_CRC_CHK_WPC waves per CU (0: as registers allow)
 #ifndef PPFS_BF_CRC_CHK_WV
-#define PPFS_BF_CRC_CHK_WV 2
+#define PPFS_BF_CRC_CHK_WV 4
 #endif
 #ifndef PPFS_BF_CRC_CHK_WPC
 #define PPFS_BF_CRC_CHK_WPC 0
