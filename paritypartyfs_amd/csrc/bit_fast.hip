@@ -1138,8 +1138,9 @@ template <typename K> static uint32_t bf_grid(K, uint64_t nb, int wv = bf::WAVES
 // 14: 1.346-1.351, two-wave at 12: 1.346-1.349); parity check at 10 waves 1.462-1.463 vs 1.516-1.521
 // (8: 1.60, 12: 1.471-1.477); Hamming encode one-wave, uncapped (16 waves by registers) 1.418-1.423
 // vs 1.466-1.468 (two-wave 1.443-1.448, one-wave at 12: 1.494-1.497).  The Hamming decode keeps
-// 4-wave workgroups at 16 waves per CU: one-wave at 20 / 24 / 32 waves 1.545-1.561 / 1.611 vs
-// 1.523-1.527 ms clean, at 6 / 8 waves 3.10 / 2.41 ms (its per-block chain needs the waves).
+// 4-wave workgroups (round 5 at 16 waves per CU, round 6 at 24, below): one-wave at 20 / 24 / 32 waves
+// 1.545-1.561 / 1.611 vs 1.523-1.527 ms clean, at 6 / 8 waves 3.10 / 2.41 ms (its per-block chain
+// needs the waves); round 6: 2- and 8-wave workgroups at 16 waves 1.504-1.515 / 1.538-1.552 ms.
 #ifndef PPFS_BF_HAM_ENC_WV
 #define PPFS_BF_HAM_ENC_WV 1
 #endif
@@ -1162,18 +1163,24 @@ static constexpr uint32_t bf_occ_lds(int wg, uint32_t static_lds)
 {
     return wg <= 0 ? 0u : (163840u / (uint32_t)(wg + 1) + 256u > static_lds ? 163840u / (uint32_t)(wg + 1) + 256u - static_lds : 0u);
 }
-// Hamming / parity: the cap in waves per CU (0 = none), i.e. WV-wave workgroups per CU x WV
+// Hamming / parity: the cap in waves per CU (0 = none), i.e. WV-wave workgroups per CU x WV.
+// Re-swept in round 6 with the XCD-local block ranges (r6u / r6v, configs leg, 3 interleaved
+// rounds): the Hamming decode at 24 waves per CU clean 1.433-1.443 vs 1.487-1.497 ms at 16, 1-error
+// 1.493-1.506 vs 1.551-1.556 (20: 1.449-1.456 / 1.502-1.505, 28: 1.444-1.450 / 1.508-1.516,
+// uncapped: 1.463-1.465 / 1.534-1.536); the parity check at 12 1.371-1.374 vs 1.388-1.390 at 10
+// (11 / 14: the same as 12, 16: 1.378-1.380, 8: 1.52); the parity encode at 10 / 16 and the
+// Hamming encode at 12: the same or slower.
 #ifndef PPFS_BF_PAR_ENC_WPC
 #define PPFS_BF_PAR_ENC_WPC 12
 #endif
 #ifndef PPFS_BF_HAM_DEC_WPC
-#define PPFS_BF_HAM_DEC_WPC 16
+#define PPFS_BF_HAM_DEC_WPC 24
 #endif
 #ifndef PPFS_BF_HAM_ENC_WPC
 #define PPFS_BF_HAM_ENC_WPC 0
 #endif
 #ifndef PPFS_BF_PAR_CHK_WPC
-#define PPFS_BF_PAR_CHK_WPC 10
+#define PPFS_BF_PAR_CHK_WPC 12
 #endif
 static constexpr int bf_wg_cap(int wpc, int wv) { return wpc <= 0 ? 0 : (wpc / wv > 0 ? wpc / wv : 1); }
 template <int NP> static constexpr uint32_t par_enc_dyn_lds()
