@@ -102,7 +102,7 @@ def main():
         km, alg = line.get("kernels_ms", {}), line.get("roofline", {}).get("algorithmic_bytes_per_launch")
         lines += ["", f"Untraced bench line of the same command (same box, just before the trace): value {line.get('value')} "
                   f"GiB/s, roofline.frac {line.get('roofline', {}).get('frac')}, in-step frac {line.get('in_step_frac')}"]
-        for kind, pref in (("encode", ("rs_wg_encode_tk", "rs_bs_encode")), ("decode", ("rs_wg_decode_tk", "rs_bs_decode"))):
+        for kind, pref in step_kernels(line):
             for k, v in latest.items():
                 if k.startswith(pref) and km.get(kind) and alg and "avg_launch_ns_in_step" in v:
                     ri = v["avg_launch_ns_in_step"] / 1e6
@@ -118,7 +118,7 @@ def main():
         lines += ["", f"Bench line of the traced run: value {line.get('value')} GiB/s, in-step frac "
                   f"{line.get('in_step_frac')}, roofline.frac {line.get('roofline', {}).get('frac')}"]
         alg = line.get("roofline", {}).get("algorithmic_bytes_per_launch")
-        for kind, pref in (("encode", ("rs_wg_encode_tk", "rs_bs_encode")), ("decode", ("rs_wg_decode_tk", "rs_bs_decode"))):
+        for kind, pref in step_kernels(line):
             for k, v in latest.items():
                 if k.startswith(pref) and km.get(kind) and alg:
                     ra = v["avg_launch_ns"] / 1e6
@@ -144,6 +144,14 @@ def main():
         old = {}
     json.dump(merge_latest(old, latest, lib_sha, tag), open(path, "w"), indent=1)
     print("\n".join(lines))
+
+
+def step_kernels(line):
+    """(kind, kernel-name prefix) of the bench step's encode and decode: the 2t = 32 byte-slice kernels
+    when the line's roofline names one, else the t <= 4 ticket kernels (the configs leg's other
+    kernels in the same profile are not the step's)."""
+    bs = "rs_bs" in str(line.get("roofline", {}).get("kernel", ""))
+    return (("encode", "rs_bs_encode" if bs else "rs_wg_encode_tk"), ("decode", "rs_bs_decode" if bs else "rs_wg_decode_tk"))
 
 
 def merge_latest(old, latest, lib_sha, tag):
