@@ -54,7 +54,7 @@ hipError_t ppfs_bit_server_launch(int ecc_type, uint32_t bs, uint32_t ds, uint32
 hipError_t ppfs_rs_server_launch(int t2, ppfs::SrvBox* box, uint8_t* zc, uint64_t zc_bytes, const uint8_t* tab,
     uint32_t gen, uint32_t idle_us, hipStream_t s);
 hipError_t ppfs_rs_fast_decode(int t2, uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb, const uint8_t* tab, int wb,
-    hipStream_t s, uint32_t* ctr, uint32_t* ctr_clear);
+    hipStream_t s, uint32_t* ctr, uint32_t* ctr_clear, uint8_t* wb_dst);
 hipError_t ppfs_rs_generic_encode(const uint8_t* d, uint8_t* r, uint64_t nb, int n, int t2, const uint8_t* tab,
     hipStream_t s);
 hipError_t ppfs_rs_generic_decode(uint8_t* r, uint8_t* d, uint8_t* st, uint8_t* spill, uint64_t nb, int n, int t2,
@@ -1259,13 +1259,25 @@ static int ppfs_ecc_encode_device_impl(ppfs_ecc_ctx* c, const uint8_t* d_data, u
     return fail(PPFS_ECC_EINVAL, "bad ctx");
 }
 
+// The RS(255, 255 - 2t), 2t <= 8 decodes (rs_wg_tk.hpp / rs_wg.hpp) can put their write-backs
+// somewhere other than the codewords they read: the host path points them at a page-locked caller
+// image mapped into the device, so a chunk's corrections land there with no codeword copy and no
+// patch pass (round 6)
+static bool rs_wb_direct(const ppfs_ecc_ctx* c)
+{
+    return c->p.ecc_type == PPFS_ECC_REED_SOLOMON && c->rs_fast && c->rs_n == 255 && c->rs_t2 <= 8;
+}
+
+// wb_dst (the host path only, rs_wb_direct): the write-backs go there instead of into d_raw
 static int ppfs_ecc_decode_device_impl(ppfs_ecc_ctx* c, uint8_t* d_raw, uint8_t* d_data, uint8_t* d_status,
-    size_t nblocks, int write_back, uint8_t* d_spill, void* stream)
+    size_t nblocks, int write_back, uint8_t* d_spill, void* stream, uint8_t* wb_dst = nullptr)
 {
     if (!c || (nblocks && !d_raw))
         return fail(PPFS_ECC_EINVAL, "decode: null argument");
     if (nblocks == 0)
         return 0;
+    if (wb_dst && !rs_wb_direct(c))
+        return fail(PPFS_ECC_EINVAL, "decode: no direct write-back for this codec");
     hipStream_t s = (hipStream_t)stream;
     switch (c->p.ecc_type) {
     case PPFS_ECC_NONE:
@@ -1289,7 +1301,7 @@ static int ppfs_ecc_decode_device_impl(ppfs_ecc_ctx* c, uint8_t* d_raw, uint8_t*
             const TkSets t = ctr_for(c, s, 1);
             return check_hip(tk_commit(c, t,
                                  ppfs_rs_fast_decode(c->rs_t2, d_raw, d_data, d_status, nblocks, c->d_tables, write_back, s,
-                                     t.mine, t.clear)),
+                                     t.mine, t.clear, wb_dst)),
                 "rs decode");
         }
         return check_hip(ppfs_rs_generic_decode(d_raw, d_data, d_status, d_spill, nblocks, c->rs_n, c->rs_t2,
@@ -2206,6 +2218,9 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
         (void)hipGetLastError();
         img_dev = nullptr;
     }
+    // RS with 2t <= 8 into such an image: the decode kernel itself stores its corrections there
+    // (rs_wb_direct), so no codeword copy before it and no patch kernel after it
+    const bool wb_direct = img_dev && rs_wb_direct(c);
     // predictor: the last drained chunk changed many codewords -> fetch the next ones eagerly
     // (queued behind the kernel, as encode does) instead of after the status has landed.  It starts
     // where the context's previous call left it: the first kSlots chunks are queued before any has
@@ -2396,7 +2411,7 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
             HIP_TRY(dma_async(d + in_lo, h + in_lo, in_hi - in_lo, hipMemcpyHostToDevice, s), "H2D");
         }
         // patch lists for the big chunks (the small-batch path takes its whole staging span back)
-        const bool patch_now = S && (direct || nb * (c->raw + c->data) > (64u << 10));
+        const bool patch_now = S && !wb_direct && (direct || nb * (c->raw + c->data) > (64u << 10));
         if (patch_now) // the codewords as they came, for the patch list after the decode (on the input
             // stream, which a decode leaves half idle, not ahead of the kernel on the output stream)
             HIP_TRY(ppfs_copy_launch(d + L.orig, d + L.raw, nb * c->raw, s_in), "orig copy");
@@ -2411,16 +2426,23 @@ static int host_run_chunks(ppfs_ecc_ctx* c, HostOp op, const uint8_t* data_in, u
             r = ppfs_ecc_write_device(c, d + L.data, d + L.raw, d + L.status, nb, s);
             break;
         case OP_DECODE:
-            r = ppfs_ecc_decode_device(c, d + L.raw, data_out ? d + L.data : nullptr, d + L.status, nb, write_back,
-                spill ? d + L.spill : nullptr, s);
+            if (wb_direct)
+                r = queued(c,
+                    ppfs_ecc_decode_device_impl(c, d + L.raw, data_out ? d + L.data : nullptr, d + L.status, nb, write_back,
+                        nullptr, ordered(c, nb, s), img_dev + b0 * c->raw),
+                    nb, s, "decode (async)");
+            else
+                r = ppfs_ecc_decode_device(c, d + L.raw, data_out ? d + L.data : nullptr, d + L.status, nb, write_back,
+                    spill ? d + L.spill : nullptr, s);
             break;
         }
         if (r)
             return r;
         // outputs device -> pinned staging (or straight to page-locked caller buffers)
-        const bool want_raw = op == OP_ENCODE || op == OP_WRITE || (lazy_raw && eager && !patch_now);
+        const bool want_raw = op == OP_ENCODE || op == OP_WRITE || (lazy_raw && eager && !patch_now && !wb_direct);
         patched[slot] = patch_now && !img_dev;
-        landed[slot] = patch_now && img_dev; // the write-back goes straight into the caller's image
+        // the write-back goes straight into the caller's image (the patch kernel's, or the decode's own)
+        landed[slot] = (patch_now && img_dev) || wb_direct;
         const bool want_data = op == OP_DECODE && data_out;
         const bool want_st = (status || lazy_raw) && op != OP_ENCODE;
         if (!direct && nb * (c->raw + c->data) <= (64u << 10)) {

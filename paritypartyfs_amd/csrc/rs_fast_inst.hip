@@ -115,21 +115,28 @@ extern "C" const char* PPFS_CAT(ppfs_rs_fast_path_t, PPFS_T2)()
 #endif
 }
 
+// wb_dst: where the write-backs go (null: the codewords in place; 2t <= 8 only: api.cpp's host path
+// passes the page-locked caller image, mapped into the device)
 extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb,
-    const uint8_t* tab, int wb, hipStream_t s, [[maybe_unused]] uint32_t* ctr, [[maybe_unused]] uint32_t* ctr_clear)
+    const uint8_t* tab, int wb, hipStream_t s, [[maybe_unused]] uint32_t* ctr, [[maybe_unused]] uint32_t* ctr_clear,
+    [[maybe_unused]] uint8_t* wb_dst)
 {
 #if PPFS_T2 <= 8
     if (ctr && ctr_clear)
         PPFS_LAUNCH((wg::rs_wg_decode_tk_kernel<PPFS_T2, DEC_WPC, TK_NTST>), dim3(rs_tile_grid(nb, DEC_WPC)), dim3(256), 0, s,
-            r, d, st, nb, tab, wb, ctr, ctr_clear);
+            r, d, st, nb, tab, wb, ctr, ctr_clear, wb_dst);
     else
         PPFS_LAUNCH((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC, 7, 1>), dim3(rs_tile_grid(nb, DEC_WPC)),
-            dim3(256), 0, s, r, d, st, nb, tab, wb);
+            dim3(256), 0, s, r, d, st, nb, tab, wb, wb_dst);
 #elif PPFS_T2 == 32
+    if (wb_dst)
+        return hipErrorInvalidValue;
     PPFS_LAUNCH((bs::rs_bs_decode_kernel<PPFS_T2, BS_DEC_NW, BS_DEC_NBUF, 1, BS_DEC_TLDS>),
         dim3(rs_tile_grid(nb, 1, bs::TBW * BS_DEC_NW)), dim3(64 * BS_DEC_NW), 0, s, r, d, st, nb, tab, wb,
         ctr, ctr_clear);
 #else
+    if (wb_dst)
+        return hipErrorInvalidValue;
     PPFS_LAUNCH(rs255_decode_kernel<PPFS_T2>, dim3(rs_grid(nb)), dim3(256), 0, s, r, d, st, nb, tab, wb);
 #endif
     return hipGetLastError();

@@ -243,7 +243,7 @@ using namespace ppfs;
     extern "C" hipError_t ppfs_rs_fast_encode_t##T(const uint8_t*, uint8_t*, uint64_t, const uint8_t*, hipStream_t,   \
         uint32_t*, uint32_t*);                                                                                         \
     extern "C" hipError_t ppfs_rs_fast_decode_t##T(uint8_t*, uint8_t*, uint8_t*, uint64_t, const uint8_t*, int,       \
-        hipStream_t, uint32_t*, uint32_t*);
+        hipStream_t, uint32_t*, uint32_t*, uint8_t*);
 PPFS_RS_CASES(X)
 #undef X
 
@@ -302,12 +302,12 @@ extern "C" const char* ppfs_rs_fast_path(int t2)
 }
 
 extern "C" hipError_t ppfs_rs_fast_decode(int t2, uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb,
-    const uint8_t* tab, int wb, hipStream_t s, uint32_t* ctr, uint32_t* ctr_clear)
+    const uint8_t* tab, int wb, hipStream_t s, uint32_t* ctr, uint32_t* ctr_clear, uint8_t* wb_dst)
 {
     switch (t2) {
 #define X(T)                                                                                                           \
     case T:                                                                                                            \
-        return ppfs_rs_fast_decode_t##T(r, d, st, nb, tab, wb, s, ctr, ctr_clear);
+        return ppfs_rs_fast_decode_t##T(r, d, st, nb, tab, wb, s, ctr, ctr_clear, wb_dst);
         PPFS_RS_CASES(X)
 #undef X
     default:

@@ -698,7 +698,8 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_kernel(const uint8_t* _
 // emission (else a plain 16-byte copy), bit 2 = correction phase
 template <int T2, int NBUF = 2, int WPC = 3, int MODE = 7, int NTST = 1>
 __global__ __launch_bounds__(256, WPC) void rs_wg_decode_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
-    uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables, int write_back)
+    uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables, int write_back,
+    uint8_t* __restrict__ raw_wb)
 {
     using L = RsWgLayout<T2>;
     using D = Lds<T2, true, NBUF>;
@@ -711,6 +712,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_kernel(uint8_t* __restr
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = wave_id();
     const uint32_t row = lane_row(lane);
     const bool wb = write_back != 0, want = data != nullptr;
+    uint8_t* const wbp = raw_wb ? raw_wb : raw; // write-back target (rs_wg_tk.hpp rs_wg_decode_tk_kernel)
     for (uint32_t p = tid; p < (uint32_t)D::TBL / 16; p += NTHR)
         *(uint4*)(lds + 16 * p) = *(const uint4*)(tables + 16 * p);
     if (tid < 128)
@@ -752,7 +754,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_kernel(uint8_t* __restr
             phase_remainder<T2, 255>(lds, buf, par, wave, row);
         barrier_lds(); // B: remainders complete
         if ((MODE & 4) && wave == 0) {
-            const uint32_t st = phase_correct<T2>(lds, buf, par, row, true, raw, t * TB + row, wb, nblocks * 255u);
+            const uint32_t st = phase_correct<T2>(lds, buf, par, row, true, wbp, t * TB + row, wb, nblocks * 255u);
             if (status && PPFS_DBG_OK(status + t * TB + row, 1, status, nblocks))
                 status[t * TB + row] = (uint8_t)st;
         }
@@ -816,7 +818,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_kernel(uint8_t* __restr
         barrier_lds();
         if (wave == 0) {
             const bool valid = row < nb;
-            const uint32_t st = phase_correct<T2>(lds, buf, par, row, valid, raw, t * TB + row, wb, nblocks * 255u);
+            const uint32_t st = phase_correct<T2>(lds, buf, par, row, valid, wbp, t * TB + row, wb, nblocks * 255u);
             if (status && valid && PPFS_DBG_OK(status + t * TB + row, 1, status, nblocks))
                 status[t * TB + row] = (uint8_t)st;
         }

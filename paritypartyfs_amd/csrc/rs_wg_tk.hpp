@@ -400,7 +400,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_encode_tk_kernel(const uint8_t
 template <int T2, int WPC = 3, int NTST = 1>
 __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __restrict__ raw, uint8_t* __restrict__ data,
     uint8_t* __restrict__ status, uint64_t nblocks, const uint8_t* __restrict__ tables, int write_back,
-    uint32_t* __restrict__ ctr, uint32_t* __restrict__ ctr_clear)
+    uint32_t* __restrict__ ctr, uint32_t* __restrict__ ctr_clear, uint8_t* __restrict__ raw_wb)
 {
     constexpr int NBUF = 2;
     using L = RsWgLayout<T2>;
@@ -418,6 +418,9 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
     const bool dmaw = wave != 0, tk_lane = wave == 0 && lane == 0;
     const uint32_t row = lane_row(lane);
     const bool wb = write_back != 0, want = data != nullptr;
+    // write-back target: the codewords in place, or (raw_wb, the host path's page-locked caller image
+    // mapped into the device) the caller's image directly
+    uint8_t* const wbp = raw_wb ? raw_wb : raw;
     const uint64_t nfull = nblocks / TB, ntiles = (nblocks + TB - 1) / TB;
     const TkGeom g = tk_geom();
     uint32_t* const my_ctr = ctr + 32u * g.xc;
@@ -472,7 +475,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         __builtin_amdgcn_s_setprio(2);
         PPFS_TK_MARK(3);
         if (wave == 0) {
-            const uint32_t st_tile = phase_correct<T2>(lds, buf, par, row, true, raw, q0 * TB + row, wb, nblocks * 255u);
+            const uint32_t st_tile = phase_correct<T2>(lds, buf, par, row, true, wbp, q0 * TB + row, wb, nblocks * 255u);
             if (status && PPFS_DBG_OK(status + q0 * TB + row, 1, status, nblocks))
                 status[q0 * TB + row] = (uint8_t)st_tile;
         }
@@ -516,7 +519,7 @@ __global__ __launch_bounds__(256, WPC) void rs_wg_decode_tk_kernel(uint8_t* __re
         barrier_lds();
         if (wave == 0) {
             const bool valid = row < nb;
-            const uint32_t st = phase_correct<T2>(lds, buf, par, row, valid, raw, t * TB + row, wb, nblocks * 255u);
+            const uint32_t st = phase_correct<T2>(lds, buf, par, row, valid, wbp, t * TB + row, wb, nblocks * 255u);
             if (status && valid && PPFS_DBG_OK(status + t * TB + row, 1, status, nblocks))
                 status[t * TB + row] = (uint8_t)st;
         }

@@ -326,7 +326,8 @@ extern "C" const char* PPFS_CAT(ppfs_rs_fast_path_t, PPFS_T2)()
 }
 
 extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8_t* d, uint8_t* st, uint64_t nb,
-    const uint8_t* tab, int wb, hipStream_t s, [[maybe_unused]] uint32_t* ctr, [[maybe_unused]] uint32_t* ctr_clear)
+    const uint8_t* tab, int wb, hipStream_t s, [[maybe_unused]] uint32_t* ctr, [[maybe_unused]] uint32_t* ctr_clear,
+    [[maybe_unused]] uint8_t* wb_dst)
 {
 #if PPFS_T2 <= 8
 #if PPFS_WG_RP
@@ -339,13 +340,13 @@ extern "C" hipError_t PPFS_CAT(ppfs_rs_fast_decode_t, PPFS_T2)(uint8_t* r, uint8
 #else
     if ((PPFS_WG_TK & 2) && ctr && PPFS_DEC_MODE == 7 && !DEC_FULL && DEC_NBUF == 2 && DEC_WPC == 3 && !(PPFS_WG_W1 & 2))
         hipLaunchKernelGGL((wg::rs_wg_decode_tk_kernel<PPFS_T2, 3, PPFS_DEC_NTST>), dim3(rs_tile_grid(nb, 3)), dim3(256), 0, s,
-            r, d, st, nb, tab, wb, ctr, ctr_clear);
+            r, d, st, nb, tab, wb, ctr, ctr_clear, wb_dst);
     else if constexpr (PPFS_WG_W1 & 2)
         hipLaunchKernelGGL((w1::rs_w1_decode_kernel<PPFS_T2, PPFS_W1_DEC_NW, PPFS_W1_DEC_NBUF, PPFS_DEC_NTST>),
             dim3(rs_tile_grid(nb, 1, w1::TB * PPFS_W1_DEC_NW)), dim3(64 * PPFS_W1_DEC_NW), 0, s, r, d, st, nb, tab, wb);
     else
     hipLaunchKernelGGL((wg::rs_wg_decode_kernel<PPFS_T2, DEC_NBUF, DEC_WPC, PPFS_DEC_MODE, PPFS_DEC_NTST>), dim3(rs_tile_grid(nb, DEC_FULL ? (1 << 24) : DEC_WPC)), dim3(256),
-        0, s, r, d, st, nb, tab, wb);
+        0, s, r, d, st, nb, tab, wb, wb_dst);
 #endif
 #elif PPFS_T2 > 16
     if constexpr (PAIR_BS)

@@ -100,7 +100,7 @@ int main()
             se + si + sd, nb * 504.0 / se / 1e3, nb * 504.0 / sd / 1e3);
     };
 #define ENC(NB, W, M, ...) [&] { hipLaunchKernelGGL((wg::rs_wg_encode_kernel<6, NB, W, M, ##__VA_ARGS__>), dim3(W * cus), dim3(256), 0, 0, d, cw, nb, tb); }
-#define DEC(NB, W, M, ...) [&] { hipLaunchKernelGGL((wg::rs_wg_decode_kernel<6, NB, W, M, ##__VA_ARGS__>), dim3(W * cus), dim3(256), 0, 0, cw, out, st, nb, tb, 1); }
+#define DEC(NB, W, M, ...) [&] { hipLaunchKernelGGL((wg::rs_wg_decode_kernel<6, NB, W, M, ##__VA_ARGS__>), dim3(W * cus), dim3(256), 0, 0, cw, out, st, nb, tb, 1, (uint8_t*)nullptr); }
     {
         // precomputed wrong bytes (the bench's store-only injection)
         ENC(2, 4, 3)();

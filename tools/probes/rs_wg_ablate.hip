@@ -68,7 +68,7 @@ int main()
     snprintf(nm, sizeof nm, "decode nbuf%d wpc%d MODE%d", NBUF, WPC, M);                                           \
     rep(nm, timeit([&] {                                                                                             \
         hipLaunchKernelGGL((wg::rs_wg_decode_kernel<6, NBUF, WPC, M>), dim3(WPC * cus), dim3(256), 0, 0, bad, out, st, \
-            nb, tb, 0);                                                                                              \
+            nb, tb, 0, nullptr);                                                                                     \
     }));
     for (int rnd = 0; rnd < 3; ++rnd) {
         printf("-- round %d\n", rnd);
@@ -79,7 +79,7 @@ int main()
     D(2, 3, 3) D(2, 3, 5) D(2, 3, 6) D(2, 3, 0) D(1, 4, 3) D(1, 4, 5) D(1, 4, 6)
     // correctness spot check of the full decode
     hipMemcpy(bad, cw.data(), cw.size(), hipMemcpyHostToDevice);
-    hipLaunchKernelGGL((wg::rs_wg_decode_kernel<6, 2, 3, 7>), dim3(3 * cus), dim3(256), 0, 0, bad, out, st, nb, tb, 1);
+    hipLaunchKernelGGL((wg::rs_wg_decode_kernel<6, 2, 3, 7>), dim3(3 * cus), dim3(256), 0, 0, bad, out, st, nb, tb, 1, nullptr);
     std::vector<uint8_t> o(nb * 249);
     hipMemcpy(o.data(), out, o.size(), hipMemcpyDeviceToHost);
     printf("decode payload %s\n", o == h ? "matches" : "DIFFERS");
